@@ -1,0 +1,572 @@
+// Host engine + C ABI of libhcpairhmm.so (include/hc_pairhmm.h).
+//
+// Flow of one batch (the reference's computeLikelihoodsNative,
+// intel_pairhmm.hpp:115-152, split into plan and execute):
+//   plan     pack reads into 32-bit row words and haps into match tables,
+//            length-bin the pairs (W class by H, then stripes, then H), H2D
+//   execute  fp32 anti-diagonal kernel per W class -> raw f32 + rescue list
+//            fp64 kernel over the rescue list (raw < 1e-28f)      [device only]
+//   finish   D2H, then glibc log10f/log10 exactly as intel_pairhmm.hpp:137-143
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/hc_pairhmm.h"
+#include "kernels.hpp"
+#include "luts.hpp"
+
+using namespace hcphmm;
+
+namespace {
+
+thread_local std::string g_err;
+std::mutex g_mu;
+
+int fail(int code, const std::string& msg)
+{
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return fail(HC_PHMM_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct Engine {
+    bool ready = false;
+    int device = -1;
+    hipStream_t stream = nullptr;
+    float* lut_f = nullptr;
+    double* lut_d = nullptr;
+};
+Engine g_eng;
+
+// ConvertChar (pairhmm_common.h:26-44).
+inline int base_code(uint8_t b)
+{
+    switch (b) {
+    case 'C': return 1;
+    case 'T': return 2;
+    case 'G': return 3;
+    case 'N': return 4;
+    default: return 0;
+    }
+}
+
+int ensure_init(int device)
+{
+    if (g_eng.ready) return HC_PHMM_OK;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return fail(HC_PHMM_ENODEV, "no HIP device visible");
+    int dev = device;
+    if (dev < 0) HIP_TRY(hipGetDevice(&dev));
+    if (dev >= n) return fail(HC_PHMM_ENODEV, "device ordinal out of range");
+    HIP_TRY(hipSetDevice(dev));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, dev));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(HC_PHMM_ENODEV, std::string("device is ") + prop.gcnArchName + ", need gfx950");
+    HIP_TRY(configure_kernels());
+    HIP_TRY(hipStreamCreateWithFlags(&g_eng.stream, hipStreamNonBlocking));
+    const Luts& L = luts();
+    HIP_TRY(hipMalloc(&g_eng.lut_f, sizeof(float) * kTableLen));
+    HIP_TRY(hipMalloc(&g_eng.lut_d, sizeof(double) * kTableLen));
+    HIP_TRY(hipMemcpy(g_eng.lut_f, L.dev_f.data(), sizeof(float) * kTableLen, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(g_eng.lut_d, L.dev_d.data(), sizeof(double) * kTableLen, hipMemcpyHostToDevice));
+    g_eng.device = dev;
+    g_eng.ready = true;
+    return HC_PHMM_OK;
+}
+
+template <typename F>
+void parallel_for(int64_t n, F&& f, int64_t grain = 4096)
+{
+    unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int64_t nt = std::min<int64_t>(std::min<int64_t>(hw, 16), (n + grain - 1) / grain);
+    if (nt <= 1) {
+        f(int64_t(0), n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const int64_t chunk = (n + nt - 1) / nt;
+    for (int64_t t = 0; t < nt; ++t) {
+        const int64_t b = t * chunk, e = std::min(n, b + chunk);
+        if (b < e) th.emplace_back([&, b, e] { f(b, e); });
+    }
+    for (auto& x : th) x.join();
+}
+
+struct ReadView {
+    int32_t len;
+    const uint8_t *bases, *q, *i, *d, *c;
+};
+struct HapView {
+    int32_t len;
+    const uint8_t* bases;
+};
+
+}  // namespace
+
+// --------------------------------------------------------------------------
+// Prepared batch.
+struct hc_phmm_batch {
+    int64_t n = 0;          // pairs
+    int64_t cells = 0;
+    int Hmax = 0;
+    struct Cls {
+        int W = 16;
+        int n = 0;
+        int ring_len = 0;
+        int* d_order = nullptr;
+    } cls[2];
+    PairDesc* d_pairs = nullptr;
+    uint32_t* d_rows = nullptr;
+    uint32_t* d_hapw = nullptr;
+    float* d_raw32 = nullptr;
+    double* d_raw64 = nullptr;
+    uint8_t* d_flag = nullptr;
+    int* d_list = nullptr;
+    int* d_count = nullptr;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    hipStream_t last_stream = nullptr;
+    int64_t launch_waves = 0;
+    bool ran = false;
+};
+
+namespace {
+
+constexpr int kW64Threshold = 768;   // H above this -> one pair per wave (W = 64)
+
+void free_batch(hc_phmm_batch* b)
+{
+    if (!b) return;
+    for (auto& c : b->cls) (void)hipFree(c.d_order);
+    (void)hipFree(b->d_pairs);
+    (void)hipFree(b->d_rows);
+    (void)hipFree(b->d_hapw);
+    (void)hipFree(b->d_raw32);
+    (void)hipFree(b->d_raw64);
+    (void)hipFree(b->d_flag);
+    (void)hipFree(b->d_list);
+    (void)hipFree(b->d_count);
+    for (auto& e : b->ev)
+        if (e) (void)hipEventDestroy(e);
+    delete b;
+}
+
+template <typename T>
+int dev_upload(T** dst, const T* src, size_t count)
+{
+    const size_t bytes = sizeof(T) * std::max<size_t>(count, 1);
+    HIP_TRY(hipMalloc(dst, bytes));
+    if (count) HIP_TRY(hipMemcpy(*dst, src, sizeof(T) * count, hipMemcpyHostToDevice));
+    return HC_PHMM_OK;
+}
+
+// Pack reads/haps once each, pairs refer to them (cross product reuses both).
+int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
+         int64_t npairs, const int32_t* pr, const int32_t* ph, hc_phmm_batch** out)
+{
+    for (const auto& r : reads)
+        if (r.len <= 0 || r.len > HC_PHMM_MAX_READ_LEN || !r.bases || !r.q || !r.i || !r.d || !r.c)
+            return fail(HC_PHMM_EINVAL, "read with invalid length or null array");
+    for (const auto& h : haps)
+        if (h.len <= 0 || h.len > HC_PHMM_MAX_HAP_LEN || !h.bases)
+            return fail(HC_PHMM_EINVAL, "haplotype with invalid length (1.." +
+                                            std::to_string(HC_PHMM_MAX_HAP_LEN) + ") or null bases");
+    if (npairs > (int64_t(1) << 31) - 1) return fail(HC_PHMM_EINVAL, "too many pairs for one batch");
+
+    const int64_t nr = reads.size(), nh = haps.size();
+    std::vector<int64_t> row_off(nr + 1, 0), hap_off(nh + 1, 0);
+    for (int64_t r = 0; r < nr; ++r) row_off[r + 1] = row_off[r] + reads[r].len;
+    for (int64_t h = 0; h < nh; ++h) hap_off[h + 1] = hap_off[h] + hap_table_words(haps[h].len);
+    if (row_off[nr] > INT32_MAX || hap_off[nh] > INT32_MAX)
+        return fail(HC_PHMM_EINVAL, "batch too large (row or hap pool exceeds 2^31 words)");
+
+    std::vector<uint32_t> rows(row_off[nr] + 1);
+    parallel_for(nr, [&](int64_t b, int64_t e) {
+        for (int64_t r = b; r < e; ++r) {
+            const ReadView& v = reads[r];
+            uint32_t* o = rows.data() + row_off[r];
+            for (int k = 0; k < v.len; ++k)
+                o[k] = pack_row(v.q[k], v.i[k], v.d[k], v.c[k], base_code(v.bases[k]));
+        }
+    }, 256);
+    std::vector<uint32_t> hapw(hap_off[nh] + 1, 0u);
+    parallel_for(nh, [&](int64_t b, int64_t e) {
+        for (int64_t h = b; h < e; ++h) {
+            const HapView& v = haps[h];
+            uint32_t* t = hapw.data() + hap_off[h];
+            for (int j = 1; j <= v.len; ++j) {
+                const uint32_t bit = 0x80000000u >> ((j - 1) & 31);
+                uint32_t* row = t + (((j - 1) >> 5) + kHapLead) * 5;
+                const int hc = base_code(v.bases[j - 1]);
+                if (hc == 4) {
+                    for (int rc = 0; rc < 5; ++rc) row[rc] |= bit;
+                } else {
+                    row[hc] |= bit;
+                    row[4] |= bit;   // read 'N' matches every column
+                }
+            }
+        }
+    }, 256);
+
+    std::vector<PairDesc> pd(npairs);
+    int64_t cells = 0;
+    int Hmax = 0;
+    for (int64_t p = 0; p < npairs; ++p) {
+        const int r = pr[p], h = ph[p];
+        pd[p] = PairDesc{int(row_off[r]), reads[r].len, int(hap_off[h]), haps[h].len};
+        cells += int64_t(reads[r].len) * haps[h].len;
+        Hmax = std::max(Hmax, haps[h].len);
+    }
+
+    // Length binning: W class by H; inside a class sort by (stripes, H) descending
+    // so the G pairs sharing a wave have equal stripe counts and similar H, and the
+    // heaviest waves dispatch first.
+    std::vector<int> ord[2];
+    for (int64_t p = 0; p < npairs; ++p) ord[pd[p].w > kW64Threshold ? 1 : 0].push_back(int(p));
+    const int Wc[2] = {16, 64};
+    auto* b = new hc_phmm_batch();
+    b->n = npairs;
+    b->cells = cells;
+    b->Hmax = Hmax;
+    for (int c = 0; c < 2; ++c) {
+        const int W = Wc[c];
+        auto& o = ord[c];
+        std::stable_sort(o.begin(), o.end(), [&](int x, int y) {
+            const int sx = (pd[x].y + W - 1) / W, sy = (pd[y].y + W - 1) / W;
+            if (sx != sy) return sx > sy;
+            return pd[x].w > pd[y].w;
+        });
+        int hm = 0;
+        for (int p : o) hm = std::max(hm, pd[p].w);
+        b->cls[c].W = W;
+        b->cls[c].n = int(o.size());
+        b->cls[c].ring_len = hm + 2 * W + 16;
+    }
+
+    int rc = HC_PHMM_OK;
+    auto chk = [&](int r) { if (rc == HC_PHMM_OK) rc = r; };
+    chk(dev_upload(&b->d_pairs, pd.data(), pd.size()));
+    chk(dev_upload(&b->d_rows, rows.data(), rows.size()));
+    chk(dev_upload(&b->d_hapw, hapw.data(), hapw.size()));
+    for (int c = 0; c < 2; ++c) chk(dev_upload(&b->cls[c].d_order, ord[c].data(), ord[c].size()));
+    if (rc == HC_PHMM_OK) {
+        const size_t n1 = std::max<int64_t>(npairs, 1);
+        if (hipMalloc(&b->d_raw32, sizeof(float) * n1) != hipSuccess ||
+            hipMalloc(&b->d_raw64, sizeof(double) * n1) != hipSuccess ||
+            hipMalloc(&b->d_flag, n1) != hipSuccess ||
+            hipMalloc(&b->d_list, sizeof(int) * n1) != hipSuccess ||
+            hipMalloc(&b->d_count, sizeof(int)) != hipSuccess)
+            chk(fail(HC_PHMM_ENOMEM, "device allocation failed"));
+    }
+    for (auto& e : b->ev)
+        if (rc == HC_PHMM_OK && hipEventCreate(&e) != hipSuccess) chk(fail(HC_PHMM_EHIP, "hipEventCreate"));
+    if (rc != HC_PHMM_OK) {
+        free_batch(b);
+        return rc;
+    }
+    *out = b;
+    return HC_PHMM_OK;
+}
+
+int run(hc_phmm_batch* b, hipStream_t s)
+{
+    if (!s) s = g_eng.stream;
+    b->last_stream = s;
+    b->launch_waves = 0;
+    HIP_TRY(hipEventRecord(b->ev[0], s));
+    HIP_TRY(hipMemsetAsync(b->d_count, 0, sizeof(int), s));
+    HIP_TRY(hipMemsetAsync(b->d_raw64, 0, sizeof(double) * std::max<int64_t>(b->n, 1), s));
+    for (auto& c : b->cls) {
+        if (c.n == 0) continue;
+        DiagArgs a{};
+        a.pairs = b->d_pairs;
+        a.order = c.d_order;
+        a.n_slots = c.n;
+        a.rows = b->d_rows;
+        a.hapw = b->d_hapw;
+        a.lut = g_eng.lut_f;
+        a.ring_len = c.ring_len;
+        a.raw_out = b->d_raw32;
+        a.rescue_flag = b->d_flag;
+        a.rescue_list = b->d_list;
+        a.rescue_count = b->d_count;
+        const int G = 64 / c.W;
+        const int grid = (c.n + G - 1) / G;
+        b->launch_waves += grid;
+        HIP_TRY(launch_diag_f32(c.W, a, grid, s));
+    }
+    HIP_TRY(hipEventRecord(b->ev[1], s));
+    if (b->n > 0) {
+        // fp64 rescue (intel_pairhmm.hpp:137-139): one pair per wave, grid-stride
+        // over the device-built list, so no host round trip for its length.
+        DiagArgs a{};
+        a.pairs = b->d_pairs;
+        a.order = b->d_list;
+        a.n_slots_dev = b->d_count;
+        a.rows = b->d_rows;
+        a.hapw = b->d_hapw;
+        a.lut = g_eng.lut_d;
+        a.ring_len = b->Hmax + 2 * 64 + 16;
+        a.raw_out = b->d_raw64;
+        const int grid = int(std::min<int64_t>(b->n, 2048));
+        HIP_TRY(launch_diag_f64(64, a, grid, s));
+    }
+    HIP_TRY(hipEventRecord(b->ev[2], s));
+    b->ran = true;
+    return HC_PHMM_OK;
+}
+
+int results(hc_phmm_batch* b, double* loglik, float* raw32, double* raw64, uint8_t* resc)
+{
+    if (!b->ran) return fail(HC_PHMM_EINVAL, "batch has not been run");
+    HIP_TRY(hipStreamSynchronize(b->last_stream));
+    const int64_t n = b->n;
+    if (n == 0) return HC_PHMM_OK;
+    std::vector<float> f(n);
+    std::vector<double> d(n);
+    std::vector<uint8_t> fl(n);
+    HIP_TRY(hipMemcpy(f.data(), b->d_raw32, sizeof(float) * n, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(d.data(), b->d_raw64, sizeof(double) * n, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(fl.data(), b->d_flag, n, hipMemcpyDeviceToHost));
+    if (raw32) std::memcpy(raw32, f.data(), sizeof(float) * n);
+    if (raw64) std::memcpy(raw64, d.data(), sizeof(double) * n);
+    if (resc) std::memcpy(resc, fl.data(), n);
+    if (loglik) {
+        const Luts& L = luts();
+        const float l10f = L.log10_init_f;
+        const double l10d = L.log10_init_d;
+        parallel_for(n, [&](int64_t lo, int64_t hi) {
+            for (int64_t p = lo; p < hi; ++p)
+                loglik[p] = fl[p] ? std::log10(d[p]) - l10d : double(std::log10(f[p]) - l10f);
+        }, 1 << 16);
+    }
+    return HC_PHMM_OK;
+}
+
+int run_sync(hc_phmm_batch* b, double* loglik, float* raw32, double* raw64, uint8_t* resc)
+{
+    int rc = run(b, nullptr);
+    if (rc == HC_PHMM_OK) rc = results(b, loglik, raw32, raw64, resc);
+    return rc;
+}
+
+int flat_views(int64_t n, const int64_t* read_off, const int32_t* R, const int64_t* hap_off,
+               const int32_t* H, const uint8_t* rs, const uint8_t* q, const uint8_t* ins,
+               const uint8_t* del, const uint8_t* gcp, const uint8_t* hap,
+               std::vector<ReadView>& rv, std::vector<HapView>& hv, std::vector<int32_t>& idx)
+{
+    if (n < 0) return fail(HC_PHMM_EINVAL, "negative pair count");
+    if (n > 0 && (!read_off || !R || !hap_off || !H || !rs || !q || !ins || !del || !gcp || !hap))
+        return fail(HC_PHMM_EINVAL, "null input array");
+    rv.resize(n);
+    hv.resize(n);
+    idx.resize(n);
+    for (int64_t p = 0; p < n; ++p) {
+        const int64_t o = read_off[p];
+        rv[p] = ReadView{R[p], rs + o, q + o, ins + o, del + o, gcp + o};
+        hv[p] = HapView{H[p], hap + hap_off[p]};
+        idx[p] = int32_t(p);
+    }
+    return HC_PHMM_OK;
+}
+
+}  // namespace
+
+// --------------------------------------------------------------------------
+// C ABI
+extern "C" {
+
+int hc_phmm_version(void) { return 100; }
+
+const char* hc_phmm_last_error(void) { return g_err.c_str(); }
+
+int hc_phmm_init(uint32_t /*flags*/, int device)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    return ensure_init(device);
+}
+
+int hc_phmm_shutdown(void)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_eng.ready) return HC_PHMM_OK;
+    (void)hipFree(g_eng.lut_f);
+    (void)hipFree(g_eng.lut_d);
+    (void)hipStreamDestroy(g_eng.stream);
+    g_eng = Engine{};
+    return HC_PHMM_OK;
+}
+
+int hc_phmm_get_luts(float* pf, double* pd, float* mf, double* md)
+{
+    const Luts& L = luts();
+    if (pf) std::memcpy(pf, L.ph2pr_f, sizeof(L.ph2pr_f));
+    if (pd) std::memcpy(pd, L.ph2pr_d, sizeof(L.ph2pr_d));
+    if (mf) std::memcpy(mf, L.mm_f.data(), sizeof(float) * kMMEntries);
+    if (md) std::memcpy(md, L.mm_d.data(), sizeof(double) * kMMEntries);
+    return HC_PHMM_OK;
+}
+
+int hc_phmm_pairs_flat(int64_t n, const int64_t* read_off, const int32_t* R, const int64_t* hap_off,
+                       const int32_t* H, const uint8_t* rs, const uint8_t* q, const uint8_t* ins,
+                       const uint8_t* del, const uint8_t* gcp, const uint8_t* hap, double* loglik,
+                       float* raw_f32, double* raw_f64, uint8_t* rescued)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    int rc = ensure_init(-1);
+    if (rc) return rc;
+    if (n == 0) return HC_PHMM_OK;
+    std::vector<ReadView> rv;
+    std::vector<HapView> hv;
+    std::vector<int32_t> idx;
+    rc = flat_views(n, read_off, R, hap_off, H, rs, q, ins, del, gcp, hap, rv, hv, idx);
+    if (rc) return rc;
+    hc_phmm_batch* b = nullptr;
+    rc = plan(rv, hv, n, idx.data(), idx.data(), &b);
+    if (rc) return rc;
+    rc = run_sync(b, loglik, raw_f32, raw_f64, rescued);
+    free_batch(b);
+    return rc;
+}
+
+int hc_phmm_cross(const hc_phmm_read* reads, int32_t n_reads, const hc_phmm_hap* haps,
+                  int32_t n_haps, double* out)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (n_reads < 0 || n_haps < 0) return fail(HC_PHMM_EINVAL, "negative count");
+    if (n_reads == 0 || n_haps == 0) return HC_PHMM_OK;
+    if (!reads || !haps || !out) return fail(HC_PHMM_EINVAL, "null argument");
+    int rc = ensure_init(-1);
+    if (rc) return rc;
+    std::vector<ReadView> rv(n_reads);
+    std::vector<HapView> hv(n_haps);
+    for (int r = 0; r < n_reads; ++r)
+        rv[r] = ReadView{reads[r].length, (const uint8_t*)reads[r].bases, (const uint8_t*)reads[r].q,
+                         (const uint8_t*)reads[r].i, (const uint8_t*)reads[r].d, (const uint8_t*)reads[r].c};
+    for (int h = 0; h < n_haps; ++h) hv[h] = HapView{haps[h].length, (const uint8_t*)haps[h].bases};
+    const int64_t np = int64_t(n_reads) * n_haps;
+    std::vector<int32_t> pr(np), ph(np);
+    for (int64_t p = 0; p < np; ++p) {
+        pr[p] = int32_t(p / n_haps);   // read-major, intel_pairhmm.hpp:131-132
+        ph[p] = int32_t(p % n_haps);
+    }
+    hc_phmm_batch* b = nullptr;
+    rc = plan(rv, hv, np, pr.data(), ph.data(), &b);
+    if (rc) return rc;
+    rc = run_sync(b, out, nullptr, nullptr, nullptr);
+    free_batch(b);
+    return rc;
+}
+
+int hc_phmm_compute_likelihoods(const hc_phmm_read* reads, int32_t n_reads, const hc_phmm_hap* haps,
+                                int32_t n_haps, double* out, uint8_t* keep, int32_t* n_kept)
+{
+    int rc = hc_phmm_cross(reads, n_reads, haps, n_haps, out);
+    if (rc) return rc;
+    if (n_reads > 0 && (!keep || !n_kept)) return fail(HC_PHMM_EINVAL, "null keep/n_kept");
+    int kept = 0;
+    // normalize_likelihoods_and_filter_poorly_modeled_reads, intel_pairhmm.hpp:24-46
+    for (int r = 0; r < n_reads; ++r) {
+        double* row = out + size_t(r) * n_haps;
+        double best = n_haps ? row[0] : -INFINITY;
+        for (int h = 1; h < n_haps; ++h)
+            if (best < row[h]) best = row[h];
+        const double cap = best + -4.5;
+        for (int h = 0; h < n_haps; ++h)
+            if (row[h] < cap) row[h] = cap;
+        const double thr = std::min(2.0, std::ceil(double(reads[r].length) * 0.02)) * -4.0;
+        keep[r] = !(best < thr);
+        kept += keep[r];
+    }
+    if (n_kept) *n_kept = kept;
+    return HC_PHMM_OK;
+}
+
+int hc_phmm_batch_create(int64_t n, const int64_t* read_off, const int32_t* R, const int64_t* hap_off,
+                         const int32_t* H, const uint8_t* rs, const uint8_t* q, const uint8_t* ins,
+                         const uint8_t* del, const uint8_t* gcp, const uint8_t* hap, hc_phmm_batch** out)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!out) return fail(HC_PHMM_EINVAL, "null out");
+    int rc = ensure_init(-1);
+    if (rc) return rc;
+    std::vector<ReadView> rv;
+    std::vector<HapView> hv;
+    std::vector<int32_t> idx;
+    rc = flat_views(n, read_off, R, hap_off, H, rs, q, ins, del, gcp, hap, rv, hv, idx);
+    if (rc) return rc;
+    return plan(rv, hv, n, idx.data(), idx.data(), out);
+}
+
+int hc_phmm_batch_run(hc_phmm_batch* b, void* stream)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!b) return fail(HC_PHMM_EINVAL, "null batch");
+    if (!g_eng.ready) return fail(HC_PHMM_ENODEV, "not initialised");
+    return run(b, static_cast<hipStream_t>(stream));
+}
+
+int hc_phmm_batch_results(hc_phmm_batch* b, double* loglik, float* raw_f32, double* raw_f64,
+                          uint8_t* rescued)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!b) return fail(HC_PHMM_EINVAL, "null batch");
+    return results(b, loglik, raw_f32, raw_f64, rescued);
+}
+
+int hc_phmm_batch_device_results(hc_phmm_batch* b, void** raw_f32, void** raw_f64, void** rescued)
+{
+    if (!b) return fail(HC_PHMM_EINVAL, "null batch");
+    if (raw_f32) *raw_f32 = b->d_raw32;
+    if (raw_f64) *raw_f64 = b->d_raw64;
+    if (rescued) *rescued = b->d_flag;
+    return HC_PHMM_OK;
+}
+
+int hc_phmm_batch_stats(hc_phmm_batch* b, hc_phmm_stats* st)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!b || !st) return fail(HC_PHMM_EINVAL, "null argument");
+    std::memset(st, 0, sizeof(*st));
+    st->n_pairs = b->n;
+    st->cells = b->cells;
+    st->n_launch_waves = b->launch_waves;
+    if (b->ran) {
+        HIP_TRY(hipStreamSynchronize(b->last_stream));
+        float a = 0, c = 0;
+        HIP_TRY(hipEventElapsedTime(&a, b->ev[0], b->ev[1]));
+        HIP_TRY(hipEventElapsedTime(&c, b->ev[1], b->ev[2]));
+        st->kernel_ms_f32 = a;
+        st->kernel_ms_f64 = c;
+        st->run_ms = double(a) + double(c);
+        int cnt = 0;
+        HIP_TRY(hipMemcpy(&cnt, b->d_count, sizeof(int), hipMemcpyDeviceToHost));
+        st->n_rescued = cnt;
+    }
+    return HC_PHMM_OK;
+}
+
+int hc_phmm_batch_destroy(hc_phmm_batch* b)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    free_batch(b);
+    return HC_PHMM_OK;
+}
+
+}  // extern "C"

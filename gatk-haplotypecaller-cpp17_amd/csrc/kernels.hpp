@@ -1,0 +1,55 @@
+// Device-side layout shared by the HIP kernels and the host engine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace hcphmm {
+
+// One row of a read, packed into 32 bits (built on the host, engine.cpp):
+//   bits  0- 6  q  (base quality byte & 127)
+//   bits  7-13  i  (insertion GOP byte & 127)
+//   bits 14-20  d  (deletion GOP byte & 127)
+//   bits 21-27  c  (gap continuation byte & 127)
+//   bits 28-30  read base code, ConvertChar (pairhmm_common.h:26-44): A0 C1 T2 G3 N4
+__host__ __device__ inline uint32_t pack_row(int q, int i, int d, int c, int code)
+{
+    return uint32_t(q & 127) | (uint32_t(i & 127) << 7) | (uint32_t(d & 127) << 14) |
+           (uint32_t(c & 127) << 21) | (uint32_t(code) << 28);
+}
+
+// Haplotype match table: for hap of length H, nw = ceil(H/32) data words,
+// stored as (nw + kHapPadWords) rows of 5 uint32 — row (w + kHapLead) holds,
+// for each read code rc, the bits of columns 32w+1 .. 32w+32 (MSB first) whose
+// hap base matches rc: equal code, or hap 'N' (matches every rc), or rc = 'N'
+// (matches every column). This is the reference's precompute_masks
+// (avx-pairhmm-template.h:3-35) laid out for per-lane windows. kHapLead zero
+// rows precede the data (columns <= 0), one zero row follows.
+constexpr int kHapLead = 2;
+constexpr int kHapPadWords = 3;
+inline int hap_table_words(int H) { return ((H + 31) / 32 + kHapPadWords) * 5; }
+
+// Per pair descriptor: {row offset into rows[], R, word offset into hapw[], H}.
+using PairDesc = int4;
+
+struct DiagArgs {
+    const PairDesc* pairs;
+    const int* order;         // slot -> pair id (caller order)
+    int n_slots;              // number of slots when n_slots_dev == nullptr
+    const int* n_slots_dev;   // device-side slot count (rescue list)
+    const uint32_t* rows;
+    const uint32_t* hapw;
+    const void* lut;          // float or double table, luts.hpp layout
+    int ring_len;             // ring entries per pair group (LDS)
+    void* raw_out;            // float[n_pairs] or double[n_pairs], by pair id
+    uint8_t* rescue_flag;     // fp32 pass: 1 if raw < 1e-28f (by pair id)
+    int* rescue_list;         // fp32 pass: appended pair ids
+    int* rescue_count;        // fp32 pass: append counter
+};
+
+// Launchers (kernels.hip). W = lanes per pair: 16, 32 or 64.
+hipError_t launch_diag_f32(int W, const DiagArgs& a, int grid, hipStream_t s);
+hipError_t launch_diag_f64(int W, const DiagArgs& a, int grid, hipStream_t s);
+size_t diag_lds_bytes(int W, int ring_len, bool f64);
+hipError_t configure_kernels();   // raise the dynamic-LDS limit once
+
+}  // namespace hcphmm

@@ -1,0 +1,228 @@
+"""Python mirror of the MI355X PairHMM engine's C ABI (include/hc_pairhmm.h).
+
+Thin ctypes binding over the in-tree ``libhcpairhmm.so``; the compute always
+runs through that library's HIP kernels. There is no Python or CPU fallback:
+if the library is missing, or no gfx950 device is usable, calls raise
+``PairHMMError``.
+
+Names follow the reference's PairHMM interface
+(src/haplotypecaller/pairhmm/intel_pairhmm.hpp):
+
+* :func:`compute_likelihoods` — IntelPairHMM::compute_likelihoods (:48-56):
+  reads x haps log10 likelihoods, normalised, poorly modelled reads removed.
+* :func:`cross` — computeLikelihoodsNative (:115-152) without normalisation.
+* :func:`pairs` — the same per-pair computation over independent pairs.
+* :class:`Batch` — plan (pack + upload) once, run the device pass many times.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libhcpairhmm.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "hc_pairhmm.h")
+
+OK, EINVAL, ENODEV, EHIP, ENOMEM = 0, -1, -2, -3, -4
+
+_u8p = C.POINTER(C.c_uint8)
+_i32p = C.POINTER(C.c_int32)
+_i64p = C.POINTER(C.c_int64)
+_f32p = C.POINTER(C.c_float)
+_f64p = C.POINTER(C.c_double)
+
+
+class PairHMMError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"hc_phmm error {code}: {msg}")
+        self.code = code
+
+
+class Read(C.Structure):
+    """hc_phmm_read == shacc_pairhmm::Read (shacc_pairhmm.h:12-19)."""
+    _fields_ = [("length", C.c_int32), ("bases", C.c_char_p), ("q", C.c_char_p),
+                ("i", C.c_char_p), ("d", C.c_char_p), ("c", C.c_char_p)]
+
+
+class Hap(C.Structure):
+    """hc_phmm_hap == shacc_pairhmm::Haplotype (shacc_pairhmm.h:21-24)."""
+    _fields_ = [("length", C.c_int32), ("bases", C.c_char_p)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("n_pairs", C.c_int64), ("cells", C.c_int64), ("n_rescued", C.c_int64),
+                ("kernel_ms_f32", C.c_double), ("kernel_ms_f64", C.c_double),
+                ("run_ms", C.c_double), ("n_launch_waves", C.c_int64)]
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+_lib = None
+
+
+def lib():
+    """Load libhcpairhmm.so (raises if it was never built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise PairHMMError(ENODEV, f"{LIB_PATH} missing: run `make -C {HERE}` (no fallback path exists)")
+    L = C.CDLL(LIB_PATH)
+    L.hc_phmm_init.argtypes = [C.c_uint32, C.c_int]
+    L.hc_phmm_last_error.restype = C.c_char_p
+    flat = [C.c_int64, _i64p, _i32p, _i64p, _i32p] + [_u8p] * 6
+    L.hc_phmm_pairs_flat.argtypes = flat + [_f64p, _f32p, _f64p, _u8p]
+    L.hc_phmm_cross.argtypes = [C.POINTER(Read), C.c_int32, C.POINTER(Hap), C.c_int32, _f64p]
+    L.hc_phmm_compute_likelihoods.argtypes = [C.POINTER(Read), C.c_int32, C.POINTER(Hap), C.c_int32,
+                                              _f64p, _u8p, _i32p]
+    L.hc_phmm_batch_create.argtypes = flat + [C.POINTER(C.c_void_p)]
+    L.hc_phmm_batch_run.argtypes = [C.c_void_p, C.c_void_p]
+    L.hc_phmm_batch_results.argtypes = [C.c_void_p, _f64p, _f32p, _f64p, _u8p]
+    L.hc_phmm_batch_stats.argtypes = [C.c_void_p, C.POINTER(Stats)]
+    L.hc_phmm_batch_device_results.argtypes = [C.c_void_p] + [C.POINTER(C.c_void_p)] * 3
+    L.hc_phmm_batch_destroy.argtypes = [C.c_void_p]
+    L.hc_phmm_get_luts.argtypes = [_f32p, _f64p, _f32p, _f64p]
+    _lib = L
+    return L
+
+
+def declared_symbols(header: str = HEADER):
+    """Every function the C header declares (for the export test)."""
+    txt = open(header).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(hc_phmm_\w+)\s*\(", txt, re.M)))
+
+
+def _check(rc: int):
+    if rc != OK:
+        msg = lib().hc_phmm_last_error()
+        raise PairHMMError(rc, msg.decode() if msg else "")
+
+
+def _p(a, t):
+    return None if a is None else a.ctypes.data_as(t)
+
+
+def init(device: int = -1) -> None:
+    _check(lib().hc_phmm_init(0, device))
+
+
+def shutdown() -> None:
+    _check(lib().hc_phmm_shutdown())
+
+
+def get_luts():
+    out = dict(ph2pr_f=np.zeros(128, np.float32), ph2pr_d=np.zeros(128, np.float64),
+               mm_f=np.zeros(32640, np.float32), mm_d=np.zeros(32640, np.float64))
+    _check(lib().hc_phmm_get_luts(_p(out["ph2pr_f"], _f32p), _p(out["ph2pr_d"], _f64p),
+                                  _p(out["mm_f"], _f32p), _p(out["mm_d"], _f64p)))
+    return out
+
+
+def _flat_args(b):
+    arrs = dict(read_off=np.ascontiguousarray(b["read_off"], np.int64),
+                R=np.ascontiguousarray(b["R"], np.int32),
+                hap_off=np.ascontiguousarray(b["hap_off"], np.int64),
+                H=np.ascontiguousarray(b["H"], np.int32))
+    for k in ("rs", "q", "ins", "dels", "gcp", "hap"):
+        arrs[k] = np.ascontiguousarray(b[k], np.uint8)
+    args = [len(arrs["R"]), _p(arrs["read_off"], _i64p), _p(arrs["R"], _i32p),
+            _p(arrs["hap_off"], _i64p), _p(arrs["H"], _i32p)] + \
+           [_p(arrs[k], _u8p) for k in ("rs", "q", "ins", "dels", "gcp", "hap")]
+    return args, arrs
+
+
+def pairs(b):
+    """Independent pairs (flat batch dict, see workloads.py) -> dict of results."""
+    args, keep = _flat_args(b)
+    n = len(keep["R"])
+    out = dict(loglik=np.zeros(n, np.float64), raw_f32=np.zeros(n, np.float32),
+               raw_f64=np.zeros(n, np.float64), rescued=np.zeros(n, np.uint8))
+    _check(lib().hc_phmm_pairs_flat(*args, _p(out["loglik"], _f64p), _p(out["raw_f32"], _f32p),
+                                    _p(out["raw_f64"], _f64p), _p(out["rescued"], _u8p)))
+    return out
+
+
+def _structs(reads, haps):
+    """reads: list of (bases, q, i, d, c) bytes; haps: list of bytes."""
+    keep = []
+    ra = (Read * max(len(reads), 1))()
+    for k, r in enumerate(reads):
+        bases, q, i, d, c = r
+        keep.extend(r)
+        ra[k] = Read(len(bases), bases, q, i, d, c)
+    ha = (Hap * max(len(haps), 1))()
+    for k, h in enumerate(haps):
+        keep.append(h)
+        ha[k] = Hap(len(h), h)
+    return ra, ha, keep
+
+
+def cross(reads, haps):
+    """All reads x all haps -> (n_reads, n_haps) log10 likelihoods (unnormalised)."""
+    ra, ha, _keep = _structs(reads, haps)
+    out = np.zeros((len(reads), len(haps)), np.float64)
+    _check(lib().hc_phmm_cross(ra, len(reads), ha, len(haps), _p(out, _f64p)))
+    return out
+
+
+def compute_likelihoods(haps, reads):
+    """IntelPairHMM::compute_likelihoods(haplotypes, reads): returns (L, kept_reads)
+    where L has one row per surviving read (intel_pairhmm.hpp:48-56, 24-46)."""
+    ra, ha, _keep = _structs(reads, haps)
+    out = np.zeros((len(reads), len(haps)), np.float64)
+    keep = np.zeros(max(len(reads), 1), np.uint8)
+    nk = C.c_int32(0)
+    _check(lib().hc_phmm_compute_likelihoods(ra, len(reads), ha, len(haps), _p(out, _f64p),
+                                             _p(keep, _u8p), C.byref(nk)))
+    mask = keep[:len(reads)].astype(bool)
+    return out[mask], [r for r, k in zip(reads, mask) if k]
+
+
+class Batch:
+    """Prepared, device-resident batch: create (pack + H2D) once, run many times."""
+
+    def __init__(self, b):
+        args, self._arrs = _flat_args(b)
+        self.n = len(self._arrs["R"])
+        h = C.c_void_p()
+        _check(lib().hc_phmm_batch_create(*args, C.byref(h)))
+        self._h = h
+
+    def run(self, stream=None):
+        """Enqueue the device pass (asynchronous). stream: hipStream_t as int, or None."""
+        _check(lib().hc_phmm_batch_run(self._h, C.c_void_p(stream) if stream else None))
+
+    def results(self):
+        n = self.n
+        out = dict(loglik=np.zeros(n, np.float64), raw_f32=np.zeros(n, np.float32),
+                   raw_f64=np.zeros(n, np.float64), rescued=np.zeros(n, np.uint8))
+        _check(lib().hc_phmm_batch_results(self._h, _p(out["loglik"], _f64p), _p(out["raw_f32"], _f32p),
+                                           _p(out["raw_f64"], _f64p), _p(out["rescued"], _u8p)))
+        return out
+
+    def stats(self) -> Stats:
+        st = Stats()
+        _check(lib().hc_phmm_batch_stats(self._h, C.byref(st)))
+        return st
+
+    def device_results(self):
+        p = [C.c_void_p() for _ in range(3)]
+        _check(lib().hc_phmm_batch_device_results(self._h, *[C.byref(x) for x in p]))
+        return tuple(x.value for x in p)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().hc_phmm_batch_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,136 @@
+/*
+ * hc_pairhmm.h — C ABI of the MI355X PairHMM engine (libhcpairhmm.so).
+ *
+ * Drop-in for the PairHMM hot path of avis9ditiu/gatk-haplotypecaller-cpp17
+ * (paths below are relative to the reference's src/haplotypecaller/):
+ *
+ *   hc_phmm_compute_likelihoods  replaces IntelPairHMM::compute_likelihoods
+ *                                (pairhmm/intel_pairhmm.hpp:48-56), including the
+ *                                normalize/filter step (:24-46)
+ *   hc_phmm_cross                replaces computeLikelihoodsNative
+ *                                (pairhmm/intel_pairhmm.hpp:115-152): every read x
+ *                                every hap, fp32 kernel + fp64 rescue + log10
+ *   hc_phmm_pairs_flat           the same per-pair computation over an explicit
+ *                                list of independent (read, hap) pairs
+ *   hc_phmm_batch_*              the same split into plan (pack + H2D) and execute
+ *                                (device only) for device-resident batches
+ *   hc_phmm_read / hc_phmm_hap   field-for-field the accelerator hook structs
+ *                                shacc_pairhmm::Read / ::Haplotype
+ *                                (pairhmm/native/shacc_pairhmm.h:12-24)
+ *
+ * Value semantics are the reference's: bases are raw bytes (A C T G N, any other
+ * byte counts as A, N matches everything); q/i/d/c are raw quality bytes used
+ * `& 127` (no -33), exactly as compute_full_prob_avx{s,d} reads them
+ * (pairhmm/native/avx-pairhmm-template.h:110-125). Results are bit-identical to
+ * the reference kernel: raw fp32 sum, fp64 rescue when raw < 1e-28f, glibc
+ * log10f/log10 finish (intel_pairhmm.hpp:131-146).
+ *
+ * Every pointer is borrowed for the duration of the call; nothing is retained.
+ * Calls are synchronous and thread-safe (serialised internally). All entry
+ * points return 0 on success or a negative HC_PHMM_E* code; the message of the
+ * calling thread's last error is available from hc_phmm_last_error(). There is
+ * no CPU fallback: without a usable MI355X the calls fail with HC_PHMM_ENODEV.
+ */
+#ifndef HC_PAIRHMM_H
+#define HC_PAIRHMM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HC_PHMM_OK 0
+#define HC_PHMM_EINVAL (-1)   /* bad argument (null pointer, length <= 0, too long) */
+#define HC_PHMM_ENODEV (-2)   /* no usable gfx950 device / not initialised        */
+#define HC_PHMM_EHIP (-3)     /* HIP runtime error                                  */
+#define HC_PHMM_ENOMEM (-4)   /* host or device allocation failed                   */
+
+#define HC_PHMM_MAX_HAP_LEN 8192   /* LDS ring bound of the anti-diagonal kernel */
+#define HC_PHMM_MAX_READ_LEN 65536
+
+/* shacc_pairhmm::Read (shacc_pairhmm.h:12-19): same fields, same order. */
+typedef struct hc_phmm_read {
+    int32_t length;
+    const char* bases;
+    const char* q;   /* base qualities, raw SAM bytes */
+    const char* i;   /* insertion gap-open qualities  */
+    const char* d;   /* deletion gap-open qualities   */
+    const char* c;   /* gap-continuation qualities    */
+} hc_phmm_read;
+
+/* shacc_pairhmm::Haplotype (shacc_pairhmm.h:21-24). */
+typedef struct hc_phmm_hap {
+    int32_t length;
+    const char* bases;
+} hc_phmm_hap;
+
+typedef struct hc_phmm_stats {
+    int64_t n_pairs;
+    int64_t cells;          /* sum over pairs of R*H                      */
+    int64_t n_rescued;      /* pairs recomputed in fp64                   */
+    double kernel_ms_f32;   /* last run: fp32 kernel(s), HIP events       */
+    double kernel_ms_f64;   /* last run: fp64 rescue kernel               */
+    double run_ms;          /* last run: whole device pass, HIP events    */
+    int64_t n_launch_waves; /* waves launched by the fp32 pass            */
+} hc_phmm_stats;
+
+/* Select the device (HIP ordinal; -1 = current) and build the device LUTs.
+ * flags: reserved, pass 0. Idempotent. (intel_pairhmm.hpp:77-113 initNative) */
+int hc_phmm_init(uint32_t flags, int device);
+int hc_phmm_shutdown(void);
+const char* hc_phmm_last_error(void);
+int hc_phmm_version(void);   /* major*10000 + minor*100 + patch */
+
+/* All reads x all haps. out is n_reads*n_haps doubles, read-major
+ * (out[r*n_haps + h]), log10 likelihoods before normalisation.
+ * n_reads == 0 or n_haps == 0 is a no-op. */
+int hc_phmm_cross(const hc_phmm_read* reads, int32_t n_reads,
+                  const hc_phmm_hap* haps, int32_t n_haps, double* out);
+
+/* hc_phmm_cross followed by normalize_likelihoods_and_filter_poorly_modeled_reads
+ * (intel_pairhmm.hpp:24-46). out is n_reads*n_haps read-major with the cap
+ * applied to every row; keep[r] = 1 for reads that survive the filter, and
+ * *n_kept is their count. The caller erases rows/reads with keep[r] == 0. */
+int hc_phmm_compute_likelihoods(const hc_phmm_read* reads, int32_t n_reads,
+                                const hc_phmm_hap* haps, int32_t n_haps,
+                                double* out, uint8_t* keep, int32_t* n_kept);
+
+/* Independent pairs over flat byte pools: pair p uses rs/q/ins/del/gcp rows
+ * [read_off[p], read_off[p]+R[p]) and hap bytes [hap_off[p], hap_off[p]+H[p]).
+ * Outputs (any may be NULL): loglik[p], raw_f32[p], raw_f64[p] (0 unless
+ * rescued), rescued[p]. */
+int hc_phmm_pairs_flat(int64_t n, const int64_t* read_off, const int32_t* R,
+                       const int64_t* hap_off, const int32_t* H,
+                       const uint8_t* rs, const uint8_t* q, const uint8_t* ins,
+                       const uint8_t* del, const uint8_t* gcp, const uint8_t* hap,
+                       double* loglik, float* raw_f32, double* raw_f64, uint8_t* rescued);
+
+/* Plan / execute split for device-resident batches (bench, multi-GPU shards). */
+typedef struct hc_phmm_batch hc_phmm_batch;
+int hc_phmm_batch_create(int64_t n, const int64_t* read_off, const int32_t* R,
+                         const int64_t* hap_off, const int32_t* H,
+                         const uint8_t* rs, const uint8_t* q, const uint8_t* ins,
+                         const uint8_t* del, const uint8_t* gcp, const uint8_t* hap,
+                         hc_phmm_batch** out);
+/* Enqueue the whole device pass (fp32 kernel, rescue list, fp64 kernel) on
+ * `stream` (a hipStream_t; NULL = the library's stream). Asynchronous. */
+int hc_phmm_batch_run(hc_phmm_batch* b, void* stream);
+/* Wait for the last run, copy results back and apply the log10 finish. */
+int hc_phmm_batch_results(hc_phmm_batch* b, double* loglik, float* raw_f32,
+                          double* raw_f64, uint8_t* rescued);
+int hc_phmm_batch_stats(hc_phmm_batch* b, hc_phmm_stats* st);
+/* Device pointers of the per-pair results of the last run (in caller pair order):
+ * raw_f32 (float[n]), raw_f64 (double[n]), rescued flags (uint8[n]). */
+int hc_phmm_batch_device_results(hc_phmm_batch* b, void** raw_f32, void** raw_f64,
+                                 void** rescued);
+int hc_phmm_batch_destroy(hc_phmm_batch* b);
+
+/* LUTs the engine uses (for parity tests against the reference's Context<>):
+ * ph2pr_f/d[128], mm_f/d[n_mm] with n_mm = 255*256/2 = 32640. */
+int hc_phmm_get_luts(float* ph2pr_f, double* ph2pr_d, float* mm_f, double* mm_d);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HC_PAIRHMM_H */

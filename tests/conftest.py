@@ -1,0 +1,46 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "gatk-haplotypecaller-cpp17_amd")
+for p in (PKG, os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden", "pairhmm_golden.npz")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    g = np.load(GOLDEN, allow_pickle=False)
+    return {k: g[k] for k in g.files}
+
+
+@pytest.fixture(scope="session")
+def golden_batch(golden):
+    keys = ("read_off", "R", "hap_off", "H", "rs", "q", "ins", "dels", "gcp", "hap")
+    return {k: golden[k] for k in keys}
+
+
+@pytest.fixture(scope="session")
+def oracle_lib():
+    import oracle
+    oracle.build(ref=False)
+    return oracle.Oracle()
+
+
+@pytest.fixture(scope="session")
+def engine():
+    """The HIP engine on cuda:0 (gpu tests only)."""
+    import hcphmm
+    if not os.path.exists(hcphmm.LIB_PATH):
+        hcphmm.build()
+    hcphmm.init(0)
+    return hcphmm

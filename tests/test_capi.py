@@ -1,0 +1,99 @@
+"""CPU: the C-ABI library loads, exports every declared symbol, and its host
+side (LUTs, argument checks) is correct without a GPU."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import hcphmm
+
+
+@pytest.fixture(scope="module")
+def built():
+    if not os.path.exists(hcphmm.LIB_PATH):
+        hcphmm.build()
+    return hcphmm.lib()
+
+
+def test_exports_every_declared_symbol(built):
+    syms = hcphmm.declared_symbols()
+    assert len(syms) >= 14
+    out = subprocess.run(["nm", "-D", "--defined-only", hcphmm.LIB_PATH],
+                         capture_output=True, text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    missing = [s for s in syms if s not in exported]
+    assert not missing, missing
+
+
+def test_library_has_gfx950_code_object(built):
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", hcphmm.LIB_PATH],
+                         capture_output=True, text=True)
+    text = out.stdout + out.stderr
+    if out.returncode != 0 or "gfx" not in text:
+        data = open(hcphmm.LIB_PATH, "rb").read()
+        assert b"gfx950" in data
+    else:
+        assert "gfx950" in text
+
+
+def test_struct_layout_matches_shacc(built):
+    # shacc_pairhmm::Read {int; 5 x const char*} / Haplotype {int; const char*}
+    assert ctypes.sizeof(hcphmm.Read) == 48
+    assert hcphmm.Read.bases.offset == 8
+    assert ctypes.sizeof(hcphmm.Hap) == 16
+
+
+def test_engine_luts_match_reference(built, golden):
+    L = hcphmm.get_luts()
+    for k in L:
+        assert np.array_equal(L[k].view(np.uint8), golden[k].view(np.uint8)), k
+
+
+def test_no_silent_fallback_without_gpu(built):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(hcphmm.PairHMMError) as e:
+        hcphmm.init()
+    assert e.value.code == hcphmm.ENODEV
+    b = {"read_off": np.zeros(1, np.int64), "R": np.ones(1, np.int32),
+         "hap_off": np.zeros(1, np.int64), "H": np.ones(1, np.int32)}
+    for k in ("rs", "q", "ins", "dels", "gcp", "hap"):
+        b[k] = np.array([65], np.uint8)
+    with pytest.raises(hcphmm.PairHMMError):
+        hcphmm.pairs(b)
+
+
+def test_cpp_shim_compiles(tmp_path):
+    """include/hc_pairhmm.hpp (the IntelPairHMM drop-in) compiles against a
+    stand-in of the caller's SAMRecord/Haplotype shape and links."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = tmp_path / "shim.cpp"
+    src.write_text(r'''
+#include "hc_pairhmm.hpp"
+#include <string>
+#include <string_view>
+#include <vector>
+struct SAMRecord { std::string SEQ, QUAL;
+  static inline const std::string GOP = std::string(200, 'I');
+  static inline const std::string GCP = std::string(200, '+');
+  auto insertionGOP() const { return std::string_view{GOP}.substr(0, SEQ.size()); }
+  auto deletionGOP() const { return std::string_view{GOP}.substr(0, SEQ.size()); }
+  auto overallGCP() const { return std::string_view{GCP}.substr(0, SEQ.size()); }
+  auto size() const { return SEQ.size(); } };
+struct Haplotype { std::string bases; };
+int main() {
+  std::vector<Haplotype> h{{"ACGT"}, {"ACGA"}};
+  std::vector<SAMRecord> r{{"ACG", "III"}};
+  hc::MI355XPairHMM phmm;
+  try { auto L = phmm.compute_likelihoods(h, r); return int(L.size()) - 1; }
+  catch (const std::exception&) { return 0; }
+}
+''')
+    exe = tmp_path / "shim"
+    subprocess.run(["g++", "-std=c++17", "-I", os.path.join(root, "include"), str(src),
+                    "-L", os.path.dirname(hcphmm.LIB_PATH), "-lhcpairhmm",
+                    "-Wl,-rpath," + os.path.dirname(hcphmm.LIB_PATH), "-o", str(exe)], check=True)
+    assert exe.exists()

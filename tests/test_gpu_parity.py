@@ -1,0 +1,129 @@
+"""GPU parity: the HIP engine (through the C ABI) against the reference's golden
+vectors and the oracle, bit for bit. Run on an MI355X: pytest -m gpu."""
+import numpy as np
+import pytest
+
+import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint8)
+
+
+def assert_same(res, ref, what=""):
+    """Bit-exact: raw f32, rescue decision, raw f64 of rescued pairs, log10 result."""
+    r32 = res["raw_f32"].view(np.uint32) != ref["raw_f32"].view(np.uint32)
+    assert not r32.any(), f"{what}: {r32.sum()} raw_f32 mismatches, first {np.nonzero(r32)[0][:10]}"
+    assert np.array_equal(res["rescued"], ref["rescued"]), what
+    m = ref["rescued"].astype(bool)
+    r64 = res["raw_f64"][m].view(np.uint64) != ref["raw_f64"][m].view(np.uint64)
+    assert not r64.any(), f"{what}: {r64.sum()} raw_f64 mismatches"
+    ll = res["loglik"].view(np.uint64) != ref["loglik"].view(np.uint64)
+    assert not ll.any(), f"{what}: {ll.sum()} loglik mismatches"
+
+
+def test_golden_bit_exact(engine, golden, golden_batch):
+    res = engine.pairs(golden_batch)
+    ref = dict(raw_f32=golden["raw_f32"], rescued=golden["rescued"],
+               raw_f64=golden["raw_f64_all"], loglik=golden["loglik"])
+    names = list(golden["set_names"])
+    for k, name in enumerate(names):
+        idx = golden["set_id"] == k
+        assert_same({x: res[x][idx] for x in res}, {x: ref[x][idx] for x in ref}, name)
+
+
+def test_golden_f64_path_on_every_pair(engine, golden, golden_batch):
+    """Force the fp64 kernel onto pairs that do not need rescue by re-running the
+    underflow set alone (all rescued) and the edge set's rescued pairs."""
+    names = list(golden["set_names"])
+    idx = np.nonzero(golden["rescued"].astype(bool))[0]
+    sub = W.subset(golden_batch, idx)
+    res = engine.pairs(sub)
+    assert res["rescued"].all()
+    assert np.array_equal(bits(res["raw_f64"]), bits(golden["raw_f64_all"][idx]))
+    assert "underflow" in names
+
+
+def test_s1_full_vs_oracle(engine, oracle_lib):
+    b = W.config("S1")
+    res = engine.pairs(b)
+    ref = oracle_lib.pairs(b, nthreads=16)
+    assert_same(res, ref, "S1")
+
+
+def test_s2_sample_vs_oracle(engine, oracle_lib):
+    b = W.config("S2", 20_000)
+    res = engine.pairs(b)
+    ref = oracle_lib.pairs(b, nthreads=16)
+    assert_same(res, ref, "S2-20k")
+
+
+def test_s4_sample_vs_oracle(engine, oracle_lib):
+    b = W.subset(W.config("S4"), np.arange(200))
+    res = engine.pairs(b)
+    ref = oracle_lib.pairs(b, nthreads=16)
+    assert res["rescued"].sum() > 100
+    assert_same(res, ref, "S4-200")
+
+
+def test_mixed_lengths_share_waves(engine, oracle_lib):
+    """Pairs of very different R/H packed into the same waves (both W classes)."""
+    b = W.generate(3000, (1, 1200), (1, 300), 0.05, seed=5)
+    res = engine.pairs(b)
+    ref = oracle_lib.pairs(b, nthreads=16)
+    assert_same(res, ref, "mixed")
+
+
+def test_batch_rerun_is_deterministic(engine):
+    b = W.config("S2", 50_000)
+    bt = engine.Batch(b)
+    bt.run()
+    r1 = bt.results()
+    bt.run()
+    r2 = bt.results()
+    st = bt.stats()
+    assert st.n_pairs == 50_000 and st.cells == W.cells(b)
+    assert st.n_rescued == int(r1["rescued"].sum())
+    for k in r1:
+        assert np.array_equal(bits(r1[k]), bits(r2[k])), k
+    assert np.isfinite(r1["loglik"]).all()
+    bt.close()
+
+
+def test_cross_and_compute_likelihoods(engine, oracle_lib):
+    """Region-shaped call: every read against every hap (intel_pairhmm.hpp:48-56)."""
+    rng = np.random.default_rng(3)
+    haps = []
+    base = W.ACGT[rng.integers(0, 4, 400)]
+    for k in range(6):
+        h = base.copy()
+        h[rng.integers(0, 400, 3)] = W.ACGT[rng.integers(0, 4, 3)]
+        haps.append(h.tobytes())
+    reads = []
+    for k in range(40):
+        o = int(rng.integers(0, 250))
+        rs = np.frombuffer(haps[k % 6], np.uint8)[o:o + 150].copy()
+        if k % 9 == 0:
+            rs[:] = W.ACGT[rng.integers(0, 4, 150)]          # junk read -> filtered
+        q = (rng.integers(10, 41, 150) + 33).astype(np.uint8).tobytes()
+        reads.append((rs.tobytes(), q, b"I" * 150, b"I" * 150, b"+" * 150))
+    L = engine.cross(reads, haps)
+    flat = W.from_pairs([(r[0], r[1], r[2], r[3], r[4], h) for r in reads for h in haps])
+    ref = oracle_lib.pairs(flat, nthreads=16)["loglik"].reshape(len(reads), len(haps))
+    assert np.array_equal(bits(L), bits(ref))
+    Ln, kept = engine.compute_likelihoods(haps, reads)
+    refn, keep = oracle_lib.normalize(ref, np.full(len(reads), 150, np.int32))
+    assert len(kept) == int(keep.sum()) < len(reads)
+    assert np.array_equal(bits(Ln), bits(refn[keep]))
+
+
+def test_edge_contract(engine):
+    empty = engine.cross([], [b"ACGT"])
+    assert empty.shape == (0, 1)
+    with pytest.raises(engine.PairHMMError) as e:
+        engine.cross([(b"", b"", b"", b"", b"")], [b"ACGT"])
+    assert e.value.code == engine.EINVAL
+    with pytest.raises(engine.PairHMMError):
+        engine.cross([(b"A", b"I", b"I", b"I", b"+")], [b"A" * 9000])
