@@ -135,9 +135,12 @@ struct hc_phmm_batch {
     PairDesc* d_pairs = nullptr;
     uint32_t* d_rows = nullptr;
     uint32_t* d_hapw = nullptr;
-    float* d_raw32 = nullptr;
+    float* d_raw32 = nullptr;     // current output targets (own or bound)
     double* d_raw64 = nullptr;
     uint8_t* d_flag = nullptr;
+    float* own_raw32 = nullptr;   // library-owned output buffers
+    double* own_raw64 = nullptr;
+    uint8_t* own_flag = nullptr;
     int* d_list = nullptr;
     int* d_count = nullptr;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
@@ -157,9 +160,9 @@ void free_batch(hc_phmm_batch* b)
     (void)hipFree(b->d_pairs);
     (void)hipFree(b->d_rows);
     (void)hipFree(b->d_hapw);
-    (void)hipFree(b->d_raw32);
-    (void)hipFree(b->d_raw64);
-    (void)hipFree(b->d_flag);
+    (void)hipFree(b->own_raw32);
+    (void)hipFree(b->own_raw64);
+    (void)hipFree(b->own_flag);
     (void)hipFree(b->d_list);
     (void)hipFree(b->d_count);
     for (auto& e : b->ev)
@@ -267,13 +270,16 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     for (int c = 0; c < 2; ++c) chk(dev_upload(&b->cls[c].d_order, ord[c].data(), ord[c].size()));
     if (rc == HC_PHMM_OK) {
         const size_t n1 = std::max<int64_t>(npairs, 1);
-        if (hipMalloc(&b->d_raw32, sizeof(float) * n1) != hipSuccess ||
-            hipMalloc(&b->d_raw64, sizeof(double) * n1) != hipSuccess ||
-            hipMalloc(&b->d_flag, n1) != hipSuccess ||
+        if (hipMalloc(&b->own_raw32, sizeof(float) * n1) != hipSuccess ||
+            hipMalloc(&b->own_raw64, sizeof(double) * n1) != hipSuccess ||
+            hipMalloc(&b->own_flag, n1) != hipSuccess ||
             hipMalloc(&b->d_list, sizeof(int) * n1) != hipSuccess ||
             hipMalloc(&b->d_count, sizeof(int)) != hipSuccess)
             chk(fail(HC_PHMM_ENOMEM, "device allocation failed"));
     }
+    b->d_raw32 = b->own_raw32;
+    b->d_raw64 = b->own_raw64;
+    b->d_flag = b->own_flag;
     for (auto& e : b->ev)
         if (rc == HC_PHMM_OK && hipEventCreate(&e) != hipSuccess) chk(fail(HC_PHMM_EHIP, "hipEventCreate"));
     if (rc != HC_PHMM_OK) {
@@ -536,6 +542,16 @@ int hc_phmm_batch_device_results(hc_phmm_batch* b, void** raw_f32, void** raw_f6
     if (raw_f32) *raw_f32 = b->d_raw32;
     if (raw_f64) *raw_f64 = b->d_raw64;
     if (rescued) *rescued = b->d_flag;
+    return HC_PHMM_OK;
+}
+
+int hc_phmm_batch_bind_outputs(hc_phmm_batch* b, void* raw_f32, void* raw_f64, void* rescued)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!b) return fail(HC_PHMM_EINVAL, "null batch");
+    b->d_raw32 = raw_f32 ? static_cast<float*>(raw_f32) : b->own_raw32;
+    b->d_raw64 = raw_f64 ? static_cast<double*>(raw_f64) : b->own_raw64;
+    b->d_flag = rescued ? static_cast<uint8_t*>(rescued) : b->own_flag;
     return HC_PHMM_OK;
 }
 

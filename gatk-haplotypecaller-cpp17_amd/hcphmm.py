@@ -86,6 +86,7 @@ def lib():
     L.hc_phmm_batch_results.argtypes = [C.c_void_p, _f64p, _f32p, _f64p, _u8p]
     L.hc_phmm_batch_stats.argtypes = [C.c_void_p, C.POINTER(Stats)]
     L.hc_phmm_batch_device_results.argtypes = [C.c_void_p] + [C.POINTER(C.c_void_p)] * 3
+    L.hc_phmm_batch_bind_outputs.argtypes = [C.c_void_p] * 4
     L.hc_phmm_batch_destroy.argtypes = [C.c_void_p]
     L.hc_phmm_get_luts.argtypes = [_f32p, _f64p, _f32p, _f64p]
     _lib = L
@@ -215,6 +216,11 @@ class Batch:
         p = [C.c_void_p() for _ in range(3)]
         _check(lib().hc_phmm_batch_device_results(self._h, *[C.byref(x) for x in p]))
         return tuple(x.value for x in p)
+
+    def bind_outputs(self, raw_f32=None, raw_f64=None, rescued=None):
+        """Write later runs' results into caller-owned device buffers (int pointers,
+        e.g. torch_tensor.data_ptr())."""
+        _check(lib().hc_phmm_batch_bind_outputs(self._h, raw_f32, raw_f64, rescued))
 
     def close(self):
         if getattr(self, "_h", None):

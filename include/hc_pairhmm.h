@@ -124,6 +124,11 @@ int hc_phmm_batch_stats(hc_phmm_batch* b, hc_phmm_stats* st);
  * raw_f32 (float[n]), raw_f64 (double[n]), rescued flags (uint8[n]). */
 int hc_phmm_batch_device_results(hc_phmm_batch* b, void** raw_f32, void** raw_f64,
                                  void** rescued);
+/* Make later runs write their per-pair results into caller-owned device buffers
+ * (e.g. torch tensors, for an RCCL gather without a copy): raw_f32 float[n],
+ * raw_f64 double[n], rescued uint8[n], all on the engine's device. NULL keeps
+ * the library's own buffer for that output. */
+int hc_phmm_batch_bind_outputs(hc_phmm_batch* b, void* raw_f32, void* raw_f64, void* rescued);
 int hc_phmm_batch_destroy(hc_phmm_batch* b);
 
 /* LUTs the engine uses (for parity tests against the reference's Context<>):
