@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""PairHMM throughput bench (GCUPS) for the MI355X engine.
+
+    python bench.py [--gpus N --steps K --warmup W --workload S2]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Workload (BASELINE.json configs[2] / configs[3]): the seeded synthetic WGS-mix
+batch S2 — 1 000 000 independent (read, hap) pairs, H ~ U[100, 500],
+R ~ U[50, min(250, H)], 1 % substitutions, Phred U[10, 40] (+33), GOP 'I',
+GCP '+' (SURVEY.md §8(d)). One step = the whole device pass of the hot path
+over that batch: fp32 anti-diagonal kernel, device-built rescue list, fp64
+rescue kernel; with N > 1 the same batch is sharded by cells over the ranks
+(strong scaling) and the step ends with the RCCL gather of the per-pair raw
+results to rank 0 (configs[3]). Inputs are resident in HBM before timing.
+
+Prints one JSON line (rank 0). `value` = total cells / max-over-ranks wall time
+of the K timed steps. `roofline` prices the dominant kernel (fp32 PairHMM) by
+its algorithmic work, 12 fp32 mul/add per cell, against the non-FMA fp32 VALU
+rate; `cpu_baseline` times the reference's own AVX kernel (oracle/_ref) on the
+host cores, same batch.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "gatk-haplotypecaller-cpp17_amd")
+sys.path.insert(0, PKG)
+
+import numpy as np  # noqa: E402
+
+VALU_PEAK_TOPS = 78.6      # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, one f32 mul/add per lane-cycle
+FLOPS_PER_CELL = 12        # computeMXY: 8 mul + 4 add (avx-pairhmm-template.h:183-198)
+HBM_PEAK_GBS = 8000.0
+
+
+def algorithmic_bytes(b):
+    """Per pair: read rows 5 B x R + hap H B + 8 B result."""
+    return int(5 * b["R"].astype(np.int64).sum() + b["H"].astype(np.int64).sum() + 8 * len(b["R"]))
+
+
+def cpu_baseline(batch, threads, reps, sample_desc):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    kind = "reference"
+    try:
+        lib = oracle.Reference()
+    except FileNotFoundError:
+        lib, kind = oracle.Oracle(), "port"
+    import workloads as W
+    cells = W.cells(batch)
+    best = None
+    res = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        res = lib.pairs(batch, nthreads=threads)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    return dict(value=cells / best / 1e9, unit="GCUPS", cores=threads, kind=kind,
+                sample=sample_desc, seconds=round(best, 3)), res
+
+
+def traffic_from_profiles(workload):
+    """HBM bytes per launch of the dominant kernel from a committed PMC summary
+    (profiles/*pmc*.json written by tools/pmc_summary.py), else None."""
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc*{workload}*.json")))
+    if not cands:
+        return None, None
+    try:
+        d = json.load(open(cands[-1]))
+        return d.get("hbm_bytes_per_launch"), os.path.relpath(cands[-1], ROOT)
+    except Exception:
+        return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="S2", choices=["S1", "S1w", "S2", "S4"])
+    ap.add_argument("--pairs", type=int, default=None, help="override pair count")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-reps", type=int, default=2)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip end-to-end and secondary configs")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    import hcphmm
+    import shard
+    import workloads as W
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    hcphmm.init(local)
+
+    batch = W.config(args.workload, args.pairs)
+    n_total = len(batch["R"])
+    total_cells = W.cells(batch)
+    shards = shard.shard_pairs(batch["R"], batch["H"], world)
+    mine = shards[rank]
+    sub = batch if world == 1 else W.subset(batch, mine)
+    my_cells = W.cells(sub)
+    nmax = max(len(s) for s in shards)
+
+    bt = hcphmm.Batch(sub)
+    raw32 = torch.zeros(nmax, dtype=torch.float32, device=dev)
+    raw64 = torch.zeros(nmax, dtype=torch.float64, device=dev)
+    flag = torch.zeros(nmax, dtype=torch.uint8, device=dev)
+    bt.bind_outputs(raw32.data_ptr(), raw64.data_ptr(), flag.data_ptr())
+    g32 = [torch.empty_like(raw32) for _ in range(world)] if (world > 1 and rank == 0) else None
+    g64 = [torch.empty_like(raw64) for _ in range(world)] if (world > 1 and rank == 0) else None
+
+    def step():
+        bt.run(torch.cuda.current_stream().cuda_stream)
+        if world > 1:
+            dist.gather(raw32, gather_list=g32, dst=0)   # RCCL gather over xGMI
+            dist.gather(raw64, gather_list=g64, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    bt.stats()   # reset the kernel event log: the averages below cover the timed steps only
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = bt.stats()
+    ms_step = elapsed / args.steps * 1e3
+    value = total_cells * args.steps / elapsed / 1e9
+
+    # Dominant kernel: fp32 anti-diagonal PairHMM. Algorithmic work 12 ops/cell.
+    k_ms = st.kernel_ms_f32
+    achieved = FLOPS_PER_CELL * my_cells / (k_ms * 1e-3) / 1e12 if k_ms > 0 else 0.0
+    traffic, tsrc = traffic_from_profiles(args.workload)
+    roofline = dict(bound="valu", achieved=round(achieved, 3), peak=VALU_PEAK_TOPS, unit="TFLOP/s",
+                    frac=round(achieved / VALU_PEAK_TOPS, 4), traffic=traffic,
+                    kernel="phmm_diag_kernel<float,16>", kernel_ms=round(k_ms, 4),
+                    flops_per_cell=FLOPS_PER_CELL, cells_per_launch=my_cells,
+                    hbm_algorithmic_GBs=round(algorithmic_bytes(sub) / (k_ms * 1e-3) / 1e9, 2) if k_ms > 0 else None,
+                    hbm_peak_GBs=HBM_PEAK_GBS, traffic_source=tsrc)
+
+    out = {
+        "metric": "PairHMM GCUPS (cell updates/s), fp32 pass + fp64 rescue",
+        "value": round(value, 2), "unit": "GCUPS", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+        "scaling": "strong" if world > 1 else "strong", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (seeded generator, SURVEY.md §8(d))",
+        "config": {"workload": f"{args.workload}: {n_total} independent pairs"
+                               + (", H~U[100,500], R~U[50,min(250,H)], 1% subst" if args.workload == "S2" else ""),
+                   "pairs": n_total, "cells": total_cells, "parallelism": f"pair-shard x{world}",
+                   "rescued_fp64": int(st.n_rescued) if world == 1 else None},
+        "roofline": roofline,
+        "kernel_ms_f64": round(st.kernel_ms_f64, 4),
+        "device_pass_ms": round(st.run_ms, 4),
+    }
+
+    cpu_res = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        thr = min(args.cpu_threads, os.cpu_count() or 1)
+        cb, cpu_res = cpu_baseline(batch, thr, args.cpu_reps,
+                                   f"the full {args.workload} batch ({n_total} pairs), {thr} OpenMP threads, "
+                                   f"best of {args.cpu_reps}")
+        out["cpu_baseline"] = cb
+        if not args.no_extra:
+            s1 = W.subset(batch, np.arange(min(n_total, 20_000)))
+            c1, _ = cpu_baseline(s1, 1, 1, f"first {len(s1['R'])} pairs of {args.workload}, 1 thread")
+            out["cpu_baseline_1core"] = c1
+
+    if rank == 0 and world == 1:
+        r = bt.results()
+        out["config"]["rescued_fp64"] = int(r["rescued"].sum())
+        if cpu_res is not None:
+            same = all(np.array_equal(np.ascontiguousarray(r[k]).view(np.uint8),
+                                      np.ascontiguousarray(cpu_res[k]).view(np.uint8))
+                       for k in ("raw_f32", "rescued", "loglik"))
+            out["parity_vs_cpu_reference"] = "bit-exact" if same else "MISMATCH"
+    if rank == 0 and world == 1 and not args.no_extra:
+        t0 = time.perf_counter()
+        hcphmm.pairs(batch)
+        e2e = time.perf_counter() - t0
+        out["end_to_end_gcups"] = round(total_cells / e2e / 1e9, 2)
+        out["end_to_end_note"] = "host pack + H2D + kernels + D2H + host log10, one call of hc_phmm_pairs_flat"
+        sec = {}
+        for name in ("S1", "S4"):
+            b2 = W.config(name)
+            bb = hcphmm.Batch(b2)
+            for _ in range(2):
+                bb.run()
+            bb.stats()
+            for _ in range(5):
+                bb.run()
+            s2 = bb.stats()
+            sec[name] = dict(pairs=len(b2["R"]), cells=W.cells(b2), device_pass_ms=round(s2.run_ms, 4),
+                             gcups=round(W.cells(b2) / (s2.run_ms * 1e-3) / 1e9, 2),
+                             rescued=int(s2.n_rescued))
+            bb.close()
+        out["secondary"] = sec
+    if world > 1:
+        out["gather"] = "dist.gather (RCCL) of raw_f32 + raw_f64 per step"
+    bt.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -10,9 +10,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <numeric>
@@ -132,6 +134,12 @@ struct hc_phmm_batch {
         int ring_len = 0;
         int* d_order = nullptr;
     } cls[2];
+    // Lane-per-pair class (large batches).
+    int n_lane = 0;
+    int lane_waves = 0;
+    int* d_lane_order = nullptr;
+    LaneWave* d_lane_waves = nullptr;
+    float2* d_carry = nullptr;
     PairDesc* d_pairs = nullptr;
     uint32_t* d_rows = nullptr;
     uint32_t* d_hapw = nullptr;
@@ -143,7 +151,11 @@ struct hc_phmm_batch {
     uint8_t* own_flag = nullptr;
     int* d_list = nullptr;
     int* d_count = nullptr;
-    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};   // current run's triple (from ev_pool)
+    // Event triples of every run since the last stats() call (reused pool), so
+    // stats() reports the average kernel time over a whole timed region.
+    std::vector<std::array<hipEvent_t, 3>> ev_pool;
+    size_t ev_used = 0;
     hipStream_t last_stream = nullptr;
     int64_t launch_waves = 0;
     bool ran = false;
@@ -152,11 +164,25 @@ struct hc_phmm_batch {
 namespace {
 
 constexpr int kW64Threshold = 768;   // H above this -> one pair per wave (W = 64)
+constexpr int64_t kLaneMinPairs = 32768;   // batches this large use the lane-per-pair kernel
+constexpr int kLaneMaxH = 4096;            // longer haps stay on the anti-diagonal kernel
+
+// Kernel selection: HC_PHMM_KERNEL=auto (default) | lane | diag.
+int kernel_policy()
+{
+    const char* e = std::getenv("HC_PHMM_KERNEL");
+    if (!e || !*e || !std::strcmp(e, "auto")) return 0;
+    if (!std::strcmp(e, "lane")) return 1;
+    return 2;
+}
 
 void free_batch(hc_phmm_batch* b)
 {
     if (!b) return;
     for (auto& c : b->cls) (void)hipFree(c.d_order);
+    (void)hipFree(b->d_lane_order);
+    (void)hipFree(b->d_lane_waves);
+    (void)hipFree(b->d_carry);
     (void)hipFree(b->d_pairs);
     (void)hipFree(b->d_rows);
     (void)hipFree(b->d_hapw);
@@ -165,8 +191,8 @@ void free_batch(hc_phmm_batch* b)
     (void)hipFree(b->own_flag);
     (void)hipFree(b->d_list);
     (void)hipFree(b->d_count);
-    for (auto& e : b->ev)
-        if (e) (void)hipEventDestroy(e);
+    for (auto& t : b->ev_pool)
+        for (auto& e : t) (void)hipEventDestroy(e);
     delete b;
 }
 
@@ -240,10 +266,49 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     // Length binning: W class by H; inside a class sort by (stripes, H) descending
     // so the G pairs sharing a wave have equal stripe counts and similar H, and the
     // heaviest waves dispatch first.
-    std::vector<int> ord[2];
-    for (int64_t p = 0; p < npairs; ++p) ord[pd[p].w > kW64Threshold ? 1 : 0].push_back(int(p));
+    std::vector<int> ord[2], lane_ord;
+    const int pol = kernel_policy();
+    const bool use_lane = pol == 1 || (pol == 0 && npairs >= kLaneMinPairs);
+    for (int64_t p = 0; p < npairs; ++p) {
+        if (use_lane && (pol == 1 || pd[p].w <= kLaneMaxH))
+            lane_ord.push_back(int(p));
+        else
+            ord[pd[p].w > kW64Threshold ? 1 : 0].push_back(int(p));
+    }
+    // Lane class: bin by column coverage (H rounded up to 16), then R, both
+    // descending, so a wave's 64 pairs sweep nearly the same rows x columns.
+    auto cols16 = [&](int p) { return (pd[p].w + 15) / 16 * 16; };
+    std::stable_sort(lane_ord.begin(), lane_ord.end(), [&](int x, int y) {
+        const int cx = cols16(x), cy = cols16(y);
+        if (cx != cy) return cx > cy;
+        return pd[x].y > pd[y].y;
+    });
+    std::vector<LaneWave> lw;
+    int64_t carry_rows = 0;
+    bool need_carry = false;
+    for (size_t s0 = 0; s0 < lane_ord.size(); s0 += 64) {
+        LaneWave w{};
+        w.slot0 = int(s0);
+        w.rmax = 0;
+        w.rmin = INT32_MAX;
+        w.ncols = 0;
+        for (size_t k = s0; k < std::min(lane_ord.size(), s0 + 64); ++k) {
+            const int p = lane_ord[k];
+            w.rmax = std::max(w.rmax, pd[p].y);
+            w.rmin = std::min(w.rmin, pd[p].y);
+            w.ncols = std::max(w.ncols, cols16(p));
+        }
+        w.carry_row = carry_rows;
+        if (w.ncols > kLaneBlock) {
+            need_carry = true;
+            carry_rows += w.rmax + 1;
+        }
+        lw.push_back(w);
+    }
     const int Wc[2] = {16, 64};
     auto* b = new hc_phmm_batch();
+    b->n_lane = int(lane_ord.size());
+    b->lane_waves = int(lw.size());
     b->n = npairs;
     b->cells = cells;
     b->Hmax = Hmax;
@@ -268,6 +333,11 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     chk(dev_upload(&b->d_rows, rows.data(), rows.size()));
     chk(dev_upload(&b->d_hapw, hapw.data(), hapw.size()));
     for (int c = 0; c < 2; ++c) chk(dev_upload(&b->cls[c].d_order, ord[c].data(), ord[c].size()));
+    chk(dev_upload(&b->d_lane_order, lane_ord.data(), lane_ord.size()));
+    chk(dev_upload(&b->d_lane_waves, lw.data(), lw.size()));
+    if (rc == HC_PHMM_OK && need_carry &&
+        hipMalloc(&b->d_carry, sizeof(float2) * size_t(carry_rows) * 64) != hipSuccess)
+        chk(fail(HC_PHMM_ENOMEM, "carry buffer allocation failed"));
     if (rc == HC_PHMM_OK) {
         const size_t n1 = std::max<int64_t>(npairs, 1);
         if (hipMalloc(&b->own_raw32, sizeof(float) * n1) != hipSuccess ||
@@ -280,8 +350,6 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     b->d_raw32 = b->own_raw32;
     b->d_raw64 = b->own_raw64;
     b->d_flag = b->own_flag;
-    for (auto& e : b->ev)
-        if (rc == HC_PHMM_OK && hipEventCreate(&e) != hipSuccess) chk(fail(HC_PHMM_EHIP, "hipEventCreate"));
     if (rc != HC_PHMM_OK) {
         free_batch(b);
         return rc;
@@ -295,9 +363,34 @@ int run(hc_phmm_batch* b, hipStream_t s)
     if (!s) s = g_eng.stream;
     b->last_stream = s;
     b->launch_waves = 0;
+    if (b->ev_used == b->ev_pool.size()) {
+        std::array<hipEvent_t, 3> t{};
+        for (auto& e : t) HIP_TRY(hipEventCreate(&e));
+        b->ev_pool.push_back(t);
+    }
+    const auto& ev = b->ev_pool[b->ev_used++];
+    for (int k = 0; k < 3; ++k) b->ev[k] = ev[k];
     HIP_TRY(hipEventRecord(b->ev[0], s));
     HIP_TRY(hipMemsetAsync(b->d_count, 0, sizeof(int), s));
     HIP_TRY(hipMemsetAsync(b->d_raw64, 0, sizeof(double) * std::max<int64_t>(b->n, 1), s));
+    if (b->n_lane > 0) {
+        LaneArgs a{};
+        a.pairs = b->d_pairs;
+        a.order = b->d_lane_order;
+        a.n_slots = b->n_lane;
+        a.n_waves = b->lane_waves;
+        a.waves = b->d_lane_waves;
+        a.carry = b->d_carry;
+        a.rows = b->d_rows;
+        a.hapw = b->d_hapw;
+        a.lut = g_eng.lut_f;
+        a.raw_out = b->d_raw32;
+        a.rescue_flag = b->d_flag;
+        a.rescue_list = b->d_list;
+        a.rescue_count = b->d_count;
+        b->launch_waves += b->lane_waves;
+        HIP_TRY(launch_lane_f32(a, s));
+    }
     for (auto& c : b->cls) {
         if (c.n == 0) continue;
         DiagArgs a{};
@@ -563,14 +656,22 @@ int hc_phmm_batch_stats(hc_phmm_batch* b, hc_phmm_stats* st)
     st->n_pairs = b->n;
     st->cells = b->cells;
     st->n_launch_waves = b->launch_waves;
-    if (b->ran) {
+    if (b->ran && b->ev_used > 0) {
         HIP_TRY(hipStreamSynchronize(b->last_stream));
-        float a = 0, c = 0;
-        HIP_TRY(hipEventElapsedTime(&a, b->ev[0], b->ev[1]));
-        HIP_TRY(hipEventElapsedTime(&c, b->ev[1], b->ev[2]));
-        st->kernel_ms_f32 = a;
-        st->kernel_ms_f64 = c;
-        st->run_ms = double(a) + double(c);
+        double sa = 0, sc = 0;
+        for (size_t k = 0; k < b->ev_used; ++k) {
+            float a = 0, c = 0;
+            HIP_TRY(hipEventSynchronize(b->ev_pool[k][2]));
+            HIP_TRY(hipEventElapsedTime(&a, b->ev_pool[k][0], b->ev_pool[k][1]));
+            HIP_TRY(hipEventElapsedTime(&c, b->ev_pool[k][1], b->ev_pool[k][2]));
+            sa += a;
+            sc += c;
+        }
+        st->n_runs = int64_t(b->ev_used);
+        st->kernel_ms_f32 = sa / double(b->ev_used);
+        st->kernel_ms_f64 = sc / double(b->ev_used);
+        st->run_ms = st->kernel_ms_f32 + st->kernel_ms_f64;
+        b->ev_used = 0;
         int cnt = 0;
         HIP_TRY(hipMemcpy(&cnt, b->d_count, sizeof(int), hipMemcpyDeviceToHost));
         st->n_rescued = cnt;

@@ -23,6 +23,7 @@
 // avx-pairhmm-template.h:224,287-291). The match prior comes from 32-column
 // bit windows of the hap match table (precompute_masks, :3-35), one select per
 // cell.
+#include "device_common.hpp"
 #include "kernels.hpp"
 #include "luts.hpp"
 
@@ -30,18 +31,6 @@ namespace hcphmm {
 namespace {
 
 template <typename T> struct Pair2 { T t, xn; };
-
-__device__ __forceinline__ int row_q(uint32_t w) { return w & 127; }
-__device__ __forceinline__ int row_i(uint32_t w) { return (w >> 7) & 127; }
-__device__ __forceinline__ int row_d(uint32_t w) { return (w >> 14) & 127; }
-__device__ __forceinline__ int row_c(uint32_t w) { return (w >> 21) & 127; }
-__device__ __forceinline__ int row_rc(uint32_t w) { return (w >> 28) & 7; }
-
-__device__ __forceinline__ int mm_idx(int a, int b)
-{
-    const int lo = min(a, b), hi = max(a, b);
-    return ((hi * (hi + 1)) >> 1) + lo;
-}
 
 // Lane shift by one inside each W-lane group: lane l gets lane l-1's `src`,
 // lane 0 of the group gets `old` (the stripe carry-in).

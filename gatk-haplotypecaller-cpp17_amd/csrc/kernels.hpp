@@ -46,6 +46,34 @@ struct DiagArgs {
     int* rescue_count;        // fp32 pass: append counter
 };
 
+// Lane-per-pair kernel (large batches): one lane owns one pair and sweeps it
+// row by row over register-resident blocks of kLaneBlock columns. A wave holds
+// 64 length-binned pairs; wave_meta gives its rows (max R) and column coverage.
+constexpr int kLaneBlock = 64;
+struct LaneWave {
+    int slot0;      // first slot of the wave in `order`
+    int rmax;       // rows swept (max R of the wave's pairs)
+    int rmin;       // min R of the wave's active pairs (first row that may need the sum)
+    int ncols;      // columns swept (max H rounded up to 16), <= nblk * 64
+    long long carry_row;  // first carry row of this wave in `carry` (units of 64 float2)
+};
+struct LaneArgs {
+    const PairDesc* pairs;
+    const int* order;
+    int n_slots;
+    int n_waves;
+    const LaneWave* waves;
+    float2* carry;            // block-to-block column carry {T, Y} per row and lane
+    const uint32_t* rows;
+    const uint32_t* hapw;
+    const float* lut;
+    float* raw_out;
+    uint8_t* rescue_flag;
+    int* rescue_list;
+    int* rescue_count;
+};
+hipError_t launch_lane_f32(const LaneArgs& a, hipStream_t s);
+
 // Launchers (kernels.hip). W = lanes per pair: 16, 32 or 64.
 hipError_t launch_diag_f32(int W, const DiagArgs& a, int grid, hipStream_t s);
 hipError_t launch_diag_f64(int W, const DiagArgs& a, int grid, hipStream_t s);

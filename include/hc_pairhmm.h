@@ -69,10 +69,11 @@ typedef struct hc_phmm_stats {
     int64_t n_pairs;
     int64_t cells;          /* sum over pairs of R*H                      */
     int64_t n_rescued;      /* pairs recomputed in fp64                   */
-    double kernel_ms_f32;   /* last run: fp32 kernel(s), HIP events       */
-    double kernel_ms_f64;   /* last run: fp64 rescue kernel               */
-    double run_ms;          /* last run: whole device pass, HIP events    */
-    int64_t n_launch_waves; /* waves launched by the fp32 pass            */
+    double kernel_ms_f32;   /* fp32 kernel(s), HIP events, mean over n_runs  */
+    double kernel_ms_f64;   /* fp64 rescue kernel, mean over n_runs          */
+    double run_ms;          /* whole device pass, mean over n_runs           */
+    int64_t n_launch_waves; /* waves launched by the fp32 pass               */
+    int64_t n_runs;         /* runs since the previous stats() call          */
 } hc_phmm_stats;
 
 /* Select the device (HIP ordinal; -1 = current) and build the device LUTs.
@@ -119,6 +120,8 @@ int hc_phmm_batch_run(hc_phmm_batch* b, void* stream);
 /* Wait for the last run, copy results back and apply the log10 finish. */
 int hc_phmm_batch_results(hc_phmm_batch* b, double* loglik, float* raw_f32,
                           double* raw_f64, uint8_t* rescued);
+/* Counters and device timings averaged over every run since the previous
+ * stats() call (the event log is reset by this call). */
 int hc_phmm_batch_stats(hc_phmm_batch* b, hc_phmm_stats* st);
 /* Device pointers of the per-pair results of the last run (in caller pair order):
  * raw_f32 (float[n]), raw_f64 (double[n]), rescued flags (uint8[n]). */

@@ -7,6 +7,15 @@ import workloads as W
 
 pytestmark = pytest.mark.gpu
 
+KERNELS = ["diag", "lane"]
+
+
+@pytest.fixture(params=KERNELS)
+def kernel(request, monkeypatch):
+    """Force one of the two fp32 kernels (anti-diagonal / lane-per-pair)."""
+    monkeypatch.setenv("HC_PHMM_KERNEL", request.param)
+    return request.param
+
 
 def bits(a):
     return np.ascontiguousarray(a).view(np.uint8)
@@ -24,14 +33,14 @@ def assert_same(res, ref, what=""):
     assert not ll.any(), f"{what}: {ll.sum()} loglik mismatches"
 
 
-def test_golden_bit_exact(engine, golden, golden_batch):
+def test_golden_bit_exact(engine, kernel, golden, golden_batch):
     res = engine.pairs(golden_batch)
     ref = dict(raw_f32=golden["raw_f32"], rescued=golden["rescued"],
                raw_f64=golden["raw_f64_all"], loglik=golden["loglik"])
     names = list(golden["set_names"])
     for k, name in enumerate(names):
         idx = golden["set_id"] == k
-        assert_same({x: res[x][idx] for x in res}, {x: ref[x][idx] for x in ref}, name)
+        assert_same({x: res[x][idx] for x in res}, {x: ref[x][idx] for x in ref}, f"{kernel}/{name}")
 
 
 def test_golden_f64_path_on_every_pair(engine, golden, golden_batch):
@@ -46,14 +55,14 @@ def test_golden_f64_path_on_every_pair(engine, golden, golden_batch):
     assert "underflow" in names
 
 
-def test_s1_full_vs_oracle(engine, oracle_lib):
+def test_s1_full_vs_oracle(engine, kernel, oracle_lib):
     b = W.config("S1")
     res = engine.pairs(b)
     ref = oracle_lib.pairs(b, nthreads=16)
     assert_same(res, ref, "S1")
 
 
-def test_s2_sample_vs_oracle(engine, oracle_lib):
+def test_s2_sample_vs_oracle(engine, kernel, oracle_lib):
     b = W.config("S2", 20_000)
     res = engine.pairs(b)
     ref = oracle_lib.pairs(b, nthreads=16)
@@ -68,7 +77,7 @@ def test_s4_sample_vs_oracle(engine, oracle_lib):
     assert_same(res, ref, "S4-200")
 
 
-def test_mixed_lengths_share_waves(engine, oracle_lib):
+def test_mixed_lengths_share_waves(engine, kernel, oracle_lib):
     """Pairs of very different R/H packed into the same waves (both W classes)."""
     b = W.generate(3000, (1, 1200), (1, 300), 0.05, seed=5)
     res = engine.pairs(b)
@@ -76,7 +85,7 @@ def test_mixed_lengths_share_waves(engine, oracle_lib):
     assert_same(res, ref, "mixed")
 
 
-def test_batch_rerun_is_deterministic(engine):
+def test_batch_rerun_is_deterministic(engine, kernel):
     b = W.config("S2", 50_000)
     bt = engine.Batch(b)
     bt.run()
@@ -92,7 +101,7 @@ def test_batch_rerun_is_deterministic(engine):
     bt.close()
 
 
-def test_cross_and_compute_likelihoods(engine, oracle_lib):
+def test_cross_and_compute_likelihoods(engine, kernel, oracle_lib):
     """Region-shaped call: every read against every hap (intel_pairhmm.hpp:48-56)."""
     rng = np.random.default_rng(3)
     haps = []
@@ -127,3 +136,23 @@ def test_edge_contract(engine):
     assert e.value.code == engine.EINVAL
     with pytest.raises(engine.PairHMMError):
         engine.cross([(b"A", b"I", b"I", b"I", b"+")], [b"A" * 9000])
+
+
+def test_s2_full_size_properties(engine):
+    """BASELINE configs[2] at full size (1M pairs, lane kernel): every result finite,
+    rescue rate tiny, rerun bit-identical, and a 2 000-pair sample equal to the
+    oracle bit for bit."""
+    import oracle
+    b = W.config("S2")
+    bt = engine.Batch(b)
+    bt.run()
+    r1 = bt.results()
+    bt.run()
+    r2 = bt.results()
+    assert np.array_equal(bits(r1["loglik"]), bits(r2["loglik"]))
+    assert np.isfinite(r1["loglik"]).all()
+    assert r1["rescued"].sum() < 200
+    idx = np.random.default_rng(0).choice(len(b["R"]), 2000, replace=False)
+    ref = oracle.Oracle().pairs(W.subset(b, idx), nthreads=16)
+    assert_same({k: r1[k][idx] for k in r1}, ref, "S2-full-sample")
+    bt.close()
