@@ -656,6 +656,7 @@ int hc_phmm_batch_stats(hc_phmm_batch* b, hc_phmm_stats* st)
     st->n_pairs = b->n;
     st->cells = b->cells;
     st->n_launch_waves = b->launch_waves;
+    st->n_lane_pairs = b->n_lane;
     if (b->ran && b->ev_used > 0) {
         HIP_TRY(hipStreamSynchronize(b->last_stream));
         double sa = 0, sc = 0;

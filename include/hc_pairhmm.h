@@ -74,6 +74,7 @@ typedef struct hc_phmm_stats {
     double run_ms;          /* whole device pass, mean over n_runs           */
     int64_t n_launch_waves; /* waves launched by the fp32 pass               */
     int64_t n_runs;         /* runs since the previous stats() call          */
+    int64_t n_lane_pairs;   /* pairs on the lane-per-pair kernel (rest: anti-diagonal) */
 } hc_phmm_stats;
 
 /* Select the device (HIP ordinal; -1 = current) and build the device LUTs.
