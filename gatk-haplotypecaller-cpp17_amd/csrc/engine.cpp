@@ -688,3 +688,47 @@ int hc_phmm_batch_destroy(hc_phmm_batch* b)
 }
 
 }  // extern "C"
+
+// --------------------------------------------------------------------------
+// The reference's own accelerator slot: a strong definition of the weak
+// `bool shacc_pairhmm::calculate(Batch&)` declared in
+// pairhmm/native/shacc_pairhmm.h:10-36. The structs below are layout- and
+// name-compatible declarations (same namespace, same member order) so the
+// mangled symbol matches; results[r * num_haps + h] receives the fp32 cast of
+// the log10 likelihood (the slot's `float* results`; hc_phmm_cross gives the
+// full double).
+namespace shacc_pairhmm {
+struct Read {
+    int length;
+    const char* bases;
+    const char* q;
+    const char* i;
+    const char* d;
+    const char* c;
+};
+struct Haplotype {
+    int length;
+    const char* bases;
+};
+struct Batch {
+    int num_reads;
+    int num_haps;
+    long num_cells;
+    Read* reads;
+    Haplotype* haps;
+    float* results;
+};
+__attribute__((visibility("default"))) bool calculate(Batch& batch);
+bool calculate(Batch& batch)
+{
+    static_assert(sizeof(Read) == sizeof(hc_phmm_read), "Read layout");
+    static_assert(sizeof(Haplotype) == sizeof(hc_phmm_hap), "Haplotype layout");
+    if (batch.num_reads < 0 || batch.num_haps < 0 || !batch.results) return false;
+    std::vector<double> out(size_t(batch.num_reads) * size_t(batch.num_haps));
+    const int rc = hc_phmm_cross(reinterpret_cast<const hc_phmm_read*>(batch.reads), batch.num_reads,
+                                 reinterpret_cast<const hc_phmm_hap*>(batch.haps), batch.num_haps, out.data());
+    if (rc != HC_PHMM_OK) return false;
+    for (size_t k = 0; k < out.size(); ++k) batch.results[k] = float(out[k]);
+    return true;
+}
+}  // namespace shacc_pairhmm
