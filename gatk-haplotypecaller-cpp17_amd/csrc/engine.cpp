@@ -123,7 +123,8 @@ struct HapView {
 }  // namespace
 
 // --------------------------------------------------------------------------
-// Prepared batch.
+// Prepared batch: every device array of one batch lives in one allocation,
+// filled by one H2D copy from one pinned staging buffer.
 struct hc_phmm_batch {
     int64_t n = 0;          // pairs
     int64_t cells = 0;
@@ -137,6 +138,7 @@ struct hc_phmm_batch {
     // Lane-per-pair class (large batches).
     int n_lane = 0;
     int lane_waves = 0;
+    int lane_p = 1;   // pairs per lane of the lane kernel
     int* d_lane_order = nullptr;
     LaneWave* d_lane_waves = nullptr;
     float2* d_carry = nullptr;
@@ -151,6 +153,8 @@ struct hc_phmm_batch {
     uint8_t* own_flag = nullptr;
     int* d_list = nullptr;
     int* d_count = nullptr;
+    char* dev_base = nullptr;     // the batch's device allocation
+    bool owns_dev = true;         // false: borrowed from the engine workspace
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};   // current run's triple (from ev_pool)
     // Event triples of every run since the last stats() call (reused pool), so
     // stats() reports the average kernel time over a whole timed region.
@@ -167,6 +171,14 @@ constexpr int kW64Threshold = 768;   // H above this -> one pair per wave (W = 6
 constexpr int64_t kLaneMinPairs = 32768;   // batches this large use the lane-per-pair kernel
 constexpr int kLaneMaxH = 4096;            // longer haps stay on the anti-diagonal kernel
 
+// Pairs per lane of the lane kernel: HC_PHMM_LANE_P=1|2 (default 2: packed f32).
+int lane_pairs_per_lane()
+{
+    const char* e = std::getenv("HC_PHMM_LANE_P");
+    if (e && *e == '1') return 1;
+    return 2;
+}
+
 // Kernel selection: HC_PHMM_KERNEL=auto (default) | lane | diag.
 int kernel_policy()
 {
@@ -176,38 +188,91 @@ int kernel_policy()
     return 2;
 }
 
+// Grow-only buffers reused by the synchronous entry points (no per-call
+// hipMalloc / hipHostMalloc once warm).
+struct Workspace {
+    char* dev = nullptr;
+    size_t dev_cap = 0;
+    char* host = nullptr;   // pinned
+    size_t host_cap = 0;
+    hc_phmm_batch* batch = nullptr;   // batch shell reused for its event pool
+};
+Workspace g_ws;
+
+int ws_dev(size_t bytes, char** out)
+{
+    if (bytes > g_ws.dev_cap) {
+        if (g_ws.dev) HIP_TRY(hipFree(g_ws.dev));
+        g_ws.dev = nullptr;
+        g_ws.dev_cap = 0;
+        const size_t cap = std::max(bytes + bytes / 4, size_t(64) << 20);
+        if (hipMalloc(&g_ws.dev, cap) != hipSuccess) return fail(HC_PHMM_ENOMEM, "device workspace");
+        g_ws.dev_cap = cap;
+    }
+    *out = g_ws.dev;
+    return HC_PHMM_OK;
+}
+
+int ws_host(size_t bytes, char** out)
+{
+    if (bytes > g_ws.host_cap) {
+        if (g_ws.host) HIP_TRY(hipHostFree(g_ws.host));
+        g_ws.host = nullptr;
+        g_ws.host_cap = 0;
+        const size_t cap = std::max(bytes + bytes / 4, size_t(16) << 20);
+        if (hipHostMalloc(&g_ws.host, cap, hipHostMallocDefault) != hipSuccess)
+            return fail(HC_PHMM_ENOMEM, "pinned staging buffer");
+        g_ws.host_cap = cap;
+    }
+    *out = g_ws.host;
+    return HC_PHMM_OK;
+}
+
+void release_batch_memory(hc_phmm_batch* b)
+{
+    if (b->owns_dev) (void)hipFree(b->dev_base);
+    b->dev_base = nullptr;
+}
+
 void free_batch(hc_phmm_batch* b)
 {
     if (!b) return;
-    for (auto& c : b->cls) (void)hipFree(c.d_order);
-    (void)hipFree(b->d_lane_order);
-    (void)hipFree(b->d_lane_waves);
-    (void)hipFree(b->d_carry);
-    (void)hipFree(b->d_pairs);
-    (void)hipFree(b->d_rows);
-    (void)hipFree(b->d_hapw);
-    (void)hipFree(b->own_raw32);
-    (void)hipFree(b->own_raw64);
-    (void)hipFree(b->own_flag);
-    (void)hipFree(b->d_list);
-    (void)hipFree(b->d_count);
+    release_batch_memory(b);
     for (auto& t : b->ev_pool)
         for (auto& e : t) (void)hipEventDestroy(e);
     delete b;
 }
 
-template <typename T>
-int dev_upload(T** dst, const T* src, size_t count)
+// LSD radix sort of `idx` by a 32-bit key, DESCENDING, stable.
+void sort_desc(std::vector<int>& idx, const std::vector<uint32_t>& key)
 {
-    const size_t bytes = sizeof(T) * std::max<size_t>(count, 1);
-    HIP_TRY(hipMalloc(dst, bytes));
-    if (count) HIP_TRY(hipMemcpy(*dst, src, sizeof(T) * count, hipMemcpyHostToDevice));
-    return HC_PHMM_OK;
+    std::vector<int> tmp(idx.size());
+    for (int shift = 0; shift < 32; shift += 16) {
+        std::vector<size_t> cnt(65537, 0);
+        for (int p : idx) ++cnt[0xffff - ((key[p] >> shift) & 0xffff) + 1];
+        for (size_t k = 1; k < cnt.size(); ++k) cnt[k] += cnt[k - 1];
+        for (int p : idx) tmp[cnt[0xffff - ((key[p] >> shift) & 0xffff)]++] = p;
+        idx.swap(tmp);
+    }
 }
 
+// Bump allocator over one device region: 256-B aligned segments.
+struct Layout {
+    size_t off = 0;
+    size_t take(size_t bytes)
+    {
+        const size_t o = off;
+        off += (bytes + 255) & ~size_t(255);
+        return o;
+    }
+};
+
 // Pack reads/haps once each, pairs refer to them (cross product reuses both).
+// borrow_ws: place the device arrays in the engine workspace (synchronous
+// calls) instead of a batch-owned allocation.
 int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
-         int64_t npairs, const int32_t* pr, const int32_t* ph, hc_phmm_batch** out)
+         int64_t npairs, const int32_t* pr, const int32_t* ph, bool borrow_ws,
+         hc_phmm_batch** out)
 {
     for (const auto& r : reads)
         if (r.len <= 0 || r.len > HC_PHMM_MAX_READ_LEN || !r.bases || !r.q || !r.i || !r.d || !r.c)
@@ -225,34 +290,7 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     if (row_off[nr] > INT32_MAX || hap_off[nh] > INT32_MAX)
         return fail(HC_PHMM_EINVAL, "batch too large (row or hap pool exceeds 2^31 words)");
 
-    std::vector<uint32_t> rows(row_off[nr] + 1);
-    parallel_for(nr, [&](int64_t b, int64_t e) {
-        for (int64_t r = b; r < e; ++r) {
-            const ReadView& v = reads[r];
-            uint32_t* o = rows.data() + row_off[r];
-            for (int k = 0; k < v.len; ++k)
-                o[k] = pack_row(v.q[k], v.i[k], v.d[k], v.c[k], base_code(v.bases[k]));
-        }
-    }, 256);
-    std::vector<uint32_t> hapw(hap_off[nh] + 1, 0u);
-    parallel_for(nh, [&](int64_t b, int64_t e) {
-        for (int64_t h = b; h < e; ++h) {
-            const HapView& v = haps[h];
-            uint32_t* t = hapw.data() + hap_off[h];
-            for (int j = 1; j <= v.len; ++j) {
-                const uint32_t bit = 0x80000000u >> ((j - 1) & 31);
-                uint32_t* row = t + (((j - 1) >> 5) + kHapLead) * 5;
-                const int hc = base_code(v.bases[j - 1]);
-                if (hc == 4) {
-                    for (int rc = 0; rc < 5; ++rc) row[rc] |= bit;
-                } else {
-                    row[hc] |= bit;
-                    row[4] |= bit;   // read 'N' matches every column
-                }
-            }
-        }
-    }, 256);
-
+    // Descriptors and length binning.
     std::vector<PairDesc> pd(npairs);
     int64_t cells = 0;
     int Hmax = 0;
@@ -262,10 +300,6 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
         cells += int64_t(reads[r].len) * haps[h].len;
         Hmax = std::max(Hmax, haps[h].len);
     }
-
-    // Length binning: W class by H; inside a class sort by (stripes, H) descending
-    // so the G pairs sharing a wave have equal stripe counts and similar H, and the
-    // heaviest waves dispatch first.
     std::vector<int> ord[2], lane_ord;
     const int pol = kernel_policy();
     const bool use_lane = pol == 1 || (pol == 0 && npairs >= kLaneMinPairs);
@@ -275,85 +309,160 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
         else
             ord[pd[p].w > kW64Threshold ? 1 : 0].push_back(int(p));
     }
+    std::vector<uint32_t> key(npairs);
     // Lane class: bin by column coverage (H rounded up to 16), then R, both
-    // descending, so a wave's 64 pairs sweep nearly the same rows x columns.
+    // descending, so a wave's 64*P pairs sweep nearly the same rows x columns.
     auto cols16 = [&](int p) { return (pd[p].w + 15) / 16 * 16; };
-    std::stable_sort(lane_ord.begin(), lane_ord.end(), [&](int x, int y) {
-        const int cx = cols16(x), cy = cols16(y);
-        if (cx != cy) return cx > cy;
-        return pd[x].y > pd[y].y;
-    });
+    for (int p : lane_ord) key[p] = (uint32_t(cols16(p)) << 16) | uint32_t(std::min(pd[p].y, 65535));
+    sort_desc(lane_ord, key);
     std::vector<LaneWave> lw;
     int64_t carry_rows = 0;
-    bool need_carry = false;
-    for (size_t s0 = 0; s0 < lane_ord.size(); s0 += 64) {
+    const int lane_p = lane_pairs_per_lane();
+    const size_t per_wave = size_t(64) * lane_p;
+    for (size_t s0 = 0; s0 < lane_ord.size(); s0 += per_wave) {
         LaneWave w{};
         w.slot0 = int(s0);
         w.rmax = 0;
         w.rmin = INT32_MAX;
         w.ncols = 0;
-        for (size_t k = s0; k < std::min(lane_ord.size(), s0 + 64); ++k) {
+        for (size_t k = s0; k < std::min(lane_ord.size(), s0 + per_wave); ++k) {
             const int p = lane_ord[k];
             w.rmax = std::max(w.rmax, pd[p].y);
             w.rmin = std::min(w.rmin, pd[p].y);
             w.ncols = std::max(w.ncols, cols16(p));
         }
         w.carry_row = carry_rows;
-        if (w.ncols > kLaneBlock) {
-            need_carry = true;
-            carry_rows += w.rmax + 1;
-        }
+        if (w.ncols > lane_block_cols(lane_p)) carry_rows += w.rmax + 1;
         lw.push_back(w);
     }
+    // Anti-diagonal classes: W by H; (stripes, H) descending so the G pairs
+    // sharing a wave have equal stripe counts and similar H, heaviest first.
     const int Wc[2] = {16, 64};
-    auto* b = new hc_phmm_batch();
-    b->n_lane = int(lane_ord.size());
-    b->lane_waves = int(lw.size());
-    b->n = npairs;
-    b->cells = cells;
-    b->Hmax = Hmax;
+    int ring_len[2];
     for (int c = 0; c < 2; ++c) {
         const int W = Wc[c];
-        auto& o = ord[c];
-        std::stable_sort(o.begin(), o.end(), [&](int x, int y) {
-            const int sx = (pd[x].y + W - 1) / W, sy = (pd[y].y + W - 1) / W;
-            if (sx != sy) return sx > sy;
-            return pd[x].w > pd[y].w;
-        });
         int hm = 0;
-        for (int p : o) hm = std::max(hm, pd[p].w);
-        b->cls[c].W = W;
-        b->cls[c].n = int(o.size());
-        b->cls[c].ring_len = hm + 2 * W + 16;
+        for (int p : ord[c]) {
+            key[p] = (uint32_t((pd[p].y + W - 1) / W) << 16) | uint32_t(pd[p].w);
+            hm = std::max(hm, pd[p].w);
+        }
+        sort_desc(ord[c], key);
+        ring_len[c] = hm + 2 * W + 16;
     }
 
+    // One device region: uploaded arrays first, then outputs and scratch.
+    Layout L;
+    const size_t o_pairs = L.take(sizeof(PairDesc) * npairs);
+    const size_t o_rows = L.take(sizeof(uint32_t) * (row_off[nr] + 1));
+    const size_t o_hapw = L.take(sizeof(uint32_t) * (hap_off[nh] + 1));
+    const size_t o_ord0 = L.take(sizeof(int) * ord[0].size());
+    const size_t o_ord1 = L.take(sizeof(int) * ord[1].size());
+    const size_t o_lord = L.take(sizeof(int) * lane_ord.size());
+    const size_t o_lw = L.take(sizeof(LaneWave) * lw.size());
+    const size_t upload = L.off;
+    const size_t n1 = size_t(std::max<int64_t>(npairs, 1));
+    const size_t o_raw32 = L.take(sizeof(float) * n1);
+    const size_t o_raw64 = L.take(sizeof(double) * n1);
+    const size_t o_flag = L.take(n1);
+    const size_t o_list = L.take(sizeof(int) * n1);
+    const size_t o_count = L.take(sizeof(int));
+    const size_t o_carry = L.take(sizeof(float2) * size_t(carry_rows) * 64 * lane_p);
+    const size_t total = L.off;
+
+    char* host = nullptr;
+    bool own_host = false;
     int rc = HC_PHMM_OK;
-    auto chk = [&](int r) { if (rc == HC_PHMM_OK) rc = r; };
-    chk(dev_upload(&b->d_pairs, pd.data(), pd.size()));
-    chk(dev_upload(&b->d_rows, rows.data(), rows.size()));
-    chk(dev_upload(&b->d_hapw, hapw.data(), hapw.size()));
-    for (int c = 0; c < 2; ++c) chk(dev_upload(&b->cls[c].d_order, ord[c].data(), ord[c].size()));
-    chk(dev_upload(&b->d_lane_order, lane_ord.data(), lane_ord.size()));
-    chk(dev_upload(&b->d_lane_waves, lw.data(), lw.size()));
-    if (rc == HC_PHMM_OK && need_carry &&
-        hipMalloc(&b->d_carry, sizeof(float2) * size_t(carry_rows) * 64) != hipSuccess)
-        chk(fail(HC_PHMM_ENOMEM, "carry buffer allocation failed"));
-    if (rc == HC_PHMM_OK) {
-        const size_t n1 = std::max<int64_t>(npairs, 1);
-        if (hipMalloc(&b->own_raw32, sizeof(float) * n1) != hipSuccess ||
-            hipMalloc(&b->own_raw64, sizeof(double) * n1) != hipSuccess ||
-            hipMalloc(&b->own_flag, n1) != hipSuccess ||
-            hipMalloc(&b->d_list, sizeof(int) * n1) != hipSuccess ||
-            hipMalloc(&b->d_count, sizeof(int)) != hipSuccess)
-            chk(fail(HC_PHMM_ENOMEM, "device allocation failed"));
+    if (borrow_ws) {
+        rc = ws_host(upload, &host);
+    } else {
+        if (hipHostMalloc(&host, std::max<size_t>(upload, 1), hipHostMallocDefault) != hipSuccess)
+            rc = fail(HC_PHMM_ENOMEM, "pinned staging buffer");
+        own_host = true;
     }
-    b->d_raw32 = b->own_raw32;
-    b->d_raw64 = b->own_raw64;
-    b->d_flag = b->own_flag;
+    if (rc) return rc;
+
+    // Fill the staging image (parallel over reads and haps).
+    std::memcpy(host + o_pairs, pd.data(), sizeof(PairDesc) * npairs);
+    uint32_t* rows = reinterpret_cast<uint32_t*>(host + o_rows);
+    parallel_for(nr, [&](int64_t b, int64_t e) {
+        for (int64_t r = b; r < e; ++r) {
+            const ReadView& v = reads[r];
+            uint32_t* o = rows + row_off[r];
+            for (int k = 0; k < v.len; ++k)
+                o[k] = pack_row(v.q[k], v.i[k], v.d[k], v.c[k], base_code(v.bases[k]));
+        }
+    }, 256);
+    rows[row_off[nr]] = 0;
+    uint32_t* hapw = reinterpret_cast<uint32_t*>(host + o_hapw);
+    parallel_for(nh, [&](int64_t b, int64_t e) {
+        for (int64_t h = b; h < e; ++h) {
+            const HapView& v = haps[h];
+            uint32_t* t = hapw + hap_off[h];
+            std::memset(t, 0, sizeof(uint32_t) * (hap_off[h + 1] - hap_off[h]));
+            for (int j = 1; j <= v.len; ++j) {
+                const uint32_t bit = 0x80000000u >> ((j - 1) & 31);
+                uint32_t* row = t + (((j - 1) >> 5) + kHapLead) * 5;
+                const int hc = base_code(v.bases[j - 1]);
+                if (hc == 4) {
+                    for (int rcode = 0; rcode < 5; ++rcode) row[rcode] |= bit;
+                } else {
+                    row[hc] |= bit;
+                    row[4] |= bit;   // read 'N' matches every column
+                }
+            }
+        }
+    }, 256);
+    hapw[hap_off[nh]] = 0;
+    std::memcpy(host + o_ord0, ord[0].data(), sizeof(int) * ord[0].size());
+    std::memcpy(host + o_ord1, ord[1].data(), sizeof(int) * ord[1].size());
+    std::memcpy(host + o_lord, lane_ord.data(), sizeof(int) * lane_ord.size());
+    std::memcpy(host + o_lw, lw.data(), sizeof(LaneWave) * lw.size());
+
+    auto* b = new hc_phmm_batch();
+    char* dev = nullptr;
+    if (borrow_ws) {
+        rc = ws_dev(total, &dev);
+        b->owns_dev = false;
+    } else if (hipMalloc(&dev, total) != hipSuccess) {
+        rc = fail(HC_PHMM_ENOMEM, "device allocation failed (" + std::to_string(total >> 20) + " MiB)");
+    }
+    if (rc == HC_PHMM_OK) {
+        b->dev_base = dev;
+        // The workspace staging stays valid until the call returns, so only a
+        // batch-owned staging buffer needs the copy to finish here.
+        const hipError_t e1 = hipMemcpyAsync(dev, host, upload, hipMemcpyHostToDevice, g_eng.stream);
+        const hipError_t e2 = (e1 == hipSuccess && own_host) ? hipStreamSynchronize(g_eng.stream) : e1;
+        if (e2 != hipSuccess) rc = fail(HC_PHMM_EHIP, std::string("H2D: ") + hipGetErrorString(e2));
+    }
+    if (own_host) (void)hipHostFree(host);
     if (rc != HC_PHMM_OK) {
         free_batch(b);
         return rc;
     }
+    b->n = npairs;
+    b->cells = cells;
+    b->Hmax = Hmax;
+    b->n_lane = int(lane_ord.size());
+    b->lane_p = lane_p;
+    b->lane_waves = int(lw.size());
+    b->d_pairs = reinterpret_cast<PairDesc*>(dev + o_pairs);
+    b->d_rows = reinterpret_cast<uint32_t*>(dev + o_rows);
+    b->d_hapw = reinterpret_cast<uint32_t*>(dev + o_hapw);
+    for (int c = 0; c < 2; ++c) {
+        b->cls[c].W = Wc[c];
+        b->cls[c].n = int(ord[c].size());
+        b->cls[c].ring_len = ring_len[c];
+    }
+    b->cls[0].d_order = reinterpret_cast<int*>(dev + o_ord0);
+    b->cls[1].d_order = reinterpret_cast<int*>(dev + o_ord1);
+    b->d_lane_order = reinterpret_cast<int*>(dev + o_lord);
+    b->d_lane_waves = reinterpret_cast<LaneWave*>(dev + o_lw);
+    b->own_raw32 = b->d_raw32 = reinterpret_cast<float*>(dev + o_raw32);
+    b->own_raw64 = b->d_raw64 = reinterpret_cast<double*>(dev + o_raw64);
+    b->own_flag = b->d_flag = reinterpret_cast<uint8_t*>(dev + o_flag);
+    b->d_list = reinterpret_cast<int*>(dev + o_list);
+    b->d_count = reinterpret_cast<int*>(dev + o_count);
+    b->d_carry = carry_rows ? reinterpret_cast<float2*>(dev + o_carry) : nullptr;
     *out = b;
     return HC_PHMM_OK;
 }
@@ -389,7 +498,7 @@ int run(hc_phmm_batch* b, hipStream_t s)
         a.rescue_list = b->d_list;
         a.rescue_count = b->d_count;
         b->launch_waves += b->lane_waves;
-        HIP_TRY(launch_lane_f32(a, s));
+        HIP_TRY(launch_lane_f32(b->lane_p, a, s));
     }
     for (auto& c : b->cls) {
         if (c.n == 0) continue;
@@ -434,26 +543,36 @@ int run(hc_phmm_batch* b, hipStream_t s)
 int results(hc_phmm_batch* b, double* loglik, float* raw32, double* raw64, uint8_t* resc)
 {
     if (!b->ran) return fail(HC_PHMM_EINVAL, "batch has not been run");
-    HIP_TRY(hipStreamSynchronize(b->last_stream));
     const int64_t n = b->n;
     if (n == 0) return HC_PHMM_OK;
-    std::vector<float> f(n);
-    std::vector<double> d(n);
-    std::vector<uint8_t> fl(n);
-    HIP_TRY(hipMemcpy(f.data(), b->d_raw32, sizeof(float) * n, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(d.data(), b->d_raw64, sizeof(double) * n, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(fl.data(), b->d_flag, n, hipMemcpyDeviceToHost));
-    if (raw32) std::memcpy(raw32, f.data(), sizeof(float) * n);
-    if (raw64) std::memcpy(raw64, d.data(), sizeof(double) * n);
-    if (resc) std::memcpy(resc, fl.data(), n);
+    // D2H into the pinned workspace: [raw32 | raw64 | flags]. Drain the stream
+    // first: growing the workspace frees the staging an earlier H2D read.
+    HIP_TRY(hipStreamSynchronize(b->last_stream));
+    char* host = nullptr;
+    const size_t o64 = (sizeof(float) * n + 15) & ~size_t(15);
+    const size_t ofl = o64 + sizeof(double) * n;
+    int rc = ws_host(ofl + n, &host);
+    if (rc) return rc;
+    hipStream_t s = b->last_stream;
+    HIP_TRY(hipMemcpyAsync(host, b->d_raw32, sizeof(float) * n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(host + o64, b->d_raw64, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(host + ofl, b->d_flag, n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const float* f = reinterpret_cast<const float*>(host);
+    const double* d = reinterpret_cast<const double*>(host + o64);
+    const uint8_t* fl = reinterpret_cast<const uint8_t*>(host + ofl);
+    if (raw32) std::memcpy(raw32, f, sizeof(float) * n);
+    if (raw64) std::memcpy(raw64, d, sizeof(double) * n);
+    if (resc) std::memcpy(resc, fl, n);
     if (loglik) {
+        // intel_pairhmm.hpp:137-143, glibc log10 / log10f as in the reference.
         const Luts& L = luts();
         const float l10f = L.log10_init_f;
         const double l10d = L.log10_init_d;
         parallel_for(n, [&](int64_t lo, int64_t hi) {
             for (int64_t p = lo; p < hi; ++p)
                 loglik[p] = fl[p] ? std::log10(d[p]) - l10d : double(std::log10(f[p]) - l10f);
-        }, 1 << 16);
+        }, 1 << 15);
     }
     return HC_PHMM_OK;
 }
@@ -507,6 +626,9 @@ int hc_phmm_shutdown(void)
     if (!g_eng.ready) return HC_PHMM_OK;
     (void)hipFree(g_eng.lut_f);
     (void)hipFree(g_eng.lut_d);
+    (void)hipFree(g_ws.dev);
+    (void)hipHostFree(g_ws.host);
+    g_ws = Workspace{};
     (void)hipStreamDestroy(g_eng.stream);
     g_eng = Engine{};
     return HC_PHMM_OK;
@@ -537,7 +659,7 @@ int hc_phmm_pairs_flat(int64_t n, const int64_t* read_off, const int32_t* R, con
     rc = flat_views(n, read_off, R, hap_off, H, rs, q, ins, del, gcp, hap, rv, hv, idx);
     if (rc) return rc;
     hc_phmm_batch* b = nullptr;
-    rc = plan(rv, hv, n, idx.data(), idx.data(), &b);
+    rc = plan(rv, hv, n, idx.data(), idx.data(), true, &b);
     if (rc) return rc;
     rc = run_sync(b, loglik, raw_f32, raw_f64, rescued);
     free_batch(b);
@@ -566,7 +688,7 @@ int hc_phmm_cross(const hc_phmm_read* reads, int32_t n_reads, const hc_phmm_hap*
         ph[p] = int32_t(p % n_haps);
     }
     hc_phmm_batch* b = nullptr;
-    rc = plan(rv, hv, np, pr.data(), ph.data(), &b);
+    rc = plan(rv, hv, np, pr.data(), ph.data(), true, &b);
     if (rc) return rc;
     rc = run_sync(b, out, nullptr, nullptr, nullptr);
     free_batch(b);
@@ -610,7 +732,7 @@ int hc_phmm_batch_create(int64_t n, const int64_t* read_off, const int32_t* R, c
     std::vector<int32_t> idx;
     rc = flat_views(n, read_off, R, hap_off, H, rs, q, ins, del, gcp, hap, rv, hv, idx);
     if (rc) return rc;
-    return plan(rv, hv, n, idx.data(), idx.data(), out);
+    return plan(rv, hv, n, idx.data(), idx.data(), false, out);
 }
 
 int hc_phmm_batch_run(hc_phmm_batch* b, void* stream)

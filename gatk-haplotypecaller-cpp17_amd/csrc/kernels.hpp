@@ -72,7 +72,9 @@ struct LaneArgs {
     int* rescue_list;
     int* rescue_count;
 };
-hipError_t launch_lane_f32(const LaneArgs& a, hipStream_t s);
+// P = pairs per lane (1, or 2 packed in float2 halves); block columns 64 / P*... see lane_block_cols.
+hipError_t launch_lane_f32(int P, const LaneArgs& a, hipStream_t s);
+int lane_block_cols(int P);
 
 // Launchers (kernels.hip). W = lanes per pair: 16, 32 or 64.
 hipError_t launch_diag_f32(int W, const DiagArgs& a, int grid, hipStream_t s);

@@ -2,12 +2,14 @@
 //
 // Same semantics as the anti-diagonal kernel (kernels.hip) and the reference's
 // compute_full_prob_avxs (avx-pairhmm-template.h:210-346), bit for bit, but the
-// parallelism is across pairs instead of inside one: each lane owns one
-// (read, hap) pair and walks its DP matrix row by row over register-resident
-// blocks of up to 64 columns. A wave holds 64 pairs binned by (column blocks,
-// R), so its lanes run the same trip counts. Nothing crosses lanes: no DPP
-// shifts, no fill/drain of anti-diagonals, no LDS — 12 mul/add + 2 select ops
-// per cell.
+// parallelism is across pairs instead of inside one: each lane owns P pairs
+// (P = 1, or P = 2 held in the .x/.y halves of float2 registers so that every
+// mul/add is one packed v_pk_mul_f32 / v_pk_add_f32 for two cells) and walks
+// their DP matrices row by row over register-resident column blocks
+// (64 columns for P = 1, 32 for P = 2: the same 128 state VGPRs). A wave holds
+// 64*P pairs binned by (column blocks, R), so its lanes run the same trip
+// counts. Nothing crosses lanes: no DPP shifts, no anti-diagonal fill/drain,
+// no LDS — 12 mul/add + 2 select ops per cell.
 //
 // Per column j of the block the lane keeps two values between rows
 //   T[j] = (M*mm + X*gapm) + Y*gapm of the previous row (row i's constants),
@@ -25,43 +27,55 @@
 namespace hcphmm {
 namespace {
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+template <int P> struct VT;
+template <> struct VT<1> { using type = float; };
+template <> struct VT<2> { using type = f2; };
+
+__device__ __forceinline__ float comp(float v, int) { return v; }
+__device__ __forceinline__ float comp(f2 v, int p) { return p ? v.y : v.x; }
+__device__ __forceinline__ void set_comp(float& v, int, float s) { v = s; }
+__device__ __forceinline__ void set_comp(f2& v, int p, float s)
+{
+    if (p) v.y = s; else v.x = s;
+}
+template <typename V> __device__ __forceinline__ V splat(float s) { return V(s); }
+
+// Columns per register block: 64 state pairs of registers either way.
+template <int P> constexpr int block_cols() { return P == 1 ? 64 : 32; }
+
+template <int P>
 struct RowConst {
-    float pm, px;        // prior: 1 - ph2pr[q], ph2pr[q] / 3          (this row)
-    float my, yy;        // Y transitions: ph2pr[d], ph2pr[c]           (this row)
-    float mm, g, mx, xx; // transitions into the NEXT row: mm, 1 - ph2pr[c], ph2pr[i], ph2pr[c]
-    int rc;              // read base code of this row
+    using V = typename VT<P>::type;
+    V pm, px;        // prior: 1 - ph2pr[q], ph2pr[q] / 3          (this row)
+    V my, yy;        // Y transitions: ph2pr[d], ph2pr[c]           (this row)
+    V mm, g, mx, xx; // transitions into the NEXT row: mm, 1 - ph2pr[c], ph2pr[i], ph2pr[c]
+    int rc[P];       // read base code of this row
 };
 
-__device__ __forceinline__ void row_const(const float* __restrict__ lut, uint32_t wc, uint32_t wn,
-                                          RowConst& k)
+template <int P>
+__device__ __forceinline__ void row_const(const float* __restrict__ lut, const uint32_t (&wc)[P],
+                                          const uint32_t (&wn)[P], RowConst<P>& k)
 {
     const float* __restrict__ ph2pr = lut + kOffPh2pr;
-    k.pm = lut[kOffPm + row_q(wc)];
-    k.px = lut[kOffPx + row_q(wc)];
-    k.my = ph2pr[row_d(wc)];
-    k.yy = ph2pr[row_c(wc)];
-    k.mm = lut[kOffMM + mm_idx(row_i(wn), row_d(wn))];
-    k.g = lut[kOffGapm + row_c(wn)];
-    k.mx = ph2pr[row_i(wn)];
-    k.xx = ph2pr[row_c(wn)];
-    k.rc = row_rc(wc);
-}
-
-// Match-bit words of this row's read code for the block's 64 columns.
-__device__ __forceinline__ void select_mask(const uint32_t (&m)[10], int rc, uint32_t& lo, uint32_t& hi)
-{
-    lo = m[0];
-    hi = m[1];
 #pragma unroll
-    for (int c = 1; c < 5; ++c) {
-        lo = (rc == c) ? m[2 * c] : lo;
-        hi = (rc == c) ? m[2 * c + 1] : hi;
+    for (int p = 0; p < P; ++p) {
+        set_comp(k.pm, p, lut[kOffPm + row_q(wc[p])]);
+        set_comp(k.px, p, lut[kOffPx + row_q(wc[p])]);
+        set_comp(k.my, p, ph2pr[row_d(wc[p])]);
+        set_comp(k.yy, p, ph2pr[row_c(wc[p])]);
+        set_comp(k.mm, p, lut[kOffMM + mm_idx(row_i(wn[p]), row_d(wn[p]))]);
+        set_comp(k.g, p, lut[kOffGapm + row_c(wn[p])]);
+        set_comp(k.mx, p, ph2pr[row_i(wn[p])]);
+        set_comp(k.xx, p, ph2pr[row_c(wn[p])]);
+        k.rc[p] = row_rc(wc[p]);
     }
 }
 
-// Prior of column bit `B` (MSB-first) of the row's match word: 2 VALU ops,
-// v_bfe_i32 (bit -> 0 / -1) and v_bfi_b32 (select pm / px bits). The asm keeps
-// the compiler from turning it into and + cmp + cndmask (3 ops + s_nop).
+// Prior of column bit `B` (MSB-first) of a match word: 2 VALU ops, v_bfe_i32
+// (bit -> 0 / -1) and v_bitop3/v_bfi (select pm / px bits). The asm keeps the
+// compiler from turning it into and + cmp + cndmask (3 ops + s_nop).
 template <int B>
 __device__ __forceinline__ float prior_of(uint32_t w, int pmi, int pxi)
 {
@@ -70,108 +84,149 @@ __device__ __forceinline__ float prior_of(uint32_t w, int pmi, int pxi)
     return __int_as_float((t & pmi) | (~t & pxi));
 }
 
-struct RowIO {
-    float Tdiag;   // in: T of the previous row at column c0 (block-local column -1)
-    float Yfirst;  // in: Y of this row at the block's first column
-    float Tout;    // out: T of this row at the block's last column
-    float Yout;    // out: Y of this row at the column after the block
-};
+template <int P, int J>
+__device__ __forceinline__ typename VT<P>::type prior_vec(const uint32_t (&mw)[P][2], const int (&pmi)[P],
+                                                       const int (&pxi)[P])
+{
+    typename VT<P>::type prior;
+#pragma unroll
+    for (int p = 0; p < P; ++p) set_comp(prior, p, prior_of<31 - (J & 31)>(mw[p][J >> 5], pmi[p], pxi[p]));
+    return prior;
+}
 
 // Column J of one row of one block; recursion unrolls the row at compile time.
-template <int J, int NC, bool SUM>
-__device__ __forceinline__ void cell(float (&T)[kLaneBlock], float (&X)[kLaneBlock], float& Tdiag,
-                                     float& Ml, float& Yl, uint32_t mlo, uint32_t mhi, int pmi, int pxi,
-                                     const RowConst& k, int lim, float& sumM, float& sumX)
+// M enters as M[i][c0+J+1] (= T_old[J-1] * prior). Before T[J] is overwritten,
+// its old value (the next column's diagonal) is consumed into the next M, so
+// the new T[J] can take the old one's register: no copies between rows.
+// mw[p][w]: match words of pair p for this row (w = 0, 1 for 64 columns).
+template <int P, int J, int NC, bool SUM>
+__device__ __forceinline__ void cell(typename VT<P>::type (&T)[64 / P], typename VT<P>::type (&X)[64 / P],
+                                     typename VT<P>::type M, typename VT<P>::type& Ml,
+                                     typename VT<P>::type& Yl, const uint32_t (&mw)[P][2],
+                                     const int (&pmi)[P], const int (&pxi)[P], const RowConst<P>& k,
+                                     const int (&lim)[P], typename VT<P>::type& sumM,
+                                     typename VT<P>::type& sumX)
 {
+    using V = typename VT<P>::type;
     if constexpr (J < NC) {
-        const float prior = prior_of<31 - (J & 31)>(J < 32 ? mlo : mhi, pmi, pxi);
-        const float M = Tdiag * prior;
-        Tdiag = T[J];
-        const float Xc = X[J];
-        const float Y = (J == 0) ? Yl : (Ml * k.my + Yl * k.yy);
+        V Mn = M;
+        if constexpr (J + 1 < NC) Mn = T[J] * prior_vec<P, J + 1>(mw, pmi, pxi);
+        const V Xc = X[J];
+        const V Y = (J == 0) ? Yl : (Ml * k.my + Yl * k.yy);
         T[J] = (M * k.mm + Xc * k.g) + Y * k.g;
         X[J] = M * k.mx + Xc * k.xx;
         if constexpr (SUM) {
-            const bool c = J < lim;   // column c0+J+1 <= H on the lane's last row
-            sumM = sumM + (c ? M : 0.f);
-            sumX = sumX + (c ? Xc : 0.f);
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                const bool c = J < lim[p];   // column c0+J+1 <= H on the pair's last row
+                set_comp(sumM, p, comp(sumM, p) + (c ? comp(M, p) : 0.f));
+                set_comp(sumX, p, comp(sumX, p) + (c ? comp(Xc, p) : 0.f));
+            }
         }
         Ml = M;
         Yl = Y;
-        cell<J + 1, NC, SUM>(T, X, Tdiag, Ml, Yl, mlo, mhi, pmi, pxi, k, lim, sumM, sumX);
+        cell<P, J + 1, NC, SUM>(T, X, Mn, Ml, Yl, mw, pmi, pxi, k, lim, sumM, sumX);
     }
 }
 
-// One row of one column block (columns c0+1 .. c0+NC).
-template <int NC, bool SUM>
-__device__ __forceinline__ void block_row(float (&T)[kLaneBlock], float (&X)[kLaneBlock], RowIO& io,
-                                          uint32_t mlo, uint32_t mhi, const RowConst& k, int lim,
-                                          float& sumM, float& sumX)
-{
-    float Tdiag = io.Tdiag, Ml = 0.f, Yl = io.Yfirst;
-    cell<0, NC, SUM>(T, X, Tdiag, Ml, Yl, mlo, mhi, __float_as_int(k.pm), __float_as_int(k.px), k, lim,
-                     sumM, sumX);
-    io.Tout = T[NC - 1];
-    io.Yout = Ml * k.my + Yl * k.yy;
-}
+template <int P>
+struct Carry {
+    typename VT<P>::type t, y;
+};
 
-template <int NC>
+template <int P>
+struct LaneCtx {
+    const uint32_t* rrow[P];
+    const uint32_t* hw[P];
+    int R[P], H[P];
+};
+
+template <int P, int NC>
 __device__ __forceinline__ void run_block(const LaneArgs& a, const LaneWave& wv, int lane, int b, int nb,
-                                          const uint32_t* __restrict__ rrow, const uint32_t* __restrict__ hw,
-                                          int R, int H, float T0, float& sumM, float& sumX)
+                                          const LaneCtx<P>& cx, typename VT<P>::type T0,
+                                          typename VT<P>::type& sumM, typename VT<P>::type& sumX)
 {
-    const int c0 = b * kLaneBlock;
-    // Match words of all 5 read codes for this block (rows of 5 words, MSB first).
-    const int nwpad = (H + 31) / 32 + kHapLead;
-    const int w0 = min(c0 / 32 + kHapLead, nwpad), w1 = min(c0 / 32 + kHapLead + 1, nwpad);
-    uint32_t m[10];
+    using V = typename VT<P>::type;
+    constexpr int BC = block_cols<P>();
+    const int c0 = b * BC;
+    // Match words of all 5 read codes for this block, per pair (rows of 5 words, MSB first).
+    uint32_t m[P][5][2];
 #pragma unroll
-    for (int c = 0; c < 5; ++c) {
-        m[2 * c] = hw[w0 * 5 + c];
-        m[2 * c + 1] = hw[w1 * 5 + c];
-    }
-    float T[kLaneBlock], X[kLaneBlock];
+    for (int p = 0; p < P; ++p) {
+        const int nwpad = (cx.H[p] + 31) / 32 + kHapLead;
+        const int w0 = min(c0 / 32 + kHapLead, nwpad), w1 = min(c0 / 32 + kHapLead + 1, nwpad);
 #pragma unroll
-    for (int j = 0; j < kLaneBlock; ++j) {
-        T[j] = T0;    // row 0: (0*mm + 0*gapm) + (INITIAL/H)*gapm, every column
-        X[j] = 0.f;   // X[1][j] = 0*mx + 0*xx
+        for (int c = 0; c < 5; ++c) {
+            m[p][c][0] = cx.hw[p][w0 * 5 + c];
+            m[p][c][1] = (BC > 32) ? cx.hw[p][w1 * 5 + c] : 0u;
+        }
     }
-    float2* __restrict__ carry = a.carry + size_t(wv.carry_row) * 64 + lane;
+    V T[64 / P], X[64 / P];
+#pragma unroll
+    for (int j = 0; j < 64 / P; ++j) {
+        T[j] = T0;           // row 0: (0*mm + 0*gapm) + (INITIAL/H)*gapm, every column
+        X[j] = splat<V>(0.f);   // X[1][j] = 0*mx + 0*xx
+    }
+    Carry<P>* __restrict__ carry = reinterpret_cast<Carry<P>*>(a.carry) + size_t(wv.carry_row) * 64 + lane;
     const bool has_in = b > 0, has_out = b + 1 < nb;
-    // Row 1's diagonal at column c0-1 is row 0's T (c0 = 0: column 0 of row 0, same value).
-    float Tdiag = T0;
-    uint32_t wc = rrow[0];
-    uint32_t wn = rrow[min(2, R) - 1];
-    float2 cin = has_in ? carry[64] : make_float2(0.f, 0.f);
-    // Rows before any lane's last row run without the sum; from wv.rmin on, the
-    // lanes whose row == R accumulate Σ M[R][j] and Σ X[R][j] (j ascending).
+    // Row 1's diagonal at column c0 is row 0's T (c0 = 0: column 0 of row 0, same value).
+    V Tdiag = T0;
+    uint32_t wc[P], wn[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        wc[p] = cx.rrow[p][0];
+        wn[p] = cx.rrow[p][min(2, cx.R[p]) - 1];
+    }
+    const Carry<P> zero{splat<V>(0.f), splat<V>(0.f)};
+    Carry<P> cin = has_in ? carry[64] : zero;
+    // Rows before any pair's last row run without the sum; from wv.rmin on, the
+    // pairs whose row == R accumulate Σ M[R][j] and Σ X[R][j] (j ascending).
     auto row = [&](int i, auto sum_tag) {
         constexpr bool SUM = decltype(sum_tag)::value;
-        RowConst k;
-        row_const(a.lut, wc, wn, k);
-        const uint32_t wnn = rrow[min(i + 2, R) - 1];
-        const float2 cnext = (has_in && i < wv.rmax) ? carry[size_t(i + 1) * 64] : make_float2(0.f, 0.f);
-        uint32_t mlo, mhi;
-        select_mask(m, k.rc, mlo, mhi);
-        RowIO io;
-        io.Tdiag = Tdiag;
-        io.Yfirst = cin.y;   // block 0: Y[i][1] = 0*my + 0*yy = 0
-        const int lim = (SUM && i == R) ? H - c0 : 0;
-        block_row<NC, SUM>(T, X, io, mlo, mhi, k, lim, sumM, sumX);
-        if (has_out) carry[size_t(i) * 64] = make_float2(io.Tout, io.Yout);
+        RowConst<P> k;
+        row_const<P>(a.lut, wc, wn, k);
+        uint32_t wnn[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) wnn[p] = cx.rrow[p][min(i + 2, cx.R[p]) - 1];
+        const Carry<P> cnext = (has_in && i < wv.rmax) ? carry[size_t(i + 1) * 64] : zero;
+        uint32_t mw[P][2];
+        int pmi[P], pxi[P], lim[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            mw[p][0] = m[p][0][0];
+            mw[p][1] = m[p][0][1];
+#pragma unroll
+            for (int c = 1; c < 5; ++c) {
+                mw[p][0] = (k.rc[p] == c) ? m[p][c][0] : mw[p][0];
+                mw[p][1] = (k.rc[p] == c) ? m[p][c][1] : mw[p][1];
+            }
+            pmi[p] = __float_as_int(comp(k.pm, p));
+            pxi[p] = __float_as_int(comp(k.px, p));
+            lim[p] = (SUM && i == cx.R[p]) ? cx.H[p] - c0 : 0;
+        }
+        V Ml = splat<V>(0.f), Yl = cin.y;   // block 0: Y[i][1] = 0*my + 0*yy = 0
+        const V M0 = Tdiag * prior_vec<P, 0>(mw, pmi, pxi);
+        cell<P, 0, NC, SUM>(T, X, M0, Ml, Yl, mw, pmi, pxi, k, lim, sumM, sumX);
+        if (has_out) carry[size_t(i) * 64] = Carry<P>{T[NC - 1], Ml * k.my + Yl * k.yy};
         // next row's diagonal at column c0: this row's T there (block 0: column 0 -> 0)
-        Tdiag = has_in ? cin.x : 0.f;
+        Tdiag = has_in ? cin.t : splat<V>(0.f);
         cin = cnext;
-        wc = wn;
-        wn = wnn;
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            wc[p] = wn[p];
+            wn[p] = wnn[p];
+        }
     };
     int i = 1;
     for (; i < wv.rmin; ++i) row(i, std::false_type{});
     for (; i <= wv.rmax; ++i) row(i, std::true_type{});
 }
 
+template <int P>
 __global__ __launch_bounds__(256) void phmm_lane_kernel(LaneArgs a)
 {
+    using V = typename VT<P>::type;
+    constexpr int BC = block_cols<P>();
     const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (wid >= a.n_waves) return;
     const int lane = threadIdx.x & 63;
@@ -188,49 +243,64 @@ __global__ __launch_bounds__(256) void phmm_lane_kernel(LaneArgs a)
         const unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(w.carry_row >> 32));
         wv.carry_row = (long long)(((unsigned long long)hi << 32) | lo);
     }
-    const int slot = wv.slot0 + lane;
-    const bool active = slot < a.n_slots;
-    const int pid = a.order[active ? slot : wv.slot0];
-    const PairDesc pd = a.pairs[pid];
-    const int R = pd.y, H = pd.w;
-    const uint32_t* __restrict__ rrow = a.rows + pd.x;
-    const uint32_t* __restrict__ hw = a.hapw + pd.z;
-
-    float T0;
-    {
-        const uint32_t w1 = rrow[0];
+    LaneCtx<P> cx;
+    int pid[P];
+    bool active[P];
+    V T0;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        const int slot = wv.slot0 + lane * P + p;
+        active[p] = slot < a.n_slots;
+        pid[p] = a.order[active[p] ? slot : wv.slot0];
+        const PairDesc pd = a.pairs[pid[p]];
+        cx.R[p] = pd.y;
+        cx.H[p] = pd.w;
+        cx.rrow[p] = a.rows + pd.x;
+        cx.hw[p] = a.hapw + pd.z;
+        const uint32_t w1 = cx.rrow[p][0];
         const float mm1 = a.lut[kOffMM + mm_idx(row_i(w1), row_d(w1))];
         const float g1 = a.lut[kOffGapm + row_c(w1)];
-        const float initY = 0x1p120f / float(H);
-        T0 = (0.f * mm1 + 0.f * g1) + initY * g1;
+        const float initY = 0x1p120f / float(pd.w);
+        set_comp(T0, p, (0.f * mm1 + 0.f * g1) + initY * g1);
     }
-    float sumM = 0.f, sumX = 0.f;
-    const int nb = (wv.ncols + kLaneBlock - 1) / kLaneBlock;
-    const int tail = wv.ncols - (nb - 1) * kLaneBlock;   // 16, 32, 48 or 64
-    for (int b = 0; b + 1 < nb; ++b)
-        run_block<64>(a, wv, lane, b, nb, rrow, hw, R, H, T0, sumM, sumX);
-    switch (tail) {
-    case 16: run_block<16>(a, wv, lane, nb - 1, nb, rrow, hw, R, H, T0, sumM, sumX); break;
-    case 32: run_block<32>(a, wv, lane, nb - 1, nb, rrow, hw, R, H, T0, sumM, sumX); break;
-    case 48: run_block<48>(a, wv, lane, nb - 1, nb, rrow, hw, R, H, T0, sumM, sumX); break;
-    default: run_block<64>(a, wv, lane, nb - 1, nb, rrow, hw, R, H, T0, sumM, sumX); break;
+    V sumM = splat<V>(0.f), sumX = splat<V>(0.f);
+    const int nb = (wv.ncols + BC - 1) / BC;
+    const int tail = wv.ncols - (nb - 1) * BC;   // multiple of 16, <= BC
+    for (int b = 0; b + 1 < nb; ++b) run_block<P, BC>(a, wv, lane, b, nb, cx, T0, sumM, sumX);
+    if constexpr (BC == 64) {
+        switch (tail) {
+        case 16: run_block<P, 16>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX); break;
+        case 32: run_block<P, 32>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX); break;
+        case 48: run_block<P, 48>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX); break;
+        default: run_block<P, 64>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX); break;
+        }
+    } else {
+        if (tail == 16) run_block<P, 16>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX);
+        else run_block<P, 32>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX);
     }
-    if (active) {
-        const float raw = sumM + sumX;
-        a.raw_out[pid] = raw;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        if (!active[p]) continue;
+        const float raw = comp(sumM, p) + comp(sumX, p);
+        a.raw_out[pid[p]] = raw;
         const bool resc = raw < 1e-28f;   // MIN_ACCEPTED, pairhmm_common.h:16
-        a.rescue_flag[pid] = resc;
-        if (resc) a.rescue_list[atomicAdd(a.rescue_count, 1)] = pid;
+        a.rescue_flag[pid[p]] = resc;
+        if (resc) a.rescue_list[atomicAdd(a.rescue_count, 1)] = pid[p];
     }
 }
 
 }  // namespace
 
-hipError_t launch_lane_f32(const LaneArgs& a, hipStream_t s)
+int lane_block_cols(int P) { return P == 1 ? block_cols<1>() : block_cols<2>(); }
+
+hipError_t launch_lane_f32(int P, const LaneArgs& a, hipStream_t s)
 {
     if (a.n_waves <= 0) return hipSuccess;
     const int grid = (a.n_waves + 3) / 4;
-    hipLaunchKernelGGL(phmm_lane_kernel, dim3(grid), dim3(256), 0, s, a);
+    if (P == 2)
+        hipLaunchKernelGGL(phmm_lane_kernel<2>, dim3(grid), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(phmm_lane_kernel<1>, dim3(grid), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -7,13 +7,15 @@ import workloads as W
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = ["diag", "lane"]
+KERNELS = ["diag", "lane", "lane1"]
 
 
 @pytest.fixture(params=KERNELS)
 def kernel(request, monkeypatch):
-    """Force one of the two fp32 kernels (anti-diagonal / lane-per-pair)."""
-    monkeypatch.setenv("HC_PHMM_KERNEL", request.param)
+    """Force one fp32 kernel: anti-diagonal, lane-per-pair packed (2 pairs per
+    lane, v_pk_*), or lane-per-pair scalar (1 pair per lane)."""
+    monkeypatch.setenv("HC_PHMM_KERNEL", "diag" if request.param == "diag" else "lane")
+    monkeypatch.setenv("HC_PHMM_LANE_P", "1" if request.param == "lane1" else "2")
     return request.param
 
 
