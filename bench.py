@@ -221,6 +221,23 @@ def main():
                              gcups=round(W.cells(b2) / (s2.run_ms * 1e-3) / 1e9, 2),
                              rescued=int(s2.n_rescued))
             bb.close()
+        # One active region, the real call shape of IntelPairHMM::compute_likelihoods:
+        # 415 reads x n haps, hap ~415 bp, read 150 bp; host buffers in, doubles out.
+        for nh in (32, 128):
+            reads, haps = W.region(415, nh)
+            hcphmm.cross(reads, haps)
+            t0 = time.perf_counter()
+            reps = 5
+            for _ in range(reps):
+                hcphmm.cross(reads, haps)
+            dt = (time.perf_counter() - t0) / reps
+            flat = W.region_flat(reads, haps)
+            ent = dict(reads=len(reads), haps=nh, cells=W.cells(flat), call_ms=round(dt * 1e3, 3),
+                       gcups=round(W.cells(flat) / dt / 1e9, 2))
+            if not args.no_cpu:
+                c1, _ = cpu_baseline(flat, 1, 1, "same region, 1 thread")
+                ent["cpu_reference_1core_ms"] = round(c1["seconds"] * 1e3, 1)
+            sec[f"region_415x{nh}"] = ent
         out["secondary"] = sec
     if world > 1:
         out["gather"] = "dist.gather (RCCL) of raw_f32 + raw_f64 per step"

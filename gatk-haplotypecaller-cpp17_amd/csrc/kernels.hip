@@ -64,18 +64,71 @@ __device__ __forceinline__ double shr1(double src, double old)
     return __longlong_as_double((long long)((unsigned long long)(unsigned)hi << 32 | (unsigned)lo));
 }
 
-// Prior for the column whose match bit is the window's MSB; shifts the window.
-template <typename T>
-__device__ __forceinline__ T take_prior(uint32_t& win, T pm, T px)
+// Prior of the column whose match bit is bit B (MSB first) of the lane's 32-bit
+// window: v_bfe_i32 (bit -> 0 / -1) + one bit-select (v_bitop3 / v_cndmask).
+template <int B>
+__device__ __forceinline__ float take_prior(uint32_t win, float pm, float px)
 {
-    const T p = (int)win < 0 ? pm : px;
-    win <<= 1;
-    return p;
+    int t;
+    asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(t) : "v"(win), "i"(B));
+    return __int_as_float((t & __float_as_int(pm)) | (~t & __float_as_int(px)));
+}
+template <int B>
+__device__ __forceinline__ double take_prior(uint32_t win, double pm, double px)
+{
+    return int(win << (31 - B)) < 0 ? pm : px;
 }
 
 template <typename T> __device__ __forceinline__ T initial_constant();
 template <> __device__ __forceinline__ float initial_constant<float>() { return 0x1p120f; }
 template <> __device__ __forceinline__ double initial_constant<double>() { return 0x1p1020; }
+
+// One anti-diagonal step (column t - l for lane l). S = step index inside the
+// 32-step window (compile time), so the prior bit is a constant.
+template <typename T, int W, bool SUM, int S>
+__device__ __forceinline__ void diag_step(Pair2<T>* __restrict__ wp, const Pair2<T>& rv, uint32_t win, int l,
+                                          int lim, int t, T pm, T px, T my, T yy, T mm1, T g1, T mx1,
+                                          T xx1, T& Ml, T& Yl, T& shT2, T& shT1, T& shX, T& sumM, T& sumX)
+{
+    const T prior = take_prior<31 - S>(win, pm, px);
+    const T M = shT2 * prior;
+    const T X = shX;
+    const T Y = Ml * my + Yl * yy;
+    const T Tn = (M * mm1 + X * g1) + Y * g1;
+    const T XN = M * mx1 + X * xx1;
+    shT2 = shT1;
+    shT1 = shr1<W>(Tn, rv.t);
+    shX = shr1<W>(XN, rv.xn);
+    if (l == W - 1) *wp = Pair2<T>{Tn, XN};   // column t-W+1 (+W offset)
+    Ml = M;
+    Yl = Y;
+    if constexpr (SUM) {
+        const bool c = t <= lim;   // lane holds row R and column t-l <= H
+        sumM = sumM + (c ? M : T(0));
+        sumX = sumX + (c ? X : T(0));
+    }
+}
+
+// Eight steps starting at step t0 + U. Returns false when the stripe ended first.
+template <typename T, int W, bool SUM, int U>
+__device__ __forceinline__ bool sub_block(Pair2<T>* __restrict__ ring, int t0, int nsteps, uint32_t win, int l,
+                                          int lim, T pm, T px, T my, T yy, T mm1, T g1, T mx1, T xx1,
+                                          T& Ml, T& Yl, T& shT2, T& shT1, T& shX, T& sumM, T& sumX)
+{
+    if (t0 + U > nsteps) return false;
+    Pair2<T>* rp = ring + (t0 + U);
+    // Carry-ins of lane 0 for the next 8 columns, read in one batch: they were
+    // written a whole stripe ago and are overwritten only W steps from now.
+    Pair2<T> rv[8];
+#pragma unroll
+    for (int v = 0; v < 8; ++v) rv[v] = rp[v + W + 1];
+    const int t = t0 + U;
+#define HC_STEP(v) diag_step<T, W, SUM, U + v>(rp + v + 1, rv[v], win, l, lim, t + v, pm, px, my, yy, mm1, \
+                                              g1, mx1, xx1, Ml, Yl, shT2, shT1, shX, sumM, sumX)
+    HC_STEP(0); HC_STEP(1); HC_STEP(2); HC_STEP(3); HC_STEP(4); HC_STEP(5); HC_STEP(6); HC_STEP(7);
+#undef HC_STEP
+    return true;
+}
 
 template <typename T, int W, bool SUM>
 __device__ __forceinline__ void run_stripe(
@@ -88,39 +141,22 @@ __device__ __forceinline__ void run_stripe(
     T shT2 = (l == 0) ? r0.t : T(0);   // T of row above at column j-1 (diagonal)
     T shT1 = (l == 0) ? r1.t : T(0);   // ... one step younger
     T shX = (l == 0) ? r1.xn : T(0);   // X of this row at column j (from row above)
+    const int lim = last ? H + l : -1;
     for (int t0 = 1; t0 <= nsteps; t0 += 32) {
         // 32-column match window starting at this lane's column j0 = t0 - l.
         const int k = t0 - 1 - l;
         const int wi = k >> 5, sh = k & 31;
         const int a0 = min(wi + kHapLead, nwpad), a1 = min(wi + kHapLead + 1, nwpad);
         const uint32_t hiw = hw[a0 * 5 + rc], low = hw[a1 * 5 + rc];
-        uint32_t win = sh ? ((hiw << sh) | (low >> (32 - sh))) : hiw;
-#pragma unroll
-        for (int u = 0; u < 32; u += 8) {
-            if (t0 + u > nsteps) break;
-            Pair2<T>* rp = ring + (t0 + u);
-#pragma unroll
-            for (int v = 0; v < 8; ++v) {
-                const T prior = take_prior<T>(win, pm, px);
-                const T M = shT2 * prior;
-                const T X = shX;
-                const T Y = Ml * my + Yl * yy;
-                const T Tn = (M * mm1 + X * g1) + Y * g1;
-                const T XN = M * mx1 + X * xx1;
-                const Pair2<T> rv = rp[v + W + 1];   // carry-in for lane 0: column t+1
-                shT2 = shT1;
-                shT1 = shr1<W>(Tn, rv.t);
-                shX = shr1<W>(XN, rv.xn);
-                if (l == W - 1) rp[v + 1] = Pair2<T>{Tn, XN};   // column t-W+1 (+W offset)
-                Ml = M;
-                Yl = Y;
-                if constexpr (SUM) {
-                    const bool c = last && (t0 + u + v - l <= H);
-                    sumM = sumM + (c ? M : T(0));
-                    sumX = sumX + (c ? X : T(0));
-                }
-            }
-        }
+        const uint32_t win = sh ? ((hiw << sh) | (low >> (32 - sh))) : hiw;
+        if (!sub_block<T, W, SUM, 0>(ring, t0, nsteps, win, l, lim, pm, px, my, yy, mm1, g1, mx1, xx1,
+                                     Ml, Yl, shT2, shT1, shX, sumM, sumX)) break;
+        if (!sub_block<T, W, SUM, 8>(ring, t0, nsteps, win, l, lim, pm, px, my, yy, mm1, g1, mx1, xx1,
+                                     Ml, Yl, shT2, shT1, shX, sumM, sumX)) break;
+        if (!sub_block<T, W, SUM, 16>(ring, t0, nsteps, win, l, lim, pm, px, my, yy, mm1, g1, mx1, xx1,
+                                      Ml, Yl, shT2, shT1, shX, sumM, sumX)) break;
+        if (!sub_block<T, W, SUM, 24>(ring, t0, nsteps, win, l, lim, pm, px, my, yy, mm1, g1, mx1, xx1,
+                                      Ml, Yl, shT2, shT1, shX, sumM, sumX)) break;
     }
 }
 

@@ -151,3 +151,43 @@ def edge_pairs(seed=7, variants=4):
                     c = rng.integers(10, 60, R).astype(np.uint8)
                 out.append((rs.tobytes(), q.tobytes(), i.tobytes(), d.tobytes(), c.tobytes(), hap.tobytes()))
     return out
+
+
+def region(n_reads=415, n_haps=32, H=415, R=150, subst=0.01, seed=45):
+    """One active-region-shaped cross product (SURVEY §8(d) 'cross-product variant'):
+    n_haps haplotypes of length ~H that differ from a common base by a few SNPs
+    and small indels, n_reads reads of length R drawn from them with `subst`
+    substitutions. Returns (reads, haps) as the C ABI's cross call takes them:
+    reads = [(bases, qual, ins_gop, del_gop, gcp)], haps = [bases]."""
+    rng = np.random.default_rng(seed)
+    base = ACGT[rng.integers(0, 4, H)]
+    haps = []
+    for h in range(n_haps):
+        x = base.copy()
+        if h:
+            k = rng.integers(1, 4)
+            pos = rng.integers(0, H, k)
+            x[pos] = ACGT[rng.integers(0, 4, k)]
+            if rng.random() < 0.5:
+                p = int(rng.integers(10, H - 10))
+                if rng.random() < 0.5:
+                    x = np.concatenate([x[:p], ACGT[rng.integers(0, 4, int(rng.integers(1, 6)))], x[p:]])
+                else:
+                    x = np.concatenate([x[:p], x[p + int(rng.integers(1, 6)):]])
+        haps.append(x.tobytes())
+    reads = []
+    for r in range(n_reads):
+        src = np.frombuffer(haps[int(rng.integers(0, n_haps))], np.uint8)
+        o = int(rng.integers(0, max(1, len(src) - R + 1)))
+        rs = src[o:o + R].copy()
+        sub = rng.random(len(rs)) < subst
+        rs[sub] = ACGT[(np.searchsorted(ACGT, rs[sub]) + rng.integers(1, 4, int(sub.sum()))) % 4]
+        q = (rng.integers(10, 41, len(rs)) + 33).astype(np.uint8)
+        n = len(rs)
+        reads.append((rs.tobytes(), q.tobytes(), bytes([GOP]) * n, bytes([GOP]) * n, bytes([GCP]) * n))
+    return reads, haps
+
+
+def region_flat(reads, haps):
+    """Expand a region's cross product into a flat batch (read-major pairs)."""
+    return from_pairs([(r[0], r[1], r[2], r[3], r[4], h) for r in reads for h in haps])
