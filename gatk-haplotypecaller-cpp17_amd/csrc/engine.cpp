@@ -138,7 +138,7 @@ struct hc_phmm_batch {
     // Lane-per-pair class (large batches).
     int n_lane = 0;
     int lane_waves = 0;
-    int lane_p = 1;   // pairs per lane of the lane kernel
+    int lane_variant = 0;   // lane kernel variant (kernels.hpp LaneVariant)
     int* d_lane_order = nullptr;
     LaneWave* d_lane_waves = nullptr;
     float2* d_carry = nullptr;
@@ -171,12 +171,12 @@ constexpr int kW64Threshold = 768;   // H above this -> one pair per wave (W = 6
 constexpr int64_t kLaneMinPairs = 32768;   // batches this large use the lane-per-pair kernel
 constexpr int kLaneMaxH = 4096;            // longer haps stay on the anti-diagonal kernel
 
-// Pairs per lane of the lane kernel: HC_PHMM_LANE_P=1|2 (default 2: packed f32).
-int lane_pairs_per_lane()
+// Lane kernel variant (kernels.hpp LaneVariant): HC_PHMM_LANE_VARIANT=<id>,
+// default 0 = {1 pair per lane, 64-column blocks, 3 waves per SIMD}.
+int lane_variant_id()
 {
-    const char* e = std::getenv("HC_PHMM_LANE_P");
-    if (e && *e == '1') return 1;
-    return 2;
+    const char* e = std::getenv("HC_PHMM_LANE_VARIANT");
+    return (e && *e) ? std::atoi(e) : 0;
 }
 
 // Kernel selection: HC_PHMM_KERNEL=auto (default) | lane | diag.
@@ -317,7 +317,9 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     sort_desc(lane_ord, key);
     std::vector<LaneWave> lw;
     int64_t carry_rows = 0;
-    const int lane_p = lane_pairs_per_lane();
+    const int lane_var = lane_variant_id();
+    const LaneVariant& LV = lane_variant(lane_var);
+    const int lane_p = LV.P;
     const size_t per_wave = size_t(64) * lane_p;
     for (size_t s0 = 0; s0 < lane_ord.size(); s0 += per_wave) {
         LaneWave w{};
@@ -332,7 +334,7 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
             w.ncols = std::max(w.ncols, cols16(p));
         }
         w.carry_row = carry_rows;
-        if (w.ncols > lane_block_cols(lane_p)) carry_rows += w.rmax + 1;
+        if (w.ncols > LV.BC) carry_rows += w.rmax + 1;
         lw.push_back(w);
     }
     // Anti-diagonal classes: W by H; (stripes, H) descending so the G pairs
@@ -443,7 +445,7 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     b->cells = cells;
     b->Hmax = Hmax;
     b->n_lane = int(lane_ord.size());
-    b->lane_p = lane_p;
+    b->lane_variant = lane_var;
     b->lane_waves = int(lw.size());
     b->d_pairs = reinterpret_cast<PairDesc*>(dev + o_pairs);
     b->d_rows = reinterpret_cast<uint32_t*>(dev + o_rows);
@@ -498,7 +500,7 @@ int run(hc_phmm_batch* b, hipStream_t s)
         a.rescue_list = b->d_list;
         a.rescue_count = b->d_count;
         b->launch_waves += b->lane_waves;
-        HIP_TRY(launch_lane_f32(b->lane_p, a, s));
+        HIP_TRY(launch_lane_f32(b->lane_variant, a, s));
     }
     for (auto& c : b->cls) {
         if (c.n == 0) continue;

@@ -72,9 +72,14 @@ struct LaneArgs {
     int* rescue_list;
     int* rescue_count;
 };
-// P = pairs per lane (1, or 2 packed in float2 halves); block columns 64 / P*... see lane_block_cols.
-hipError_t launch_lane_f32(int P, const LaneArgs& a, hipStream_t s);
-int lane_block_cols(int P);
+// Variants of the lane kernel (lane_kernel.hip kVariants): pairs per lane P
+// (1, or 2 packed in float2 halves), register block width in columns, and the
+// waves per SIMD the register allocation targets. Variant 0 is the default.
+struct LaneVariant {
+    int P, BC, occ;
+};
+const LaneVariant& lane_variant(int id);
+hipError_t launch_lane_f32(int variant, const LaneArgs& a, hipStream_t s);
 
 // Launchers (kernels.hip). W = lanes per pair: 16, 32 or 64.
 hipError_t launch_diag_f32(int W, const DiagArgs& a, int grid, hipStream_t s);

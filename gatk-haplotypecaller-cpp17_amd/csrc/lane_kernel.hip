@@ -42,8 +42,6 @@ __device__ __forceinline__ void set_comp(f2& v, int p, float s)
 }
 template <typename V> __device__ __forceinline__ V splat(float s) { return V(s); }
 
-// Columns per register block: 64 state pairs of registers either way.
-template <int P> constexpr int block_cols() { return P == 1 ? 64 : 32; }
 
 template <int P>
 struct RowConst {
@@ -99,8 +97,8 @@ __device__ __forceinline__ typename VT<P>::type prior_vec(const uint32_t (&mw)[P
 // its old value (the next column's diagonal) is consumed into the next M, so
 // the new T[J] can take the old one's register: no copies between rows.
 // mw[p][w]: match words of pair p for this row (w = 0, 1 for 64 columns).
-template <int P, int J, int NC, bool SUM>
-__device__ __forceinline__ void cell(typename VT<P>::type (&T)[64 / P], typename VT<P>::type (&X)[64 / P],
+template <int P, int BC, int J, int NC, bool SUM>
+__device__ __forceinline__ void cell(typename VT<P>::type (&T)[BC], typename VT<P>::type (&X)[BC],
                                      typename VT<P>::type M, typename VT<P>::type& Ml,
                                      typename VT<P>::type& Yl, const uint32_t (&mw)[P][2],
                                      const int (&pmi)[P], const int (&pxi)[P], const RowConst<P>& k,
@@ -125,7 +123,7 @@ __device__ __forceinline__ void cell(typename VT<P>::type (&T)[64 / P], typename
         }
         Ml = M;
         Yl = Y;
-        cell<P, J + 1, NC, SUM>(T, X, Mn, Ml, Yl, mw, pmi, pxi, k, lim, sumM, sumX);
+        cell<P, BC, J + 1, NC, SUM>(T, X, Mn, Ml, Yl, mw, pmi, pxi, k, lim, sumM, sumX);
     }
 }
 
@@ -141,13 +139,12 @@ struct LaneCtx {
     int R[P], H[P];
 };
 
-template <int P, int NC>
+template <int P, int BC, int NC>
 __device__ __forceinline__ void run_block(const LaneArgs& a, const LaneWave& wv, int lane, int b, int nb,
                                           const LaneCtx<P>& cx, typename VT<P>::type T0,
                                           typename VT<P>::type& sumM, typename VT<P>::type& sumX)
 {
     using V = typename VT<P>::type;
-    constexpr int BC = block_cols<P>();
     const int c0 = b * BC;
     // Match words of all 5 read codes for this block, per pair (rows of 5 words, MSB first).
     uint32_t m[P][5][2];
@@ -161,9 +158,9 @@ __device__ __forceinline__ void run_block(const LaneArgs& a, const LaneWave& wv,
             m[p][c][1] = (BC > 32) ? cx.hw[p][w1 * 5 + c] : 0u;
         }
     }
-    V T[64 / P], X[64 / P];
+    V T[BC], X[BC];
 #pragma unroll
-    for (int j = 0; j < 64 / P; ++j) {
+    for (int j = 0; j < BC; ++j) {
         T[j] = T0;           // row 0: (0*mm + 0*gapm) + (INITIAL/H)*gapm, every column
         X[j] = splat<V>(0.f);   // X[1][j] = 0*mx + 0*xx
     }
@@ -206,7 +203,7 @@ __device__ __forceinline__ void run_block(const LaneArgs& a, const LaneWave& wv,
         }
         V Ml = splat<V>(0.f), Yl = cin.y;   // block 0: Y[i][1] = 0*my + 0*yy = 0
         const V M0 = Tdiag * prior_vec<P, 0>(mw, pmi, pxi);
-        cell<P, 0, NC, SUM>(T, X, M0, Ml, Yl, mw, pmi, pxi, k, lim, sumM, sumX);
+        cell<P, BC, 0, NC, SUM>(T, X, M0, Ml, Yl, mw, pmi, pxi, k, lim, sumM, sumX);
         if (has_out) carry[size_t(i) * 64] = Carry<P>{T[NC - 1], Ml * k.my + Yl * k.yy};
         // next row's diagonal at column c0: this row's T there (block 0: column 0 -> 0)
         Tdiag = has_in ? cin.t : splat<V>(0.f);
@@ -222,11 +219,10 @@ __device__ __forceinline__ void run_block(const LaneArgs& a, const LaneWave& wv,
     for (; i <= wv.rmax; ++i) row(i, std::true_type{});
 }
 
-template <int P>
-__global__ __launch_bounds__(256) void phmm_lane_kernel(LaneArgs a)
+template <int P, int BC, int OCC>
+__global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
 {
     using V = typename VT<P>::type;
-    constexpr int BC = block_cols<P>();
     const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (wid >= a.n_waves) return;
     const int lane = threadIdx.x & 63;
@@ -266,18 +262,11 @@ __global__ __launch_bounds__(256) void phmm_lane_kernel(LaneArgs a)
     V sumM = splat<V>(0.f), sumX = splat<V>(0.f);
     const int nb = (wv.ncols + BC - 1) / BC;
     const int tail = wv.ncols - (nb - 1) * BC;   // multiple of 16, <= BC
-    for (int b = 0; b + 1 < nb; ++b) run_block<P, BC>(a, wv, lane, b, nb, cx, T0, sumM, sumX);
-    if constexpr (BC == 64) {
-        switch (tail) {
-        case 16: run_block<P, 16>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX); break;
-        case 32: run_block<P, 32>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX); break;
-        case 48: run_block<P, 48>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX); break;
-        default: run_block<P, 64>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX); break;
-        }
-    } else {
-        if (tail == 16) run_block<P, 16>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX);
-        else run_block<P, 32>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX);
-    }
+    for (int b = 0; b + 1 < nb; ++b) run_block<P, BC, BC>(a, wv, lane, b, nb, cx, T0, sumM, sumX);
+    if (tail == 16) run_block<P, BC, 16>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX);
+    else if (BC >= 32 && tail == 32) run_block<P, BC, (BC >= 32 ? 32 : 16)>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX);
+    else if (BC >= 64 && tail == 48) run_block<P, BC, (BC >= 64 ? 48 : 16)>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX);
+    else run_block<P, BC, BC>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX);
 #pragma unroll
     for (int p = 0; p < P; ++p) {
         if (!active[p]) continue;
@@ -291,16 +280,30 @@ __global__ __launch_bounds__(256) void phmm_lane_kernel(LaneArgs a)
 
 }  // namespace
 
-int lane_block_cols(int P) { return P == 1 ? block_cols<1>() : block_cols<2>(); }
+// Lane kernel variants: {pairs per lane, block columns, waves per SIMD}.
+// Block widths are multiples of 32 (a block starts on a match-word boundary).
+// Measured on S2 (ms per fp32 pass): v0 11.5, v1 12.8, v2 15.6, v3 17.7.
+static const LaneVariant kVariants[] = {
+    {1, 64, 3}, {1, 64, 2}, {1, 32, 4}, {2, 32, 2},
+};
 
-hipError_t launch_lane_f32(int P, const LaneArgs& a, hipStream_t s)
+const LaneVariant& lane_variant(int id)
+{
+    const int n = int(sizeof(kVariants) / sizeof(kVariants[0]));
+    return kVariants[(id >= 0 && id < n) ? id : 0];
+}
+
+hipError_t launch_lane_f32(int id, const LaneArgs& a, hipStream_t s)
 {
     if (a.n_waves <= 0) return hipSuccess;
     const int grid = (a.n_waves + 3) / 4;
-    if (P == 2)
-        hipLaunchKernelGGL(phmm_lane_kernel<2>, dim3(grid), dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL(phmm_lane_kernel<1>, dim3(grid), dim3(256), 0, s, a);
+    const dim3 g(grid), blk(256);
+    switch ((id >= 0 && id < 4) ? id : 0) {
+    case 1: hipLaunchKernelGGL((phmm_lane_kernel<1, 64, 2>), g, blk, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((phmm_lane_kernel<1, 32, 4>), g, blk, 0, s, a); break;
+    case 3: hipLaunchKernelGGL((phmm_lane_kernel<2, 32, 2>), g, blk, 0, s, a); break;
+    default: hipLaunchKernelGGL((phmm_lane_kernel<1, 64, 3>), g, blk, 0, s, a); break;
+    }
     return hipGetLastError();
 }
 

@@ -7,15 +7,20 @@ import workloads as W
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = ["diag", "lane", "lane1"]
+# "diag" = anti-diagonal kernel; "laneN" = lane-per-pair kernel variant N
+# (lane_kernel.hip kVariants: 0 = 64-col blocks 3 waves/SIMD (default),
+# 1 = 64-col 2 waves, 2 = 32-col 4 waves, 3 = two pairs per lane, packed f32).
+KERNELS = ["diag", "lane0", "lane1", "lane2", "lane3"]
 
 
 @pytest.fixture(params=KERNELS)
 def kernel(request, monkeypatch):
-    """Force one fp32 kernel: anti-diagonal, lane-per-pair packed (2 pairs per
-    lane, v_pk_*), or lane-per-pair scalar (1 pair per lane)."""
-    monkeypatch.setenv("HC_PHMM_KERNEL", "diag" if request.param == "diag" else "lane")
-    monkeypatch.setenv("HC_PHMM_LANE_P", "1" if request.param == "lane1" else "2")
+    """Force one fp32 kernel / lane-kernel variant for the test."""
+    if request.param == "diag":
+        monkeypatch.setenv("HC_PHMM_KERNEL", "diag")
+    else:
+        monkeypatch.setenv("HC_PHMM_KERNEL", "lane")
+        monkeypatch.setenv("HC_PHMM_LANE_VARIANT", request.param[4:])
     return request.param
 
 
