@@ -290,6 +290,21 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     if (row_off[nr] > INT32_MAX || hap_off[nh] > INT32_MAX)
         return fail(HC_PHMM_EINVAL, "batch too large (row or hap pool exceeds 2^31 words)");
 
+    // Reads whose gap qualities (i, d, c) are the same on every row — always the
+    // case for the reference's SAMRecord (sam.hpp:30-32) — take the lane kernel's
+    // constant-gap path.
+    std::vector<uint8_t> read_cg(nr);
+    parallel_for(nr, [&](int64_t b, int64_t e) {
+        for (int64_t r = b; r < e; ++r) {
+            const ReadView& v = reads[r];
+            const int i0 = v.i[0] & 127, d0 = v.d[0] & 127, c0 = v.c[0] & 127;
+            bool cg = true;
+            for (int k = 1; k < v.len && cg; ++k)
+                cg = (v.i[k] & 127) == i0 && (v.d[k] & 127) == d0 && (v.c[k] & 127) == c0;
+            read_cg[r] = cg;
+        }
+    }, 1024);
+
     // Descriptors and length binning.
     std::vector<PairDesc> pd(npairs);
     int64_t cells = 0;
@@ -313,7 +328,10 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     // Lane class: bin by column coverage (H rounded up to 16), then R, both
     // descending, so a wave's 64*P pairs sweep nearly the same rows x columns.
     auto cols16 = [&](int p) { return (pd[p].w + 15) / 16 * 16; };
-    for (int p : lane_ord) key[p] = (uint32_t(cols16(p)) << 16) | uint32_t(std::min(pd[p].y, 65535));
+    // Constant-gap pairs first (bit 31) so waves are homogeneous in that too.
+    for (int p : lane_ord)
+        key[p] = (uint32_t(read_cg[pr[p]]) << 31) | (uint32_t(cols16(p)) << 16) |
+                 uint32_t(std::min(pd[p].y, 65535));
     sort_desc(lane_ord, key);
     std::vector<LaneWave> lw;
     int64_t carry_rows = 0;
@@ -327,8 +345,10 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
         w.rmax = 0;
         w.rmin = INT32_MAX;
         w.ncols = 0;
+        w.cg = 1;
         for (size_t k = s0; k < std::min(lane_ord.size(), s0 + per_wave); ++k) {
             const int p = lane_ord[k];
+            w.cg &= read_cg[pr[p]];
             w.rmax = std::max(w.rmax, pd[p].y);
             w.rmin = std::min(w.rmin, pd[p].y);
             w.ncols = std::max(w.ncols, cols16(p));

@@ -55,6 +55,8 @@ struct LaneWave {
     int rmax;       // rows swept (max R of the wave's pairs)
     int rmin;       // min R of the wave's active pairs (first row that may need the sum)
     int ncols;      // columns swept (max H rounded up to 16), <= nblk * 64
+    int cg;         // 1: every pair of the wave has constant gap qualities
+    int pad_;
     long long carry_row;  // first carry row of this wave in `carry` (units of 64 float2)
 };
 struct LaneArgs {

@@ -139,24 +139,29 @@ struct LaneCtx {
     int R[P], H[P];
 };
 
-template <int P, int BC, int NC>
+// One register block of columns c0+1 .. c0+NC for all rows of the wave.
+// CG: every pair of the wave has constant gap qualities (i, d, c identical on
+// all rows — what the reference's SAMRecord always supplies, sam.hpp:30-32), so
+// the six transition constants are per-lane registers and a row only needs its
+// prior (pm, px from q) and match word; those are fetched one row ahead.
+// mt: this wave's LDS match table [P][5 read codes][64 lanes] of 2 words.
+template <int P, int BC, int NC, bool CG>
 __device__ __forceinline__ void run_block(const LaneArgs& a, const LaneWave& wv, int lane, int b, int nb,
                                           const LaneCtx<P>& cx, typename VT<P>::type T0,
-                                          typename VT<P>::type& sumM, typename VT<P>::type& sumX)
+                                          typename VT<P>::type& sumM, typename VT<P>::type& sumX,
+                                          uint2* __restrict__ mt)
 {
     using V = typename VT<P>::type;
     const int c0 = b * BC;
-    // Match words of all 5 read codes for this block, per pair (rows of 5 words, MSB first).
-    uint32_t m[P][5][2];
+    // Match words of all 5 read codes for this block (rows of 5 words, MSB first)
+    // into LDS; each lane later reads only its own entries.
 #pragma unroll
     for (int p = 0; p < P; ++p) {
         const int nwpad = (cx.H[p] + 31) / 32 + kHapLead;
         const int w0 = min(c0 / 32 + kHapLead, nwpad), w1 = min(c0 / 32 + kHapLead + 1, nwpad);
 #pragma unroll
-        for (int c = 0; c < 5; ++c) {
-            m[p][c][0] = cx.hw[p][w0 * 5 + c];
-            m[p][c][1] = (BC > 32) ? cx.hw[p][w1 * 5 + c] : 0u;
-        }
+        for (int c = 0; c < 5; ++c)
+            mt[(p * 5 + c) * 64 + lane] = make_uint2(cx.hw[p][w0 * 5 + c], (BC > 32) ? cx.hw[p][w1 * 5 + c] : 0u);
     }
     V T[BC], X[BC];
 #pragma unroll
@@ -176,27 +181,41 @@ __device__ __forceinline__ void run_block(const LaneArgs& a, const LaneWave& wv,
     }
     const Carry<P> zero{splat<V>(0.f), splat<V>(0.f)};
     Carry<P> cin = has_in ? carry[64] : zero;
+    RowConst<P> k;
+    row_const<P>(a.lut, wc, wn, k);   // CG: the transition constants of every row
+    uint2 mrow[P];                    // this row's match words
+#pragma unroll
+    for (int p = 0; p < P; ++p) mrow[p] = mt[(p * 5 + k.rc[p]) * 64 + lane];
     // Rows before any pair's last row run without the sum; from wv.rmin on, the
     // pairs whose row == R accumulate Σ M[R][j] and Σ X[R][j] (j ascending).
     auto row = [&](int i, auto sum_tag) {
         constexpr bool SUM = decltype(sum_tag)::value;
-        RowConst<P> k;
-        row_const<P>(a.lut, wc, wn, k);
+        if constexpr (!CG) {
+            row_const<P>(a.lut, wc, wn, k);
+#pragma unroll
+            for (int p = 0; p < P; ++p) mrow[p] = mt[(p * 5 + k.rc[p]) * 64 + lane];
+        }
         uint32_t wnn[P];
 #pragma unroll
         for (int p = 0; p < P; ++p) wnn[p] = cx.rrow[p][min(i + 2, cx.R[p]) - 1];
         const Carry<P> cnext = (has_in && i < wv.rmax) ? carry[size_t(i + 1) * 64] : zero;
+        // CG: next row's prior constants and match words, issued a row ahead.
+        V pm_n, px_n;
+        uint2 m_n[P];
+        if constexpr (CG) {
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                set_comp(pm_n, p, a.lut[kOffPm + row_q(wn[p])]);
+                set_comp(px_n, p, a.lut[kOffPx + row_q(wn[p])]);
+                m_n[p] = mt[(p * 5 + row_rc(wn[p])) * 64 + lane];
+            }
+        }
         uint32_t mw[P][2];
         int pmi[P], pxi[P], lim[P];
 #pragma unroll
         for (int p = 0; p < P; ++p) {
-            mw[p][0] = m[p][0][0];
-            mw[p][1] = m[p][0][1];
-#pragma unroll
-            for (int c = 1; c < 5; ++c) {
-                mw[p][0] = (k.rc[p] == c) ? m[p][c][0] : mw[p][0];
-                mw[p][1] = (k.rc[p] == c) ? m[p][c][1] : mw[p][1];
-            }
+            mw[p][0] = mrow[p].x;
+            mw[p][1] = mrow[p].y;
             pmi[p] = __float_as_int(comp(k.pm, p));
             pxi[p] = __float_as_int(comp(k.px, p));
             lim[p] = (SUM && i == cx.R[p]) ? cx.H[p] - c0 : 0;
@@ -208,6 +227,12 @@ __device__ __forceinline__ void run_block(const LaneArgs& a, const LaneWave& wv,
         // next row's diagonal at column c0: this row's T there (block 0: column 0 -> 0)
         Tdiag = has_in ? cin.t : splat<V>(0.f);
         cin = cnext;
+        if constexpr (CG) {
+            k.pm = pm_n;
+            k.px = px_n;
+#pragma unroll
+            for (int p = 0; p < P; ++p) mrow[p] = m_n[p];
+        }
 #pragma unroll
         for (int p = 0; p < P; ++p) {
             wc[p] = wn[p];
@@ -217,6 +242,20 @@ __device__ __forceinline__ void run_block(const LaneArgs& a, const LaneWave& wv,
     int i = 1;
     for (; i < wv.rmin; ++i) row(i, std::false_type{});
     for (; i <= wv.rmax; ++i) row(i, std::true_type{});
+}
+
+template <int P, int BC, bool CG>
+__device__ __forceinline__ void run_pairs(const LaneArgs& a, const LaneWave& wv, int lane, const LaneCtx<P>& cx,
+                                          typename VT<P>::type T0, typename VT<P>::type& sumM,
+                                          typename VT<P>::type& sumX, uint2* __restrict__ mt)
+{
+    const int nb = (wv.ncols + BC - 1) / BC;
+    const int tail = wv.ncols - (nb - 1) * BC;   // multiple of 16, <= BC
+    for (int b = 0; b + 1 < nb; ++b) run_block<P, BC, BC, CG>(a, wv, lane, b, nb, cx, T0, sumM, sumX, mt);
+    if (tail == 16) run_block<P, BC, 16, CG>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX, mt);
+    else if (BC >= 32 && tail == 32) run_block<P, BC, (BC >= 32 ? 32 : 16), CG>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX, mt);
+    else if (BC >= 64 && tail == 48) run_block<P, BC, (BC >= 64 ? 48 : 16), CG>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX, mt);
+    else run_block<P, BC, BC, CG>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX, mt);
 }
 
 template <int P, int BC, int OCC>
@@ -235,6 +274,7 @@ __global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
         wv.rmax = __builtin_amdgcn_readfirstlane(w.rmax);
         wv.rmin = __builtin_amdgcn_readfirstlane(w.rmin);
         wv.ncols = __builtin_amdgcn_readfirstlane(w.ncols);
+        wv.cg = __builtin_amdgcn_readfirstlane(w.cg);
         const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(w.carry_row & 0xffffffffll));
         const unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(w.carry_row >> 32));
         wv.carry_row = (long long)(((unsigned long long)hi << 32) | lo);
@@ -260,13 +300,12 @@ __global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
         set_comp(T0, p, (0.f * mm1 + 0.f * g1) + initY * g1);
     }
     V sumM = splat<V>(0.f), sumX = splat<V>(0.f);
-    const int nb = (wv.ncols + BC - 1) / BC;
-    const int tail = wv.ncols - (nb - 1) * BC;   // multiple of 16, <= BC
-    for (int b = 0; b + 1 < nb; ++b) run_block<P, BC, BC>(a, wv, lane, b, nb, cx, T0, sumM, sumX);
-    if (tail == 16) run_block<P, BC, 16>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX);
-    else if (BC >= 32 && tail == 32) run_block<P, BC, (BC >= 32 ? 32 : 16)>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX);
-    else if (BC >= 64 && tail == 48) run_block<P, BC, (BC >= 64 ? 48 : 16)>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX);
-    else run_block<P, BC, BC>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX);
+    __shared__ uint2 mtab[4][P * 5 * 64];
+    uint2* mt = mtab[threadIdx.x >> 6];
+    if (wv.cg)
+        run_pairs<P, BC, true>(a, wv, lane, cx, T0, sumM, sumX, mt);
+    else
+        run_pairs<P, BC, false>(a, wv, lane, cx, T0, sumM, sumX, mt);
 #pragma unroll
     for (int p = 0; p < P; ++p) {
         if (!active[p]) continue;
