@@ -65,15 +65,18 @@ def cpu_baseline(batch, threads, reps, sample_desc):
                 sample=sample_desc, seconds=round(best, 3)), res
 
 
-def traffic_from_profiles(workload):
-    """HBM bytes per launch of the dominant kernel from a committed PMC summary
-    (profiles/*pmc*.json written by tools/pmc_summary.py), else None."""
+def traffic_from_profiles(workload, cells):
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary
+    of this workload (profiles/*pmc*<workload>*.json, tools/pmc_summary.py),
+    scaled by cells when this launch is a shard of the profiled one; else None."""
     cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc*{workload}*.json")))
     if not cands:
         return None, None
     try:
         d = json.load(open(cands[-1]))
-        return d.get("hbm_bytes_per_launch"), os.path.relpath(cands[-1], ROOT)
+        per_cell = d.get("hbm_bytes_per_cell")
+        t = int(per_cell * cells) if per_cell else d.get("hbm_bytes_per_launch")
+        return t, os.path.relpath(cands[-1], ROOT)
     except Exception:
         return None, None
 
@@ -89,6 +92,11 @@ def main():
     ap.add_argument("--cpu-reps", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip end-to-end and secondary configs")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (default); gloo only to rehearse N ranks on one GPU")
+    ap.add_argument("--check", type=int, default=0,
+                    help="rank 0 re-computes this many random pairs alone and compares them bit for bit "
+                         "with the gathered multi-rank results")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -102,12 +110,18 @@ def main():
     import shard
     import workloads as W
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    gpu = local % max(ndev, 1)   # several ranks per GPU only when rehearsing with gloo
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    gloo = args.dist_backend == "gloo"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
-    hcphmm.init(local)
+        if gloo:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    hcphmm.init(gpu)
 
     batch = W.config(args.workload, args.pairs)
     n_total = len(batch["R"])
@@ -123,14 +137,16 @@ def main():
     raw64 = torch.zeros(nmax, dtype=torch.float64, device=dev)
     flag = torch.zeros(nmax, dtype=torch.uint8, device=dev)
     bt.bind_outputs(raw32.data_ptr(), raw64.data_ptr(), flag.data_ptr())
-    g32 = [torch.empty_like(raw32) for _ in range(world)] if (world > 1 and rank == 0) else None
-    g64 = [torch.empty_like(raw64) for _ in range(world)] if (world > 1 and rank == 0) else None
+    gdev = torch.device("cpu") if gloo else dev
+    g32 = [torch.empty(nmax, dtype=torch.float32, device=gdev) for _ in range(world)] if (world > 1 and rank == 0) else None
+    g64 = [torch.empty(nmax, dtype=torch.float64, device=gdev) for _ in range(world)] if (world > 1 and rank == 0) else None
 
     def step():
         bt.run(torch.cuda.current_stream().cuda_stream)
         if world > 1:
-            dist.gather(raw32, gather_list=g32, dst=0)   # RCCL gather over xGMI
-            dist.gather(raw64, gather_list=g64, dst=0)
+            s32, s64 = (raw32.cpu(), raw64.cpu()) if gloo else (raw32, raw64)
+            dist.gather(s32, gather_list=g32, dst=0)   # RCCL gather over xGMI
+            dist.gather(s64, gather_list=g64, dst=0)
 
     for _ in range(args.warmup):
         step()
@@ -157,7 +173,7 @@ def main():
     # Dominant kernel: fp32 anti-diagonal PairHMM. Algorithmic work 12 ops/cell.
     k_ms = st.kernel_ms_f32
     achieved = FLOPS_PER_CELL * my_cells / (k_ms * 1e-3) / 1e12 if k_ms > 0 else 0.0
-    traffic, tsrc = traffic_from_profiles(args.workload)
+    traffic, tsrc = traffic_from_profiles(args.workload, my_cells)
     roofline = dict(bound="valu", achieved=round(achieved, 3), peak=VALU_PEAK_TOPS, unit="TFLOP/s",
                     frac=round(achieved / VALU_PEAK_TOPS, 4), traffic=traffic,
                     kernel=("phmm_lane_kernel" if st.n_lane_pairs == st.n_pairs else "phmm_diag_kernel<float,16>"),
@@ -240,7 +256,20 @@ def main():
             sec[f"region_415x{nh}"] = ent
         out["secondary"] = sec
     if world > 1:
-        out["gather"] = "dist.gather (RCCL) of raw_f32 + raw_f64 per step"
+        out["gather"] = f"dist.gather ({'gloo, rehearsal' if gloo else 'RCCL'}) of raw_f32 + raw_f64 per step"
+    if args.check and world > 1 and rank == 0:
+        # Reassemble batch order from the last step's gathered shards and compare a
+        # random sample with a single-process run of the same pairs.
+        full32 = np.zeros(n_total, np.float32)
+        full64 = np.zeros(n_total, np.float64)
+        for r, sh in enumerate(shards):
+            full32[sh] = g32[r][: len(sh)].cpu().numpy()
+            full64[sh] = g64[r][: len(sh)].cpu().numpy()
+        idx = np.sort(np.random.default_rng(7).choice(n_total, min(args.check, n_total), replace=False))
+        ref = hcphmm.pairs(W.subset(batch, idx))
+        ok = (np.array_equal(full32[idx].view(np.uint32), ref["raw_f32"].view(np.uint32)) and
+              np.array_equal(full64[idx].view(np.uint64), ref["raw_f64"].view(np.uint64)))
+        out["multi_rank_check"] = f"{len(idx)} pairs {'bit-exact' if ok else 'MISMATCH'}"
     bt.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
