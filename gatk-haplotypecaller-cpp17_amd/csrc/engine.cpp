@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -188,6 +189,21 @@ int kernel_policy()
     return 2;
 }
 
+// HC_PHMM_TRACE=1: per-phase host timings of plan/results on stderr.
+struct PhaseTimer {
+    bool on;
+    std::chrono::steady_clock::time_point t0;
+    PhaseTimer() : on(std::getenv("HC_PHMM_TRACE") != nullptr), t0(std::chrono::steady_clock::now()) {}
+    void mark(const char* what)
+    {
+        if (!on) return;
+        const auto t1 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[hc_phmm] %-18s %8.3f ms\n", what,
+                     std::chrono::duration<double, std::milli>(t1 - t0).count());
+        t0 = t1;
+    }
+};
+
 // Grow-only buffers reused by the synchronous entry points (no per-call
 // hipMalloc / hipHostMalloc once warm).
 struct Workspace {
@@ -243,15 +259,20 @@ void free_batch(hc_phmm_batch* b)
     delete b;
 }
 
-// LSD radix sort of `idx` by a 32-bit key, DESCENDING, stable.
+// LSD radix sort of `idx` by a 32-bit key, DESCENDING, stable: 11-bit digits
+// (cache-resident counters), passes above the largest key's top bit skipped.
 void sort_desc(std::vector<int>& idx, const std::vector<uint32_t>& key)
 {
+    if (idx.size() < 2) return;
+    uint32_t kmax = 0;
+    for (int p : idx) kmax = std::max(kmax, key[p]);
     std::vector<int> tmp(idx.size());
-    for (int shift = 0; shift < 32; shift += 16) {
-        std::vector<size_t> cnt(65537, 0);
-        for (int p : idx) ++cnt[0xffff - ((key[p] >> shift) & 0xffff) + 1];
-        for (size_t k = 1; k < cnt.size(); ++k) cnt[k] += cnt[k - 1];
-        for (int p : idx) tmp[cnt[0xffff - ((key[p] >> shift) & 0xffff)]++] = p;
+    constexpr int kBits = 11, kBuckets = 1 << kBits;
+    for (int shift = 0; shift < 32 && (kmax >> shift) != 0; shift += kBits) {
+        size_t cnt[kBuckets + 1] = {};
+        for (int p : idx) ++cnt[(kBuckets - 1 - ((key[p] >> shift) & (kBuckets - 1))) + 1];
+        for (int k = 1; k <= kBuckets; ++k) cnt[k] += cnt[k - 1];
+        for (int p : idx) tmp[cnt[kBuckets - 1 - ((key[p] >> shift) & (kBuckets - 1))]++] = p;
         idx.swap(tmp);
     }
 }
@@ -283,6 +304,7 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
                                             std::to_string(HC_PHMM_MAX_HAP_LEN) + ") or null bases");
     if (npairs > (int64_t(1) << 31) - 1) return fail(HC_PHMM_EINVAL, "too many pairs for one batch");
 
+    PhaseTimer tm;
     const int64_t nr = reads.size(), nh = haps.size();
     std::vector<int64_t> row_off(nr + 1, 0), hap_off(nh + 1, 0);
     for (int64_t r = 0; r < nr; ++r) row_off[r + 1] = row_off[r] + reads[r].len;
@@ -290,21 +312,7 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     if (row_off[nr] > INT32_MAX || hap_off[nh] > INT32_MAX)
         return fail(HC_PHMM_EINVAL, "batch too large (row or hap pool exceeds 2^31 words)");
 
-    // Reads whose gap qualities (i, d, c) are the same on every row — always the
-    // case for the reference's SAMRecord (sam.hpp:30-32) — take the lane kernel's
-    // constant-gap path.
-    std::vector<uint8_t> read_cg(nr);
-    parallel_for(nr, [&](int64_t b, int64_t e) {
-        for (int64_t r = b; r < e; ++r) {
-            const ReadView& v = reads[r];
-            const int i0 = v.i[0] & 127, d0 = v.d[0] & 127, c0 = v.c[0] & 127;
-            bool cg = true;
-            for (int k = 1; k < v.len && cg; ++k)
-                cg = (v.i[k] & 127) == i0 && (v.d[k] & 127) == d0 && (v.c[k] & 127) == c0;
-            read_cg[r] = cg;
-        }
-    }, 1024);
-
+    tm.mark("offsets");
     // Descriptors and length binning.
     std::vector<PairDesc> pd(npairs);
     int64_t cells = 0;
@@ -316,6 +324,7 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
         Hmax = std::max(Hmax, haps[h].len);
     }
     std::vector<int> ord[2], lane_ord;
+    lane_ord.reserve(npairs);
     const int pol = kernel_policy();
     const bool use_lane = pol == 1 || (pol == 0 && npairs >= kLaneMinPairs);
     for (int64_t p = 0; p < npairs; ++p) {
@@ -328,10 +337,7 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     // Lane class: bin by column coverage (H rounded up to 16), then R, both
     // descending, so a wave's 64*P pairs sweep nearly the same rows x columns.
     auto cols16 = [&](int p) { return (pd[p].w + 15) / 16 * 16; };
-    // Constant-gap pairs first (bit 31) so waves are homogeneous in that too.
-    for (int p : lane_ord)
-        key[p] = (uint32_t(read_cg[pr[p]]) << 31) | (uint32_t(cols16(p)) << 16) |
-                 uint32_t(std::min(pd[p].y, 65535));
+    for (int p : lane_ord) key[p] = (uint32_t(cols16(p)) << 16) | uint32_t(std::min(pd[p].y, 65535));
     sort_desc(lane_ord, key);
     std::vector<LaneWave> lw;
     int64_t carry_rows = 0;
@@ -345,10 +351,8 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
         w.rmax = 0;
         w.rmin = INT32_MAX;
         w.ncols = 0;
-        w.cg = 1;
         for (size_t k = s0; k < std::min(lane_ord.size(), s0 + per_wave); ++k) {
             const int p = lane_ord[k];
-            w.cg &= read_cg[pr[p]];
             w.rmax = std::max(w.rmax, pd[p].y);
             w.rmin = std::min(w.rmin, pd[p].y);
             w.ncols = std::max(w.ncols, cols16(p));
@@ -372,16 +376,28 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
         ring_len[c] = hm + 2 * W + 16;
     }
 
+    tm.mark("binning");
     // One device region: uploaded arrays first, then outputs and scratch.
+    // Host uploads raw bytes; the device packs rows and hap tables
+    // (pack_kernels.hip), so the host work is memcpy.
+    std::vector<int64_t> hb_off(nh + 1, 0);
+    for (int64_t h = 0; h < nh; ++h) hb_off[h + 1] = hb_off[h] + haps[h].len;
+    const size_t nrows = size_t(row_off[nr]);
+    const size_t stride = (nrows + 16 + 15) & ~size_t(15);   // one byte plane, padded
     Layout L;
     const size_t o_pairs = L.take(sizeof(PairDesc) * npairs);
-    const size_t o_rows = L.take(sizeof(uint32_t) * (row_off[nr] + 1));
-    const size_t o_hapw = L.take(sizeof(uint32_t) * (hap_off[nh] + 1));
+    const size_t o_raw = L.take(5 * stride);
+    const size_t o_hb = L.take(size_t(hb_off[nh]) + 16);
+    const size_t o_hd = L.take(sizeof(int4) * nh);
+    const size_t o_t0 = L.take(sizeof(long long) * nh);
+    const size_t o_rd = L.take(sizeof(int2) * nr);
     const size_t o_ord0 = L.take(sizeof(int) * ord[0].size());
     const size_t o_ord1 = L.take(sizeof(int) * ord[1].size());
     const size_t o_lord = L.take(sizeof(int) * lane_ord.size());
     const size_t o_lw = L.take(sizeof(LaneWave) * lw.size());
     const size_t upload = L.off;
+    const size_t o_rows = L.take(sizeof(uint32_t) * (nrows + 16));
+    const size_t o_hapw = L.take(sizeof(uint32_t) * (hap_off[nh] + 1));
     const size_t n1 = size_t(std::max<int64_t>(npairs, 1));
     const size_t o_raw32 = L.take(sizeof(float) * n1);
     const size_t o_raw64 = L.take(sizeof(double) * n1);
@@ -402,44 +418,40 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
         own_host = true;
     }
     if (rc) return rc;
+    tm.mark("staging alloc");
 
     // Fill the staging image (parallel over reads and haps).
     std::memcpy(host + o_pairs, pd.data(), sizeof(PairDesc) * npairs);
-    uint32_t* rows = reinterpret_cast<uint32_t*>(host + o_rows);
+    uint8_t* raw = reinterpret_cast<uint8_t*>(host + o_raw);
+    int2* rdesc = reinterpret_cast<int2*>(host + o_rd);
     parallel_for(nr, [&](int64_t b, int64_t e) {
         for (int64_t r = b; r < e; ++r) {
             const ReadView& v = reads[r];
-            uint32_t* o = rows + row_off[r];
-            for (int k = 0; k < v.len; ++k)
-                o[k] = pack_row(v.q[k], v.i[k], v.d[k], v.c[k], base_code(v.bases[k]));
+            const size_t o = size_t(row_off[r]);
+            std::memcpy(raw + o, v.bases, v.len);
+            std::memcpy(raw + stride + o, v.q, v.len);
+            std::memcpy(raw + 2 * stride + o, v.i, v.len);
+            std::memcpy(raw + 3 * stride + o, v.d, v.len);
+            std::memcpy(raw + 4 * stride + o, v.c, v.len);
+            rdesc[r] = make_int2(int(o), v.len);
         }
-    }, 256);
-    rows[row_off[nr]] = 0;
-    uint32_t* hapw = reinterpret_cast<uint32_t*>(host + o_hapw);
+    }, 1024);
+    uint8_t* hb = reinterpret_cast<uint8_t*>(host + o_hb);
+    int4* hd = reinterpret_cast<int4*>(host + o_hd);
+    long long* t0 = reinterpret_cast<long long*>(host + o_t0);
     parallel_for(nh, [&](int64_t b, int64_t e) {
         for (int64_t h = b; h < e; ++h) {
-            const HapView& v = haps[h];
-            uint32_t* t = hapw + hap_off[h];
-            std::memset(t, 0, sizeof(uint32_t) * (hap_off[h + 1] - hap_off[h]));
-            for (int j = 1; j <= v.len; ++j) {
-                const uint32_t bit = 0x80000000u >> ((j - 1) & 31);
-                uint32_t* row = t + (((j - 1) >> 5) + kHapLead) * 5;
-                const int hc = base_code(v.bases[j - 1]);
-                if (hc == 4) {
-                    for (int rcode = 0; rcode < 5; ++rcode) row[rcode] |= bit;
-                } else {
-                    row[hc] |= bit;
-                    row[4] |= bit;   // read 'N' matches every column
-                }
-            }
+            std::memcpy(hb + hb_off[h], haps[h].bases, haps[h].len);
+            hd[h] = make_int4(int(hb_off[h]), haps[h].len, int(hap_off[h]), 0);
+            t0[h] = hap_off[h] / 5;
         }
-    }, 256);
-    hapw[hap_off[nh]] = 0;
+    }, 1024);
     std::memcpy(host + o_ord0, ord[0].data(), sizeof(int) * ord[0].size());
     std::memcpy(host + o_ord1, ord[1].data(), sizeof(int) * ord[1].size());
     std::memcpy(host + o_lord, lane_ord.data(), sizeof(int) * lane_ord.size());
     std::memcpy(host + o_lw, lw.data(), sizeof(LaneWave) * lw.size());
 
+    tm.mark("pack");
     auto* b = new hc_phmm_batch();
     char* dev = nullptr;
     if (borrow_ws) {
@@ -452,11 +464,23 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
         b->dev_base = dev;
         // The workspace staging stays valid until the call returns, so only a
         // batch-owned staging buffer needs the copy to finish here.
-        const hipError_t e1 = hipMemcpyAsync(dev, host, upload, hipMemcpyHostToDevice, g_eng.stream);
+        hipError_t e1 = hipMemcpyAsync(dev, host, upload, hipMemcpyHostToDevice, g_eng.stream);
+        if (e1 == hipSuccess)
+            e1 = launch_pack_rows(reinterpret_cast<const uint8_t*>(dev + o_raw), (long long)nrows,
+                                  (long long)stride, reinterpret_cast<uint32_t*>(dev + o_rows), g_eng.stream);
+        if (e1 == hipSuccess)
+            e1 = launch_mark_cg(reinterpret_cast<uint32_t*>(dev + o_rows), reinterpret_cast<const int2*>(dev + o_rd),
+                                int(nr), g_eng.stream);
+        if (e1 == hipSuccess)
+            e1 = launch_hap_tables(reinterpret_cast<const uint8_t*>(dev + o_hb),
+                                   reinterpret_cast<const int4*>(dev + o_hd), int(nh),
+                                   reinterpret_cast<const long long*>(dev + o_t0), hap_off[nh] / 5,
+                                   reinterpret_cast<uint32_t*>(dev + o_hapw), g_eng.stream);
         const hipError_t e2 = (e1 == hipSuccess && own_host) ? hipStreamSynchronize(g_eng.stream) : e1;
         if (e2 != hipSuccess) rc = fail(HC_PHMM_EHIP, std::string("H2D: ") + hipGetErrorString(e2));
     }
     if (own_host) (void)hipHostFree(host);
+    tm.mark("device alloc+H2D");
     if (rc != HC_PHMM_OK) {
         free_batch(b);
         return rc;

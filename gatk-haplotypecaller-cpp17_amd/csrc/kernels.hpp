@@ -11,6 +11,8 @@ namespace hcphmm {
 //   bits 14-20  d  (deletion GOP byte & 127)
 //   bits 21-27  c  (gap continuation byte & 127)
 //   bits 28-30  read base code, ConvertChar (pairhmm_common.h:26-44): A0 C1 T2 G3 N4
+//   bit  31     first row of a read only: the read's gap qualities are constant
+//               (set on the device by mark_cg_kernel)
 __host__ __device__ inline uint32_t pack_row(int q, int i, int d, int c, int code)
 {
     return uint32_t(q & 127) | (uint32_t(i & 127) << 7) | (uint32_t(d & 127) << 14) |
@@ -55,8 +57,6 @@ struct LaneWave {
     int rmax;       // rows swept (max R of the wave's pairs)
     int rmin;       // min R of the wave's active pairs (first row that may need the sum)
     int ncols;      // columns swept (max H rounded up to 16), <= nblk * 64
-    int cg;         // 1: every pair of the wave has constant gap qualities
-    int pad_;
     long long carry_row;  // first carry row of this wave in `carry` (units of 64 float2)
 };
 struct LaneArgs {
@@ -88,5 +88,14 @@ hipError_t launch_diag_f32(int W, const DiagArgs& a, int grid, hipStream_t s);
 hipError_t launch_diag_f64(int W, const DiagArgs& a, int grid, hipStream_t s);
 size_t diag_lds_bytes(int W, int ring_len, bool f64);
 hipError_t configure_kernels();   // raise the dynamic-LDS limit once
+
+// Device packing (pack_kernels.hip). raw: 5 byte planes (bases, q, i, d, c) of
+// `stride` bytes (multiple of 16, 16-B aligned); haps: {byte offset, H, table
+// word offset, 0}; tab_row0: first table row of each hap (prefix sum).
+hipError_t launch_pack_rows(const uint8_t* raw, long long nrows, long long stride, uint32_t* rows,
+                            hipStream_t s);
+hipError_t launch_mark_cg(uint32_t* rows, const int2* reads, int nreads, hipStream_t s);
+hipError_t launch_hap_tables(const uint8_t* hap_bytes, const int4* haps, int nhaps, const long long* tab_row0,
+                             long long ntab_rows, uint32_t* hapw, hipStream_t s);
 
 }  // namespace hcphmm

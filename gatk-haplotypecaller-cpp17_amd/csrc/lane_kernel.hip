@@ -274,7 +274,6 @@ __global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
         wv.rmax = __builtin_amdgcn_readfirstlane(w.rmax);
         wv.rmin = __builtin_amdgcn_readfirstlane(w.rmin);
         wv.ncols = __builtin_amdgcn_readfirstlane(w.ncols);
-        wv.cg = __builtin_amdgcn_readfirstlane(w.cg);
         const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(w.carry_row & 0xffffffffll));
         const unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(w.carry_row >> 32));
         wv.carry_row = (long long)(((unsigned long long)hi << 32) | lo);
@@ -299,10 +298,16 @@ __global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
         const float initY = 0x1p120f / float(pd.w);
         set_comp(T0, p, (0.f * mm1 + 0.f * g1) + initY * g1);
     }
+    // Constant-gap tag of each read (bit 31 of its first row word, set by
+    // mark_cg_kernel); the CG path runs only if all the wave's pairs qualify.
+    bool cg = true;
+#pragma unroll
+    for (int p = 0; p < P; ++p) cg &= (cx.rrow[p][0] >> 31) != 0;
+    const bool wave_cg = __builtin_amdgcn_ballot_w64(!cg) == 0;
     V sumM = splat<V>(0.f), sumX = splat<V>(0.f);
     __shared__ uint2 mtab[4][P * 5 * 64];
     uint2* mt = mtab[threadIdx.x >> 6];
-    if (wv.cg)
+    if (wave_cg)
         run_pairs<P, BC, true>(a, wv, lane, cx, T0, sumM, sumX, mt);
     else
         run_pairs<P, BC, false>(a, wv, lane, cx, T0, sumM, sumX, mt);
