@@ -254,6 +254,15 @@ def main():
                 c1, _ = cpu_baseline(flat, 1, 1, "same region, 1 thread")
                 ent["cpu_reference_1core_ms"] = round(c1["seconds"] * 1e3, 1)
             sec[f"region_415x{nh}"] = ent
+        # Cross-region batching: 64 such regions (415 x 32) in one call.
+        regs = [W.region(415, 32, seed=1000 + k) for k in range(64)]
+        hcphmm.cross_regions(regs)
+        t0 = time.perf_counter()
+        hcphmm.cross_regions(regs)
+        dt = time.perf_counter() - t0
+        rc = sum(W.cells(W.region_flat(r, h)) for r, h in regs[:1]) * len(regs)
+        sec["regions_64x_415x32_one_call"] = dict(regions=len(regs), cells_approx=rc, call_ms=round(dt * 1e3, 2),
+                                                   gcups=round(rc / dt / 1e9, 2))
         out["secondary"] = sec
     if world > 1:
         out["gather"] = f"dist.gather ({'gloo, rehearsal' if gloo else 'RCCL'}) of raw_f32 + raw_f64 per step"

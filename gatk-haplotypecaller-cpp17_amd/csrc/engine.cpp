@@ -741,6 +741,51 @@ int hc_phmm_cross(const hc_phmm_read* reads, int32_t n_reads, const hc_phmm_hap*
     return rc;
 }
 
+int hc_phmm_cross_regions(const hc_phmm_region* regions, int32_t n_regions)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (n_regions < 0 || (n_regions > 0 && !regions)) return fail(HC_PHMM_EINVAL, "bad region list");
+    int rc = ensure_init(-1);
+    if (rc) return rc;
+    std::vector<ReadView> rv;
+    std::vector<HapView> hv;
+    std::vector<int32_t> pr, ph;
+    std::vector<int64_t> out_base;   // first pair of each region
+    for (int k = 0; k < n_regions; ++k) {
+        const hc_phmm_region& g = regions[k];
+        if (g.n_reads < 0 || g.n_haps < 0) return fail(HC_PHMM_EINVAL, "negative count in region");
+        out_base.push_back(int64_t(pr.size()));
+        if (g.n_reads == 0 || g.n_haps == 0) continue;
+        if (!g.reads || !g.haps || !g.out) return fail(HC_PHMM_EINVAL, "null pointer in region");
+        const int32_t r0 = int32_t(rv.size()), h0 = int32_t(hv.size());
+        for (int r = 0; r < g.n_reads; ++r)
+            rv.push_back(ReadView{g.reads[r].length, (const uint8_t*)g.reads[r].bases, (const uint8_t*)g.reads[r].q,
+                                  (const uint8_t*)g.reads[r].i, (const uint8_t*)g.reads[r].d,
+                                  (const uint8_t*)g.reads[r].c});
+        for (int h = 0; h < g.n_haps; ++h) hv.push_back(HapView{g.haps[h].length, (const uint8_t*)g.haps[h].bases});
+        for (int r = 0; r < g.n_reads; ++r)
+            for (int h = 0; h < g.n_haps; ++h) {
+                pr.push_back(r0 + r);
+                ph.push_back(h0 + h);
+            }
+    }
+    const int64_t np = int64_t(pr.size());
+    if (np == 0) return HC_PHMM_OK;
+    hc_phmm_batch* b = nullptr;
+    rc = plan(rv, hv, np, pr.data(), ph.data(), true, &b);
+    if (rc) return rc;
+    std::vector<double> all(np);
+    rc = run_sync(b, all.data(), nullptr, nullptr, nullptr);
+    free_batch(b);
+    if (rc) return rc;
+    for (int k = 0; k < n_regions; ++k) {
+        const hc_phmm_region& g = regions[k];
+        if (g.n_reads == 0 || g.n_haps == 0) continue;
+        std::memcpy(g.out, all.data() + out_base[k], sizeof(double) * size_t(g.n_reads) * g.n_haps);
+    }
+    return HC_PHMM_OK;
+}
+
 int hc_phmm_compute_likelihoods(const hc_phmm_read* reads, int32_t n_reads, const hc_phmm_hap* haps,
                                 int32_t n_haps, double* out, uint8_t* keep, int32_t* n_kept)
 {

@@ -53,6 +53,12 @@ class Hap(C.Structure):
     _fields_ = [("length", C.c_int32), ("bases", C.c_char_p)]
 
 
+class Region(C.Structure):
+    """hc_phmm_region: one active region's reads x haps cross product."""
+    _fields_ = [("reads", C.POINTER(Read)), ("n_reads", C.c_int32), ("haps", C.POINTER(Hap)),
+                ("n_haps", C.c_int32), ("out", C.POINTER(C.c_double))]
+
+
 class Stats(C.Structure):
     _fields_ = [("n_pairs", C.c_int64), ("cells", C.c_int64), ("n_rescued", C.c_int64),
                 ("kernel_ms_f32", C.c_double), ("kernel_ms_f64", C.c_double),
@@ -80,6 +86,7 @@ def lib():
     flat = [C.c_int64, _i64p, _i32p, _i64p, _i32p] + [_u8p] * 6
     L.hc_phmm_pairs_flat.argtypes = flat + [_f64p, _f32p, _f64p, _u8p]
     L.hc_phmm_cross.argtypes = [C.POINTER(Read), C.c_int32, C.POINTER(Hap), C.c_int32, _f64p]
+    L.hc_phmm_cross_regions.argtypes = [C.POINTER(Region), C.c_int32]
     L.hc_phmm_compute_likelihoods.argtypes = [C.POINTER(Read), C.c_int32, C.POINTER(Hap), C.c_int32,
                                               _f64p, _u8p, _i32p]
     L.hc_phmm_batch_create.argtypes = flat + [C.POINTER(C.c_void_p)]
@@ -171,6 +178,21 @@ def cross(reads, haps):
     out = np.zeros((len(reads), len(haps)), np.float64)
     _check(lib().hc_phmm_cross(ra, len(reads), ha, len(haps), _p(out, _f64p)))
     return out
+
+
+def cross_regions(regions):
+    """Many regions in one device pass: regions = [(reads, haps), ...] as for
+    :func:`cross`; returns one (n_reads, n_haps) array per region."""
+    keep, outs = [], []
+    arr = (Region * max(len(regions), 1))()
+    for k, (reads, haps) in enumerate(regions):
+        ra, ha, kk = _structs(reads, haps)
+        out = np.zeros((len(reads), len(haps)), np.float64)
+        keep.extend([ra, ha, kk])
+        outs.append(out)
+        arr[k] = Region(ra, len(reads), ha, len(haps), _p(out, _f64p))
+    _check(lib().hc_phmm_cross_regions(arr, len(regions)))
+    return outs
 
 
 def compute_likelihoods(haps, reads):

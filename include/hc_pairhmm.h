@@ -90,6 +90,21 @@ int hc_phmm_version(void);   /* major*10000 + minor*100 + patch */
 int hc_phmm_cross(const hc_phmm_read* reads, int32_t n_reads,
                   const hc_phmm_hap* haps, int32_t n_haps, double* out);
 
+/* Many active regions in one device pass (cross-region batching, SURVEY §8(f)
+ * row 2): region k is the cross product reads x haps of regions[k], written
+ * read-major to regions[k].out exactly as hc_phmm_cross would. All regions'
+ * pairs are packed, length-binned and launched together, so a caller that
+ * queues regions fills the GPU even though one region (<= 415 reads x <= 128
+ * haps in the reference, haplotypecaller.hpp:83-107) does not. */
+typedef struct hc_phmm_region {
+    const hc_phmm_read* reads;
+    int32_t n_reads;
+    const hc_phmm_hap* haps;
+    int32_t n_haps;
+    double* out;   /* n_reads * n_haps, read-major */
+} hc_phmm_region;
+int hc_phmm_cross_regions(const hc_phmm_region* regions, int32_t n_regions);
+
 /* hc_phmm_cross followed by normalize_likelihoods_and_filter_poorly_modeled_reads
  * (intel_pairhmm.hpp:24-46). out is n_reads*n_haps read-major with the cap
  * applied to every row; keep[r] = 1 for reads that survive the filter, and

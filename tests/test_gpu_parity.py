@@ -163,3 +163,16 @@ def test_s2_full_size_properties(engine):
     ref = oracle.Oracle().pairs(W.subset(b, idx), nthreads=16)
     assert_same({k: r1[k][idx] for k in r1}, ref, "S2-full-sample")
     bt.close()
+
+
+def test_cross_regions_matches_per_region_calls(engine):
+    """Cross-region batching returns exactly what one call per region returns."""
+    regions = [W.region(n_reads=int(nr), n_haps=int(nh), seed=100 + k)
+               for k, (nr, nh) in enumerate([(50, 2), (120, 8), (0, 3), (415, 32), (7, 1)])]
+    together = engine.cross_regions(regions)
+    for (reads, haps), got in zip(regions, together):
+        if not reads:
+            assert got.shape == (0, len(haps))
+            continue
+        alone = engine.cross(reads, haps)
+        assert np.array_equal(bits(got), bits(alone))
