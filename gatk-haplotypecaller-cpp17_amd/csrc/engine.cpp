@@ -468,7 +468,7 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
         if (e1 == hipSuccess)
             e1 = launch_pack_rows(reinterpret_cast<const uint8_t*>(dev + o_raw), (long long)nrows,
                                   (long long)stride, reinterpret_cast<uint32_t*>(dev + o_rows), g_eng.stream);
-        if (e1 == hipSuccess)
+        if (e1 == hipSuccess && !std::getenv("HC_PHMM_NO_CG"))   // A/B switch for the CG path
             e1 = launch_mark_cg(reinterpret_cast<uint32_t*>(dev + o_rows), reinterpret_cast<const int2*>(dev + o_rd),
                                 int(nr), g_eng.stream);
         if (e1 == hipSuccess)
