@@ -50,7 +50,10 @@ int fail(int code, const std::string& msg)
 struct Engine {
     bool ready = false;
     int device = -1;
+    int n_cu = 256;   // compute units (4 SIMDs each): sizes the lane-wave latency ceiling
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;                  // segmented lane waves run here, concurrently
+    hipEvent_t fork = nullptr, join = nullptr;   // side-stream fork / join (timing disabled)
     float* lut_f = nullptr;
     double* lut_d = nullptr;
 };
@@ -83,7 +86,11 @@ int ensure_init(int device)
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return fail(HC_PHMM_ENODEV, std::string("device is ") + prop.gcnArchName + ", need gfx950");
     HIP_TRY(configure_kernels());
+    g_eng.n_cu = std::max(1, prop.multiProcessorCount);
     HIP_TRY(hipStreamCreateWithFlags(&g_eng.stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&g_eng.side, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&g_eng.fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&g_eng.join, hipEventDisableTiming));
     const Luts& L = luts();
     HIP_TRY(hipMalloc(&g_eng.lut_f, sizeof(float) * kTableLen));
     HIP_TRY(hipMalloc(&g_eng.lut_d, sizeof(double) * kTableLen));
@@ -138,6 +145,7 @@ struct hc_phmm_batch {
     } cls[2];
     // Lane-per-pair class (large batches).
     int n_lane = 0;
+    int n_seg_waves = 0;
     int lane_waves = 0;
     int lane_variant = 0;   // lane kernel variant (kernels.hpp LaneVariant)
     int* d_lane_order = nullptr;
@@ -178,6 +186,16 @@ int lane_variant_id()
 {
     const char* e = std::getenv("HC_PHMM_LANE_VARIANT");
     return (e && *e) ? std::atoi(e) : 0;
+}
+
+// Column-segmented lane waves (lane_kernel.hip run_cols): HC_PHMM_LANE_SEG=
+// auto (default) | off | all (every wave with more than one column block; for
+// tests). Returns -1 auto, 0 off, 1 all.
+int lane_seg_policy()
+{
+    const char* e = std::getenv("HC_PHMM_LANE_SEG");
+    if (!e || !*e || !std::strcmp(e, "auto")) return -1;
+    return std::strcmp(e, "all") ? 0 : 1;
 }
 
 // Kernel selection: HC_PHMM_KERNEL=auto (default) | lane | diag.
@@ -345,22 +363,76 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     const LaneVariant& LV = lane_variant(lane_var);
     const int lane_p = LV.P;
     const size_t per_wave = size_t(64) * lane_p;
-    for (size_t s0 = 0; s0 < lane_ord.size(); s0 += per_wave) {
+    const size_t nl = lane_ord.size();
+    // Shape of the wave over lane_ord[s0, s0 + n): max R, max column coverage,
+    // min R.
+    auto group = [&](size_t s0, size_t n, int& rmax, int& rmin, int& ncols) {
+        rmax = 0;
+        rmin = INT32_MAX;
+        ncols = 0;
+        for (size_t k = s0; k < std::min(nl, s0 + n); ++k) {
+            const int p = lane_ord[k];
+            rmax = std::max(rmax, pd[p].y);
+            rmin = std::min(rmin, pd[p].y);
+            ncols = std::max(ncols, cols16(p));
+        }
+    };
+    // Wave latency in block-rows (a wave's lanes step through BC-column rows
+    // in lockstep): nb * rmax for one lane per pair; rmax + nb - 1 for a
+    // column-segmented wave (nb lanes per pair, 64-column blocks).
+    auto latency_one = [&](int rmax, int ncols) { return int64_t((ncols + LV.BC - 1) / LV.BC) * rmax; };
+    // A batch too small to fill the chip several times over is bound by its
+    // heaviest waves, not by its total work: every wave whose one-lane latency
+    // exceeds 1/div of a SIMD's fair share of the batch is column-segmented
+    // (div = HC_PHMM_SEG_CAP, default 2). Large batches stay one lane per pair.
+    const int seg_pol = lane_p == 1 && LV.BC == 64 ? lane_seg_policy() : 0;
+    double lat_cap = 0.0;
+    if (seg_pol == -1) {
+        double U = 0.0;
+        for (size_t s0 = 0; s0 < nl; s0 += per_wave) {
+            int rmax, rmin, ncols;
+            group(s0, per_wave, rmax, rmin, ncols);
+            U += double(latency_one(rmax, ncols));
+        }
+        const char* e = std::getenv("HC_PHMM_SEG_CAP");
+        const double div = (e && std::atof(e) > 0) ? std::atof(e) : 2.0;
+        lat_cap = U / (div * 4.0 * g_eng.n_cu);
+    }
+    // Column-segmented waves go first in `lw` (their own launch, lane_kernel.hip
+    // launch_lane_seg_f32), one-lane waves after them.
+    std::vector<LaneWave> lw_one;
+    int n_seg_waves = 0;
+    for (size_t s0 = 0; s0 < nl;) {
+        int rmax, rmin, ncols;
+        // Sorted by columns first: the group's first pair has its widest hap.
+        const int nb = (cols16(lane_ord[s0]) + 63) / 64;
+        bool seg = false;
+        if (seg_pol == 1) {
+            seg = nb > 1;
+        } else if (seg_pol == -1 && nb > 1) {
+            group(s0, per_wave, rmax, rmin, ncols);
+            seg = double(latency_one(rmax, ncols)) > lat_cap;
+        }
+        const size_t n = seg ? size_t(64 / nb) : per_wave;
+        group(s0, n, rmax, rmin, ncols);
         LaneWave w{};
         w.slot0 = int(s0);
-        w.rmax = 0;
-        w.rmin = INT32_MAX;
-        w.ncols = 0;
-        for (size_t k = s0; k < std::min(lane_ord.size(), s0 + per_wave); ++k) {
-            const int p = lane_ord[k];
-            w.rmax = std::max(w.rmax, pd[p].y);
-            w.rmin = std::min(w.rmin, pd[p].y);
-            w.ncols = std::max(w.ncols, cols16(p));
+        w.rmax = rmax;
+        w.rmin = rmin;
+        if (!seg) {
+            w.ncols = ncols;
+            w.carry_row = carry_rows;
+            if (w.ncols > LV.BC) carry_rows += w.rmax + 1;
+            lw_one.push_back(w);
+        } else {
+            w.ncols = nb * 64;
+            w.group = nb;
+            lw.push_back(w);
+            ++n_seg_waves;
         }
-        w.carry_row = carry_rows;
-        if (w.ncols > LV.BC) carry_rows += w.rmax + 1;
-        lw.push_back(w);
+        s0 += n;
     }
+    lw.insert(lw.end(), lw_one.begin(), lw_one.end());
     // Anti-diagonal classes: W by H; (stripes, H) descending so the G pairs
     // sharing a wave have equal stripe counts and similar H, heaviest first.
     const int Wc[2] = {16, 64};
@@ -489,6 +561,7 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     b->cells = cells;
     b->Hmax = Hmax;
     b->n_lane = int(lane_ord.size());
+    b->n_seg_waves = n_seg_waves;
     b->lane_variant = lane_var;
     b->lane_waves = int(lw.size());
     b->d_pairs = reinterpret_cast<PairDesc*>(dev + o_pairs);
@@ -533,8 +606,6 @@ int run(hc_phmm_batch* b, hipStream_t s)
         a.pairs = b->d_pairs;
         a.order = b->d_lane_order;
         a.n_slots = b->n_lane;
-        a.n_waves = b->lane_waves;
-        a.waves = b->d_lane_waves;
         a.carry = b->d_carry;
         a.rows = b->d_rows;
         a.hapw = b->d_hapw;
@@ -544,7 +615,23 @@ int run(hc_phmm_batch* b, hipStream_t s)
         a.rescue_list = b->d_list;
         a.rescue_count = b->d_count;
         b->launch_waves += b->lane_waves;
+        const int n_one = b->lane_waves - b->n_seg_waves;
+        if (b->n_seg_waves > 0) {
+            // Segmented waves (the batch's heaviest pairs) on the side stream,
+            // launched first so they are dispatched first, and concurrent with
+            // the one-lane waves on `s`.
+            LaneArgs g = a;
+            g.waves = b->d_lane_waves;
+            g.n_waves = b->n_seg_waves;
+            HIP_TRY(hipEventRecord(g_eng.fork, s));
+            HIP_TRY(hipStreamWaitEvent(g_eng.side, g_eng.fork, 0));
+            HIP_TRY(launch_lane_seg_f32(g, g_eng.side));
+            HIP_TRY(hipEventRecord(g_eng.join, g_eng.side));
+        }
+        a.waves = b->d_lane_waves + b->n_seg_waves;
+        a.n_waves = n_one;
         HIP_TRY(launch_lane_f32(b->lane_variant, a, s));
+        if (b->n_seg_waves > 0) HIP_TRY(hipStreamWaitEvent(s, g_eng.join, 0));
     }
     for (auto& c : b->cls) {
         if (c.n == 0) continue;
@@ -674,7 +761,11 @@ int hc_phmm_shutdown(void)
     (void)hipFree(g_eng.lut_d);
     (void)hipFree(g_ws.dev);
     (void)hipHostFree(g_ws.host);
+    free_batch(g_ws.batch);
     g_ws = Workspace{};
+    (void)hipEventDestroy(g_eng.fork);
+    (void)hipEventDestroy(g_eng.join);
+    (void)hipStreamDestroy(g_eng.side);
     (void)hipStreamDestroy(g_eng.stream);
     g_eng = Engine{};
     return HC_PHMM_OK;
@@ -870,6 +961,7 @@ int hc_phmm_batch_stats(hc_phmm_batch* b, hc_phmm_stats* st)
     st->cells = b->cells;
     st->n_launch_waves = b->launch_waves;
     st->n_lane_pairs = b->n_lane;
+    st->n_seg_waves = b->n_seg_waves;
     if (b->ran && b->ev_used > 0) {
         HIP_TRY(hipStreamSynchronize(b->last_stream));
         double sa = 0, sc = 0;

@@ -56,7 +56,9 @@ struct LaneWave {
     int slot0;      // first slot of the wave in `order`
     int rmax;       // rows swept (max R of the wave's pairs)
     int rmin;       // min R of the wave's active pairs (first row that may need the sum)
-    int ncols;      // columns swept (max H rounded up to 16), <= nblk * 64
+    int ncols;      // columns swept (max H rounded up to 16; column-segmented: to 64)
+    int group;      // column-segmented waves (run_cols): lanes per pair = ncols / 64
+    int pad;
     long long carry_row;  // first carry row of this wave in `carry` (units of 64 float2)
 };
 struct LaneArgs {
@@ -82,6 +84,8 @@ struct LaneVariant {
 };
 const LaneVariant& lane_variant(int id);
 hipError_t launch_lane_f32(int variant, const LaneArgs& a, hipStream_t s);
+// Column-segmented waves only (LaneWave.group lanes per pair; run_cols).
+hipError_t launch_lane_seg_f32(const LaneArgs& a, hipStream_t s);
 
 // Launchers (kernels.hip). W = lanes per pair: 16, 32 or 64.
 hipError_t launch_diag_f32(int W, const DiagArgs& a, int grid, hipStream_t s);

@@ -258,7 +258,112 @@ __device__ __forceinline__ void run_pairs(const LaneArgs& a, const LaneWave& wv,
     else run_block<P, BC, BC, CG>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX, mt);
 }
 
-template <int P, int BC, int OCC>
+__device__ __forceinline__ float from_left(float v)
+{
+    // DPP wave_shr:1: lane l receives lane l-1's v (lane 0 receives 0).
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+
+// Column-segmented wave (the heaviest pairs of a batch too small to fill the
+// chip, whose one-lane waves would set the kernel time): a pair's nb column
+// blocks sit on nb consecutive lanes, lane s owning columns 64s+1 .. 64s+64 on
+// every row, and lane s sweeps row i = k - s in step k — a one-row skew per
+// block — so the pair finishes in R + nb - 1 steps instead of nb * R, with no
+// carry buffer. Each step lane s takes from lane s-1 (DPP wave_shr:1):
+//   - the Y entering its first column on row i (lane s-1's row i, last step),
+//   - the right-edge T of row i-1, its first diagonal (two steps back: held
+//     one step in a register),
+//   - on row R, the running sums ΣM, ΣX, so the final sums are accumulated
+//     column by column left to right exactly as the reference does.
+// Lanes outside 1 <= i <= rmax (pipeline fill / drain) are masked off; blocks
+// are always 64 wide (host rounds ncols up); columns past H compute values
+// that only flow right and are never summed.
+template <bool CG>
+__device__ __forceinline__ void run_cols(const LaneArgs& a, const LaneWave& wv, int lane, int s, int nb,
+                                         const LaneCtx<1>& cx, float T0, float& sumM, float& sumX,
+                                         uint2* __restrict__ mt)
+{
+    constexpr int BC = 64;
+    const int c0 = s * BC;
+    const int R = cx.R[0];
+    {   // this lane's block of the match table, fixed for the sweep
+        const int nwpad = (cx.H[0] + 31) / 32 + kHapLead;
+        const int w0 = min(c0 / 32 + kHapLead, nwpad), w1 = min(c0 / 32 + kHapLead + 1, nwpad);
+#pragma unroll
+        for (int c = 0; c < 5; ++c) mt[c * 64 + lane] = make_uint2(cx.hw[0][w0 * 5 + c], cx.hw[0][w1 * 5 + c]);
+    }
+    float T[BC], X[BC];
+#pragma unroll
+    for (int j = 0; j < BC; ++j) {
+        T[j] = T0;   // row 0
+        X[j] = 0.f;
+    }
+    uint32_t wc[1] = {cx.rrow[0][0]}, wn[1] = {cx.rrow[0][min(2, R) - 1]};
+    RowConst<1> k;
+    row_const<1>(a.lut, wc, wn, k);
+    uint2 mrow = mt[k.rc[0] * 64 + lane];
+    float y_out = 0.f, t_out = 0.f;   // handed to lane s+1: Y past column c0+64, T[63] of the last row
+    float t_hold = 0.f;               // lane s-1's right-edge T of the previous row
+    const int lim0 = cx.H[0] - c0;    // columns of this block inside the hap (<= 0: none)
+    auto step = [&](int kk, auto sum_tag) {
+        constexpr bool SUM = decltype(sum_tag)::value;
+        const int i = kk - s;
+        const float y_in = from_left(y_out);
+        const float t_in = from_left(t_out);
+        float sM_in = 0.f, sX_in = 0.f;
+        if constexpr (SUM) {
+            sM_in = from_left(sumM);
+            sX_in = from_left(sumX);
+        }
+        // Row 1's diagonal is row 0's T at every column; below that, lane
+        // s-1's right edge (column 0 for block 0: T[i][0] = 0 for i >= 1).
+        const float Tdiag = i == 1 ? T0 : (s ? t_hold : 0.f);
+        const float Yl0 = s ? y_in : 0.f;   // block 0: Y[i][1] = 0*my + 0*yy = 0
+        t_hold = t_in;
+        if (unsigned(i - 1) < unsigned(wv.rmax)) {
+            if constexpr (!CG) {
+                row_const<1>(a.lut, wc, wn, k);
+                mrow = mt[k.rc[0] * 64 + lane];
+            }
+            const uint32_t wnn = cx.rrow[0][min(i + 2, R) - 1];
+            float pm_n = 0.f, px_n = 0.f;
+            uint2 m_n = mrow;
+            if constexpr (CG) {
+                pm_n = a.lut[kOffPm + row_q(wn[0])];
+                px_n = a.lut[kOffPx + row_q(wn[0])];
+                m_n = mt[row_rc(wn[0]) * 64 + lane];
+            }
+            const uint32_t mw[1][2] = {{mrow.x, mrow.y}};
+            const int pmi[1] = {__float_as_int(k.pm)}, pxi[1] = {__float_as_int(k.px)};
+            const bool last = SUM && i == R;
+            const int lim[1] = {last ? lim0 : 0};
+            if (last) {
+                sumM = s ? sM_in : 0.f;
+                sumX = s ? sX_in : 0.f;
+            }
+            float Ml = 0.f, Yl = Yl0;
+            const float M0 = Tdiag * prior_vec<1, 0>(mw, pmi, pxi);
+            cell<1, BC, 0, BC, SUM>(T, X, M0, Ml, Yl, mw, pmi, pxi, k, lim, sumM, sumX);
+            y_out = Ml * k.my + Yl * k.yy;
+            t_out = T[BC - 1];
+            if constexpr (CG) {
+                k.pm = pm_n;
+                k.px = px_n;
+                mrow = m_n;
+            }
+            wc[0] = wn[0];
+            wn[0] = wnn;
+        }
+    };
+    const int nsteps = wv.rmax + nb - 1;
+    int kk = 1;
+    for (; kk < wv.rmin; ++kk) step(kk, std::false_type{});
+    for (; kk <= nsteps; ++kk) step(kk, std::true_type{});
+}
+
+// SEG: the launch holds only column-segmented waves (run_cols, LaneWave.group
+// lanes per pair) — a separate instantiation with its own register budget.
+template <int P, int BC, int OCC, bool SEG>
 __global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
 {
     using V = typename VT<P>::type;
@@ -274,6 +379,7 @@ __global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
         wv.rmax = __builtin_amdgcn_readfirstlane(w.rmax);
         wv.rmin = __builtin_amdgcn_readfirstlane(w.rmin);
         wv.ncols = __builtin_amdgcn_readfirstlane(w.ncols);
+        wv.group = __builtin_amdgcn_readfirstlane(w.group);
         const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(w.carry_row & 0xffffffffll));
         const unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(w.carry_row >> 32));
         wv.carry_row = (long long)(((unsigned long long)hi << 32) | lo);
@@ -282,10 +388,14 @@ __global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
     int pid[P];
     bool active[P];
     V T0;
+    // Column-segmented waves: lane = pair * group + block; lanes past the last
+    // whole group idle.
+    const int grp = SEG ? wv.group : 1;
+    const int gi = SEG ? lane / grp : 0, blk = SEG ? lane - gi * grp : 0;
 #pragma unroll
     for (int p = 0; p < P; ++p) {
-        const int slot = wv.slot0 + lane * P + p;
-        active[p] = slot < a.n_slots;
+        const int slot = wv.slot0 + (SEG ? gi : lane * P + p);
+        active[p] = slot < a.n_slots && (!SEG || gi < 64 / grp);
         pid[p] = a.order[active[p] ? slot : wv.slot0];
         const PairDesc pd = a.pairs[pid[p]];
         cx.R[p] = pd.y;
@@ -307,13 +417,22 @@ __global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
     V sumM = splat<V>(0.f), sumX = splat<V>(0.f);
     __shared__ uint2 mtab[4][P * 5 * 64];
     uint2* mt = mtab[threadIdx.x >> 6];
-    if (wave_cg)
-        run_pairs<P, BC, true>(a, wv, lane, cx, T0, sumM, sumX, mt);
-    else
-        run_pairs<P, BC, false>(a, wv, lane, cx, T0, sumM, sumX, mt);
+    bool owner = true;   // the lane that holds the pair's last column block writes the result
+    if constexpr (SEG && P == 1) {
+        if (wave_cg)
+            run_cols<true>(a, wv, lane, blk, grp, cx, T0, sumM, sumX, mt);
+        else
+            run_cols<false>(a, wv, lane, blk, grp, cx, T0, sumM, sumX, mt);
+        owner = blk == grp - 1;
+    } else {
+        if (wave_cg)
+            run_pairs<P, BC, true>(a, wv, lane, cx, T0, sumM, sumX, mt);
+        else
+            run_pairs<P, BC, false>(a, wv, lane, cx, T0, sumM, sumX, mt);
+    }
 #pragma unroll
     for (int p = 0; p < P; ++p) {
-        if (!active[p]) continue;
+        if (!active[p] || !owner) continue;
         const float raw = comp(sumM, p) + comp(sumX, p);
         a.raw_out[pid[p]] = raw;
         const bool resc = raw < 1e-28f;   // MIN_ACCEPTED, pairhmm_common.h:16
@@ -327,6 +446,7 @@ __global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
 // Lane kernel variants: {pairs per lane, block columns, waves per SIMD}.
 // Block widths are multiples of 32 (a block starts on a match-word boundary).
 // Measured on S2 (ms per fp32 pass): v0 11.5, v1 12.8, v2 15.6, v3 17.7.
+constexpr int kSegOcc = 3;   // waves per SIMD of the column-segmented kernel
 static const LaneVariant kVariants[] = {
     {1, 64, 3}, {1, 64, 2}, {1, 32, 4}, {2, 32, 2},
 };
@@ -343,11 +463,19 @@ hipError_t launch_lane_f32(int id, const LaneArgs& a, hipStream_t s)
     const int grid = (a.n_waves + 3) / 4;
     const dim3 g(grid), blk(256);
     switch ((id >= 0 && id < 4) ? id : 0) {
-    case 1: hipLaunchKernelGGL((phmm_lane_kernel<1, 64, 2>), g, blk, 0, s, a); break;
-    case 2: hipLaunchKernelGGL((phmm_lane_kernel<1, 32, 4>), g, blk, 0, s, a); break;
-    case 3: hipLaunchKernelGGL((phmm_lane_kernel<2, 32, 2>), g, blk, 0, s, a); break;
-    default: hipLaunchKernelGGL((phmm_lane_kernel<1, 64, 3>), g, blk, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((phmm_lane_kernel<1, 64, 2, false>), g, blk, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((phmm_lane_kernel<1, 32, 4, false>), g, blk, 0, s, a); break;
+    case 3: hipLaunchKernelGGL((phmm_lane_kernel<2, 32, 2, false>), g, blk, 0, s, a); break;
+    default: hipLaunchKernelGGL((phmm_lane_kernel<1, 64, 3, false>), g, blk, 0, s, a); break;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_lane_seg_f32(const LaneArgs& a, hipStream_t s)
+{
+    if (a.n_waves <= 0) return hipSuccess;
+    const int grid = (a.n_waves + 3) / 4;
+    hipLaunchKernelGGL((phmm_lane_kernel<1, 64, kSegOcc, true>), dim3(grid), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -63,7 +63,7 @@ class Stats(C.Structure):
     _fields_ = [("n_pairs", C.c_int64), ("cells", C.c_int64), ("n_rescued", C.c_int64),
                 ("kernel_ms_f32", C.c_double), ("kernel_ms_f64", C.c_double),
                 ("run_ms", C.c_double), ("n_launch_waves", C.c_int64), ("n_runs", C.c_int64),
-                ("n_lane_pairs", C.c_int64)]
+                ("n_lane_pairs", C.c_int64), ("n_seg_waves", C.c_int64)]
 
 
 def build() -> None:

@@ -75,6 +75,7 @@ typedef struct hc_phmm_stats {
     int64_t n_launch_waves; /* waves launched by the fp32 pass               */
     int64_t n_runs;         /* runs since the previous stats() call          */
     int64_t n_lane_pairs;   /* pairs on the lane-per-pair kernel (rest: anti-diagonal) */
+    int64_t n_seg_waves;    /* lane waves that split each pair over 2..16 lanes       */
 } hc_phmm_stats;
 
 /* Select the device (HIP ordinal; -1 = current) and build the device LUTs.

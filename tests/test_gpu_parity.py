@@ -9,8 +9,10 @@ pytestmark = pytest.mark.gpu
 
 # "diag" = anti-diagonal kernel; "laneN" = lane-per-pair kernel variant N
 # (lane_kernel.hip kVariants: 0 = 64-col blocks 3 waves/SIMD (default),
-# 1 = 64-col 2 waves, 2 = 32-col 4 waves, 3 = two pairs per lane, packed f32).
-KERNELS = ["diag", "lane0", "lane1", "lane2", "lane3"]
+# 1 = 64-col 2 waves, 2 = 32-col 4 waves, 3 = two pairs per lane, packed f32);
+# "segall" = every lane wave with more than one column block column-segmented
+# (run_cols: one lane per 64-column block of a pair).
+KERNELS = ["diag", "lane0", "lane1", "lane2", "lane3", "segall"]
 
 
 @pytest.fixture(params=KERNELS)
@@ -18,9 +20,13 @@ def kernel(request, monkeypatch):
     """Force one fp32 kernel / lane-kernel variant for the test."""
     if request.param == "diag":
         monkeypatch.setenv("HC_PHMM_KERNEL", "diag")
+    elif request.param.startswith("seg"):
+        monkeypatch.setenv("HC_PHMM_KERNEL", "lane")
+        monkeypatch.setenv("HC_PHMM_LANE_SEG", "all")
     else:
         monkeypatch.setenv("HC_PHMM_KERNEL", "lane")
         monkeypatch.setenv("HC_PHMM_LANE_VARIANT", request.param[4:])
+        monkeypatch.setenv("HC_PHMM_LANE_SEG", "off")
     return request.param
 
 
@@ -176,3 +182,28 @@ def test_cross_regions_matches_per_region_calls(engine):
             continue
         alone = engine.cross(reads, haps)
         assert np.array_equal(bits(got), bits(alone))
+
+
+def test_auto_segmentation_on_a_shard(engine, oracle_lib, monkeypatch):
+    """A 125k-pair S2 shard (one rank's share of configs[3] at 8 GPUs) is too
+    small to fill the chip with one-lane waves: the engine column-segments its
+    heaviest waves (one lane per 64-column block) and runs them beside the
+    rest. Same arithmetic in the same order, so the whole shard is
+    bit-identical to the unsegmented run, and a sample equals the oracle."""
+    b = W.config("S2", 125_000)
+    bt = engine.Batch(b)
+    bt.run()
+    seg = bt.results()
+    st = bt.stats()
+    bt.close()
+    assert st.n_lane_pairs == 125_000 and st.n_seg_waves > 0
+    monkeypatch.setenv("HC_PHMM_LANE_SEG", "off")
+    bt = engine.Batch(b)
+    bt.run()
+    one = bt.results()
+    assert bt.stats().n_seg_waves == 0
+    bt.close()
+    for k in seg:
+        assert np.array_equal(bits(seg[k]), bits(one[k])), k
+    idx = np.random.default_rng(1).choice(125_000, 3000, replace=False)
+    assert_same({k: seg[k][idx] for k in seg}, oracle_lib.pairs(W.subset(b, idx), nthreads=16), "shard")
