@@ -179,6 +179,7 @@ namespace {
 constexpr int kW64Threshold = 768;   // H above this -> one pair per wave (W = 64)
 constexpr int64_t kLaneMinPairs = 32768;   // batches this large use the lane-per-pair kernel
 constexpr int kLaneMaxH = 4096;            // longer haps stay on the anti-diagonal kernel
+constexpr int kSegMaxH = 1024;             // column-segmented lane waves up to this H (16 lanes)
 
 // Lane kernel variant (kernels.hpp LaneVariant): HC_PHMM_LANE_VARIANT=<id>,
 // default 0 = {1 pair per lane, 64-column blocks, 3 waves per SIMD}.
@@ -188,9 +189,10 @@ int lane_variant_id()
     return (e && *e) ? std::atoi(e) : 0;
 }
 
-// Column-segmented lane waves (lane_kernel.hip run_cols): HC_PHMM_LANE_SEG=
-// auto (default) | off | all (every wave with more than one column block; for
-// tests). Returns -1 auto, 0 off, 1 all.
+// Column-segmented lane waves (lane_kernel.hip run_seg): HC_PHMM_LANE_SEG=
+// auto (default: haps up to kSegMaxH) | off (one lane per pair) | all (every
+// lane pair up to 64 * kSegMaxBC columns; for tests). Returns -1 auto, 0 off,
+// 1 all.
 int lane_seg_policy()
 {
     const char* e = std::getenv("HC_PHMM_LANE_SEG");
@@ -352,87 +354,104 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
             ord[pd[p].w > kW64Threshold ? 1 : 0].push_back(int(p));
     }
     std::vector<uint32_t> key(npairs);
-    // Lane class: bin by column coverage (H rounded up to 16), then R, both
-    // descending, so a wave's 64*P pairs sweep nearly the same rows x columns.
-    auto cols16 = [&](int p) { return (pd[p].w + 15) / 16 * 16; };
-    for (int p : lane_ord) key[p] = (uint32_t(cols16(p)) << 16) | uint32_t(std::min(pd[p].y, 65535));
-    sort_desc(lane_ord, key);
+    // Lane class. Column-segmented waves (lane_kernel.hip run_seg) take every
+    // pair with H <= kSegMaxH (policy "all": H <= 64 * kSegMaxBC): a pair gets
+    // nb lanes of BC columns, BC from the compiled widths, choosing between
+    // nb0 = ceil(H/64) and nb0 + 1 lanes by modelled cost nb*BC*(R + nb - 1).
+    // Pairs are binned by (BC, R) descending and packed greedily into waves of
+    // up to 64 lanes (a short look-ahead fills a wave's last lanes). Longer
+    // haps (or policy "off") take one lane per pair with the carry buffer,
+    // binned by (H rounded up to 16, R).
     std::vector<LaneWave> lw;
     int64_t carry_rows = 0;
     const int lane_var = lane_variant_id();
     const LaneVariant& LV = lane_variant(lane_var);
     const int lane_p = LV.P;
-    const size_t per_wave = size_t(64) * lane_p;
-    const size_t nl = lane_ord.size();
-    // Shape of the wave over lane_ord[s0, s0 + n): max R, max column coverage,
-    // min R.
-    auto group = [&](size_t s0, size_t n, int& rmax, int& rmin, int& ncols) {
-        rmax = 0;
-        rmin = INT32_MAX;
-        ncols = 0;
-        for (size_t k = s0; k < std::min(nl, s0 + n); ++k) {
-            const int p = lane_ord[k];
-            rmax = std::max(rmax, pd[p].y);
-            rmin = std::min(rmin, pd[p].y);
-            ncols = std::max(ncols, cols16(p));
+    const int seg_pol = lane_seg_policy();
+    const int seg_max_h = seg_pol == 0 ? 0 : (seg_pol == 1 ? 64 * kSegMaxBC : kSegMaxH);
+    std::vector<int> seg_in, one_ord;
+    std::vector<uint8_t> seg_bc(npairs, 0), seg_nb(npairs, 0);
+    for (int p : lane_ord) {
+        const int H = pd[p].w, R = pd[p].y;
+        if (H > seg_max_h) {
+            one_ord.push_back(p);
+            continue;
         }
-    };
-    // Wave latency in block-rows (a wave's lanes step through BC-column rows
-    // in lockstep): nb * rmax for one lane per pair; rmax + nb - 1 for a
-    // column-segmented wave (nb lanes per pair, 64-column blocks).
-    auto latency_one = [&](int rmax, int ncols) { return int64_t((ncols + LV.BC - 1) / LV.BC) * rmax; };
-    // A batch too small to fill the chip several times over is bound by its
-    // heaviest waves, not by its total work: every wave whose one-lane latency
-    // exceeds 1/div of a SIMD's fair share of the batch is column-segmented
-    // (div = HC_PHMM_SEG_CAP, default 2). Large batches stay one lane per pair.
-    const int seg_pol = lane_p == 1 && LV.BC == 64 ? lane_seg_policy() : 0;
-    double lat_cap = 0.0;
-    if (seg_pol == -1) {
-        double U = 0.0;
-        for (size_t s0 = 0; s0 < nl; s0 += per_wave) {
-            int rmax, rmin, ncols;
-            group(s0, per_wave, rmax, rmin, ncols);
-            U += double(latency_one(rmax, ncols));
+        const int nb0 = (H + 63) / 64;
+        int64_t best = INT64_MAX;
+        for (int nb = nb0; nb <= std::min(nb0 + 1, 64); ++nb) {
+            int bc = std::max(16, ((H + nb - 1) / nb + 7) / 8 * 8);
+            while (!seg_width_ok(bc)) bc += 8;
+            const int n = (H + bc - 1) / bc;
+            const int64_t cost = int64_t(n) * bc * (R + n - 1);
+            if (cost < best) {
+                best = cost;
+                seg_bc[p] = uint8_t(bc);
+                seg_nb[p] = uint8_t(n);
+            }
         }
-        const char* e = std::getenv("HC_PHMM_SEG_CAP");
-        const double div = (e && std::atof(e) > 0) ? std::atof(e) : 2.0;
-        lat_cap = U / (div * 4.0 * g_eng.n_cu);
+        key[p] = (uint32_t(seg_bc[p]) << 16) | uint32_t(std::min(R, 65535));
+        seg_in.push_back(p);
     }
-    // Column-segmented waves go first in `lw` (their own launch, lane_kernel.hip
-    // launch_lane_seg_f32), one-lane waves after them.
-    std::vector<LaneWave> lw_one;
-    int n_seg_waves = 0;
-    for (size_t s0 = 0; s0 < nl;) {
-        int rmax, rmin, ncols;
-        // Sorted by columns first: the group's first pair has its widest hap.
-        const int nb = (cols16(lane_ord[s0]) + 63) / 64;
-        bool seg = false;
-        if (seg_pol == 1) {
-            seg = nb > 1;
-        } else if (seg_pol == -1 && nb > 1) {
-            group(s0, per_wave, rmax, rmin, ncols);
-            seg = double(latency_one(rmax, ncols)) > lat_cap;
-        }
-        const size_t n = seg ? size_t(64 / nb) : per_wave;
-        group(s0, n, rmax, rmin, ncols);
-        LaneWave w{};
-        w.slot0 = int(s0);
-        w.rmax = rmax;
-        w.rmin = rmin;
-        if (!seg) {
-            w.ncols = ncols;
-            w.carry_row = carry_rows;
-            if (w.ncols > LV.BC) carry_rows += w.rmax + 1;
-            lw_one.push_back(w);
-        } else {
-            w.ncols = nb * 64;
-            w.group = nb;
+    sort_desc(seg_in, key);
+    std::vector<int> seg_ord;
+    seg_ord.reserve(seg_in.size());
+    {
+        std::vector<uint8_t> used(seg_in.size(), 0);
+        size_t i = 0;
+        const size_t ns = seg_in.size();
+        constexpr size_t kLook = 64;
+        while (i < ns) {
+            if (used[i]) {
+                ++i;
+                continue;
+            }
+            const int bc = seg_bc[seg_in[i]];
+            LaneWave w{};
+            w.slot0 = int(seg_ord.size());
+            w.ncols = bc;
+            w.rmin = INT32_MAX;
+            int free = 64;
+            for (size_t j = i; j < ns && j < i + kLook && free > 0; ++j) {
+                const int p = seg_in[j];
+                if (used[j] || seg_bc[p] != bc) {
+                    if (!used[j]) break;
+                    continue;
+                }
+                if (seg_nb[p] > free) continue;
+                used[j] = 1;
+                free -= seg_nb[p];
+                seg_ord.push_back(p);
+                ++w.npairs;
+                w.rmax = std::max(w.rmax, pd[p].y);
+                w.rmin = std::min(w.rmin, pd[p].y);
+                w.nsteps = std::max(w.nsteps, pd[p].y + seg_nb[p] - 1);
+            }
             lw.push_back(w);
-            ++n_seg_waves;
         }
-        s0 += n;
     }
-    lw.insert(lw.end(), lw_one.begin(), lw_one.end());
+    const int n_seg_waves = int(lw.size());
+    const int n_seg_slots = int(seg_ord.size());
+    auto cols16 = [&](int p) { return (pd[p].w + 15) / 16 * 16; };
+    for (int p : one_ord) key[p] = (uint32_t(cols16(p)) << 16) | uint32_t(std::min(pd[p].y, 65535));
+    sort_desc(one_ord, key);
+    const size_t per_wave = size_t(64) * lane_p;
+    for (size_t s0 = 0; s0 < one_ord.size(); s0 += per_wave) {
+        LaneWave w{};
+        w.slot0 = n_seg_slots + int(s0);
+        w.rmin = INT32_MAX;
+        for (size_t k = s0; k < std::min(one_ord.size(), s0 + per_wave); ++k) {
+            const int p = one_ord[k];
+            w.rmax = std::max(w.rmax, pd[p].y);
+            w.rmin = std::min(w.rmin, pd[p].y);
+            w.ncols = std::max(w.ncols, cols16(p));
+        }
+        w.carry_row = carry_rows;
+        if (w.ncols > LV.BC) carry_rows += w.rmax + 1;
+        lw.push_back(w);
+    }
+    lane_ord = std::move(seg_ord);
+    lane_ord.insert(lane_ord.end(), one_ord.begin(), one_ord.end());
     // Anti-diagonal classes: W by H; (stripes, H) descending so the G pairs
     // sharing a wave have equal stripe counts and similar H, heaviest first.
     const int Wc[2] = {16, 64};

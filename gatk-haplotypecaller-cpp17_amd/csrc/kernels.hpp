@@ -55,11 +55,12 @@ constexpr int kLaneBlock = 64;
 struct LaneWave {
     int slot0;      // first slot of the wave in `order`
     int rmax;       // rows swept (max R of the wave's pairs)
-    int rmin;       // min R of the wave's active pairs (first row that may need the sum)
-    int ncols;      // columns swept (max H rounded up to 16; column-segmented: to 64)
-    int group;      // column-segmented waves (run_cols): lanes per pair = ncols / 64
-    int pad;
-    long long carry_row;  // first carry row of this wave in `carry` (units of 64 float2)
+    int rmin;       // min R of the wave's pairs (first row that may need the sum)
+    int ncols;      // one-lane waves: columns swept (max H rounded up to 16);
+                    // column-segmented waves: block width BC (seg_width_ok)
+    int npairs;     // column-segmented waves: pairs in the wave (slot0 ..)
+    int nsteps;     // column-segmented waves: steps = max over pairs of R + nb - 1
+    long long carry_row;  // one-lane waves: first carry row in `carry` (units of 64 float2)
 };
 struct LaneArgs {
     const PairDesc* pairs;
@@ -84,8 +85,11 @@ struct LaneVariant {
 };
 const LaneVariant& lane_variant(int id);
 hipError_t launch_lane_f32(int variant, const LaneArgs& a, hipStream_t s);
-// Column-segmented waves only (LaneWave.group lanes per pair; run_cols).
+// Column-segmented waves only (lane_kernel.hip run_seg): a pair of hap length H
+// takes ceil(H / BC) lanes; BC per wave, one of the compiled block widths.
 hipError_t launch_lane_seg_f32(const LaneArgs& a, hipStream_t s);
+bool seg_width_ok(int bc);
+constexpr int kSegMaxBC = 64;
 
 // Launchers (kernels.hip). W = lanes per pair: 16, 32 or 64.
 hipError_t launch_diag_f32(int W, const DiagArgs& a, int grid, hipStream_t s);

@@ -97,7 +97,12 @@ __device__ __forceinline__ typename VT<P>::type prior_vec(const uint32_t (&mw)[P
 // its old value (the next column's diagonal) is consumed into the next M, so
 // the new T[J] can take the old one's register: no copies between rows.
 // mw[p][w]: match words of pair p for this row (w = 0, 1 for 64 columns).
-template <int P, int BC, int J, int NC, bool SUM>
+// EQ: mx == my bitwise (insertion and deletion gap qualities equal on every
+// row: the reference's SAMRecord passes 'I' for both, sam.hpp:30-32), so the
+// product M*mx that feeds X[J] is also the M*my term of the next column's Y:
+// one multiply fewer per cell, the same rounded values. Ml then carries that
+// product instead of M.
+template <int P, int BC, int J, int NC, bool SUM, bool EQ>
 __device__ __forceinline__ void cell(typename VT<P>::type (&T)[BC], typename VT<P>::type (&X)[BC],
                                      typename VT<P>::type M, typename VT<P>::type& Ml,
                                      typename VT<P>::type& Yl, const uint32_t (&mw)[P][2],
@@ -110,9 +115,18 @@ __device__ __forceinline__ void cell(typename VT<P>::type (&T)[BC], typename VT<
         V Mn = M;
         if constexpr (J + 1 < NC) Mn = T[J] * prior_vec<P, J + 1>(mw, pmi, pxi);
         const V Xc = X[J];
-        const V Y = (J == 0) ? Yl : (Ml * k.my + Yl * k.yy);
+        V Y, Mx;
+        if constexpr (EQ) {
+            Mx = M * k.mx;
+            Y = (J == 0) ? Yl : (Ml + Yl * k.yy);
+        } else {
+            Y = (J == 0) ? Yl : (Ml * k.my + Yl * k.yy);
+        }
         T[J] = (M * k.mm + Xc * k.g) + Y * k.g;
-        X[J] = M * k.mx + Xc * k.xx;
+        if constexpr (EQ)
+            X[J] = Mx + Xc * k.xx;
+        else
+            X[J] = M * k.mx + Xc * k.xx;
         if constexpr (SUM) {
 #pragma unroll
             for (int p = 0; p < P; ++p) {
@@ -121,10 +135,24 @@ __device__ __forceinline__ void cell(typename VT<P>::type (&T)[BC], typename VT<
                 set_comp(sumX, p, comp(sumX, p) + (c ? comp(Xc, p) : 0.f));
             }
         }
-        Ml = M;
+        if constexpr (EQ)
+            Ml = Mx;
+        else
+            Ml = M;
         Yl = Y;
-        cell<P, BC, J + 1, NC, SUM>(T, X, Mn, Ml, Yl, mw, pmi, pxi, k, lim, sumM, sumX);
+        cell<P, BC, J + 1, NC, SUM, EQ>(T, X, Mn, Ml, Yl, mw, pmi, pxi, k, lim, sumM, sumX);
     }
+}
+
+// Y entering the column after the last one of a row segment: Ml*my + Yl*yy
+// (EQ: Ml already holds M*mx = M*my).
+template <bool EQ, typename V>
+__device__ __forceinline__ V y_next(V Ml, V Yl, V my, V yy)
+{
+    if constexpr (EQ)
+        return Ml + Yl * yy;
+    else
+        return Ml * my + Yl * yy;
 }
 
 template <int P>
@@ -145,7 +173,7 @@ struct LaneCtx {
 // the six transition constants are per-lane registers and a row only needs its
 // prior (pm, px from q) and match word; those are fetched one row ahead.
 // mt: this wave's LDS match table [P][5 read codes][64 lanes] of 2 words.
-template <int P, int BC, int NC, bool CG>
+template <int P, int BC, int NC, bool CG, bool EQ>
 __device__ __forceinline__ void run_block(const LaneArgs& a, const LaneWave& wv, int lane, int b, int nb,
                                           const LaneCtx<P>& cx, typename VT<P>::type T0,
                                           typename VT<P>::type& sumM, typename VT<P>::type& sumX,
@@ -222,8 +250,8 @@ __device__ __forceinline__ void run_block(const LaneArgs& a, const LaneWave& wv,
         }
         V Ml = splat<V>(0.f), Yl = cin.y;   // block 0: Y[i][1] = 0*my + 0*yy = 0
         const V M0 = Tdiag * prior_vec<P, 0>(mw, pmi, pxi);
-        cell<P, BC, 0, NC, SUM>(T, X, M0, Ml, Yl, mw, pmi, pxi, k, lim, sumM, sumX);
-        if (has_out) carry[size_t(i) * 64] = Carry<P>{T[NC - 1], Ml * k.my + Yl * k.yy};
+        cell<P, BC, 0, NC, SUM, EQ>(T, X, M0, Ml, Yl, mw, pmi, pxi, k, lim, sumM, sumX);
+        if (has_out) carry[size_t(i) * 64] = Carry<P>{T[NC - 1], y_next<EQ>(Ml, Yl, k.my, k.yy)};
         // next row's diagonal at column c0: this row's T there (block 0: column 0 -> 0)
         Tdiag = has_in ? cin.t : splat<V>(0.f);
         cin = cnext;
@@ -244,18 +272,18 @@ __device__ __forceinline__ void run_block(const LaneArgs& a, const LaneWave& wv,
     for (; i <= wv.rmax; ++i) row(i, std::true_type{});
 }
 
-template <int P, int BC, bool CG>
+template <int P, int BC, bool CG, bool EQ>
 __device__ __forceinline__ void run_pairs(const LaneArgs& a, const LaneWave& wv, int lane, const LaneCtx<P>& cx,
                                           typename VT<P>::type T0, typename VT<P>::type& sumM,
                                           typename VT<P>::type& sumX, uint2* __restrict__ mt)
 {
     const int nb = (wv.ncols + BC - 1) / BC;
     const int tail = wv.ncols - (nb - 1) * BC;   // multiple of 16, <= BC
-    for (int b = 0; b + 1 < nb; ++b) run_block<P, BC, BC, CG>(a, wv, lane, b, nb, cx, T0, sumM, sumX, mt);
-    if (tail == 16) run_block<P, BC, 16, CG>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX, mt);
-    else if (BC >= 32 && tail == 32) run_block<P, BC, (BC >= 32 ? 32 : 16), CG>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX, mt);
-    else if (BC >= 64 && tail == 48) run_block<P, BC, (BC >= 64 ? 48 : 16), CG>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX, mt);
-    else run_block<P, BC, BC, CG>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX, mt);
+    for (int b = 0; b + 1 < nb; ++b) run_block<P, BC, BC, CG, EQ>(a, wv, lane, b, nb, cx, T0, sumM, sumX, mt);
+    if (tail == 16) run_block<P, BC, 16, CG, EQ>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX, mt);
+    else if (BC >= 32 && tail == 32) run_block<P, BC, (BC >= 32 ? 32 : 16), CG, EQ>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX, mt);
+    else if (BC >= 64 && tail == 48) run_block<P, BC, (BC >= 64 ? 48 : 16), CG, EQ>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX, mt);
+    else run_block<P, BC, BC, CG, EQ>(a, wv, lane, nb - 1, nb, cx, T0, sumM, sumX, mt);
 }
 
 __device__ __forceinline__ float from_left(float v)
@@ -264,33 +292,38 @@ __device__ __forceinline__ float from_left(float v)
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
 }
 
-// Column-segmented wave (the heaviest pairs of a batch too small to fill the
-// chip, whose one-lane waves would set the kernel time): a pair's nb column
-// blocks sit on nb consecutive lanes, lane s owning columns 64s+1 .. 64s+64 on
-// every row, and lane s sweeps row i = k - s in step k — a one-row skew per
-// block — so the pair finishes in R + nb - 1 steps instead of nb * R, with no
-// carry buffer. Each step lane s takes from lane s-1 (DPP wave_shr:1):
+// Column-segmented wave: a pair's nb column blocks of BC columns sit on nb
+// consecutive lanes (a "group"), lane s of the group owning columns
+// s*BC+1 .. s*BC+BC on every row, and lane s sweeps row i = k - s in step k —
+// a one-row skew per block — so the pair finishes in R + nb - 1 steps, with no
+// carry buffer. Groups of different nb share a wave (the host packs the 64
+// lanes); BC is per wave (all its pairs have nb*BC >= H). Each step lane s
+// takes from lane s-1 (DPP wave_shr:1; ignored on a group's first lane):
 //   - the Y entering its first column on row i (lane s-1's row i, last step),
 //   - the right-edge T of row i-1, its first diagonal (two steps back: held
 //     one step in a register),
 //   - on row R, the running sums ΣM, ΣX, so the final sums are accumulated
 //     column by column left to right exactly as the reference does.
-// Lanes outside 1 <= i <= rmax (pipeline fill / drain) are masked off; blocks
-// are always 64 wide (host rounds ncols up); columns past H compute values
-// that only flow right and are never summed.
-template <bool CG>
-__device__ __forceinline__ void run_cols(const LaneArgs& a, const LaneWave& wv, int lane, int s, int nb,
-                                         const LaneCtx<1>& cx, float T0, float& sumM, float& sumX,
-                                         uint2* __restrict__ mt)
+// Lanes outside 1 <= i <= rmax (pipeline fill / drain) are masked off; columns
+// past H compute values that only flow right and are never summed.
+template <int BC, bool CG, bool EQ>
+__device__ __forceinline__ void run_seg(const LaneArgs& a, const LaneWave& wv, int lane, int s,
+                                        const LaneCtx<1>& cx, float T0, float& sumM, float& sumX,
+                                        uint2* __restrict__ mt)
 {
-    constexpr int BC = 64;
     const int c0 = s * BC;
     const int R = cx.R[0];
-    {   // this lane's block of the match table, fixed for the sweep
-        const int nwpad = (cx.H[0] + 31) / 32 + kHapLead;
-        const int w0 = min(c0 / 32 + kHapLead, nwpad), w1 = min(c0 / 32 + kHapLead + 1, nwpad);
+    {   // this lane's BC-column window of the match table, fixed for the sweep:
+        // columns c0+1 .. c0+BC start at bit 31-r of table row c0/32+lead
+        const int nwpad = (cx.H[0] + 31) / 32 + kHapLead;   // the trailing zero row
+        const int w0 = c0 / 32 + kHapLead, r = c0 & 31;
+        const int i0 = min(w0, nwpad), i1 = min(w0 + 1, nwpad), i2 = min(w0 + 2, nwpad);
 #pragma unroll
-        for (int c = 0; c < 5; ++c) mt[c * 64 + lane] = make_uint2(cx.hw[0][w0 * 5 + c], cx.hw[0][w1 * 5 + c]);
+        for (int c = 0; c < 5; ++c) {
+            const uint64_t x01 = (uint64_t(cx.hw[0][i0 * 5 + c]) << 32) | cx.hw[0][i1 * 5 + c];
+            const uint64_t x12 = (uint64_t(cx.hw[0][i1 * 5 + c]) << 32) | cx.hw[0][i2 * 5 + c];
+            mt[c * 64 + lane] = make_uint2(uint32_t((x01 << r) >> 32), uint32_t((x12 << r) >> 32));
+        }
     }
     float T[BC], X[BC];
 #pragma unroll
@@ -302,7 +335,7 @@ __device__ __forceinline__ void run_cols(const LaneArgs& a, const LaneWave& wv, 
     RowConst<1> k;
     row_const<1>(a.lut, wc, wn, k);
     uint2 mrow = mt[k.rc[0] * 64 + lane];
-    float y_out = 0.f, t_out = 0.f;   // handed to lane s+1: Y past column c0+64, T[63] of the last row
+    float y_out = 0.f, t_out = 0.f;   // handed to lane s+1: Y past column c0+BC, T[BC-1] of the last row
     float t_hold = 0.f;               // lane s-1's right-edge T of the previous row
     const int lim0 = cx.H[0] - c0;    // columns of this block inside the hap (<= 0: none)
     auto step = [&](int kk, auto sum_tag) {
@@ -343,8 +376,8 @@ __device__ __forceinline__ void run_cols(const LaneArgs& a, const LaneWave& wv, 
             }
             float Ml = 0.f, Yl = Yl0;
             const float M0 = Tdiag * prior_vec<1, 0>(mw, pmi, pxi);
-            cell<1, BC, 0, BC, SUM>(T, X, M0, Ml, Yl, mw, pmi, pxi, k, lim, sumM, sumX);
-            y_out = Ml * k.my + Yl * k.yy;
+            cell<1, BC, 0, BC, SUM, EQ>(T, X, M0, Ml, Yl, mw, pmi, pxi, k, lim, sumM, sumX);
+            y_out = y_next<EQ>(Ml, Yl, k.my, k.yy);
             t_out = T[BC - 1];
             if constexpr (CG) {
                 k.pm = pm_n;
@@ -355,47 +388,93 @@ __device__ __forceinline__ void run_cols(const LaneArgs& a, const LaneWave& wv, 
             wn[0] = wnn;
         }
     };
-    const int nsteps = wv.rmax + nb - 1;
     int kk = 1;
     for (; kk < wv.rmin; ++kk) step(kk, std::false_type{});
-    for (; kk <= nsteps; ++kk) step(kk, std::true_type{});
+    for (; kk <= wv.nsteps; ++kk) step(kk, std::true_type{});
 }
 
-// SEG: the launch holds only column-segmented waves (run_cols, LaneWave.group
-// lanes per pair) — a separate instantiation with its own register budget.
-template <int P, int BC, int OCC, bool SEG>
+// Block widths of column-segmented waves (LaneWave.ncols of a segmented wave).
+#define HC_SEG_WIDTHS(X) X(16) X(24) X(32) X(40) X(48) X(56) X(64)
+
+template <int BC>
+__device__ __forceinline__ void run_seg_bc(const LaneArgs& a, const LaneWave& wv, int lane, int s,
+                                           const LaneCtx<1>& cx, float T0, float& sumM, float& sumX,
+                                           uint2* __restrict__ mt, bool wave_cg, bool wave_eq)
+{
+    if (wave_eq)
+        run_seg<BC, true, true>(a, wv, lane, s, cx, T0, sumM, sumX, mt);
+    else if (wave_cg)
+        run_seg<BC, true, false>(a, wv, lane, s, cx, T0, sumM, sumX, mt);
+    else
+        run_seg<BC, false, false>(a, wv, lane, s, cx, T0, sumM, sumX, mt);
+}
+
+// Per-lane pair context and the row-0 diagonal T0 = (0*mm + 0*gapm) + (INITIAL/H)*gapm
+// (avx-pairhmm-template.h:160-166 with row 1's constants).
+__device__ __forceinline__ void load_pair(const LaneArgs& a, int pid, LaneCtx<1>& cx, int p, float& t0)
+{
+    const PairDesc pd = a.pairs[pid];
+    cx.R[p] = pd.y;
+    cx.H[p] = pd.w;
+    cx.rrow[p] = a.rows + pd.x;
+    cx.hw[p] = a.hapw + pd.z;
+    const uint32_t w1 = cx.rrow[p][0];
+    const float mm1 = a.lut[kOffMM + mm_idx(row_i(w1), row_d(w1))];
+    const float g1 = a.lut[kOffGapm + row_c(w1)];
+    const float initY = 0x1p120f / float(pd.w);
+    t0 = (0.f * mm1 + 0.f * g1) + initY * g1;
+}
+
+// Wave metadata is wave-uniform: pin it to SGPRs so loops and switches are
+// scalar branches.
+__device__ __forceinline__ LaneWave load_wave(const LaneArgs& a, int wid)
+{
+    LaneWave wv;
+    const LaneWave w = a.waves[wid];
+    wv.slot0 = __builtin_amdgcn_readfirstlane(w.slot0);
+    wv.rmax = __builtin_amdgcn_readfirstlane(w.rmax);
+    wv.rmin = __builtin_amdgcn_readfirstlane(w.rmin);
+    wv.ncols = __builtin_amdgcn_readfirstlane(w.ncols);
+    wv.npairs = __builtin_amdgcn_readfirstlane(w.npairs);
+    wv.nsteps = __builtin_amdgcn_readfirstlane(w.nsteps);
+    const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(w.carry_row & 0xffffffffll));
+    const unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(w.carry_row >> 32));
+    wv.carry_row = (long long)(((unsigned long long)hi << 32) | lo);
+    return wv;
+}
+
+__device__ __forceinline__ void emit(const LaneArgs& a, int pid, float raw)
+{
+    a.raw_out[pid] = raw;
+    const bool resc = raw < 1e-28f;   // MIN_ACCEPTED, pairhmm_common.h:16
+    a.rescue_flag[pid] = resc;
+    if (resc) a.rescue_list[atomicAdd(a.rescue_count, 1)] = pid;
+}
+
+// Constant-gap tag of a read: bit 31 of its first row word (mark_cg_kernel).
+// EQ additionally needs insertion == deletion gap quality.
+__device__ __forceinline__ bool read_cg(uint32_t w1) { return (w1 >> 31) != 0; }
+__device__ __forceinline__ bool read_eq(uint32_t w1) { return read_cg(w1) && row_i(w1) == row_d(w1); }
+
+// One lane per pair (P pairs per lane), column blocks of BC with the carry
+// buffer between blocks.
+template <int P, int BC, int OCC>
 __global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
 {
     using V = typename VT<P>::type;
     const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (wid >= a.n_waves) return;
     const int lane = threadIdx.x & 63;
-    // Wave metadata is wave-uniform: pin it to SGPRs so loops and the tail switch
-    // are scalar branches.
-    LaneWave wv;
-    {
-        const LaneWave w = a.waves[wid];
-        wv.slot0 = __builtin_amdgcn_readfirstlane(w.slot0);
-        wv.rmax = __builtin_amdgcn_readfirstlane(w.rmax);
-        wv.rmin = __builtin_amdgcn_readfirstlane(w.rmin);
-        wv.ncols = __builtin_amdgcn_readfirstlane(w.ncols);
-        wv.group = __builtin_amdgcn_readfirstlane(w.group);
-        const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(w.carry_row & 0xffffffffll));
-        const unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(w.carry_row >> 32));
-        wv.carry_row = (long long)(((unsigned long long)hi << 32) | lo);
-    }
+    const LaneWave wv = load_wave(a, wid);
     LaneCtx<P> cx;
     int pid[P];
     bool active[P];
     V T0;
-    // Column-segmented waves: lane = pair * group + block; lanes past the last
-    // whole group idle.
-    const int grp = SEG ? wv.group : 1;
-    const int gi = SEG ? lane / grp : 0, blk = SEG ? lane - gi * grp : 0;
+    bool cg = true, eq = true;
 #pragma unroll
     for (int p = 0; p < P; ++p) {
-        const int slot = wv.slot0 + (SEG ? gi : lane * P + p);
-        active[p] = slot < a.n_slots && (!SEG || gi < 64 / grp);
+        const int slot = wv.slot0 + lane * P + p;
+        active[p] = slot < a.n_slots;
         pid[p] = a.order[active[p] ? slot : wv.slot0];
         const PairDesc pd = a.pairs[pid[p]];
         cx.R[p] = pd.y;
@@ -407,38 +486,87 @@ __global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
         const float g1 = a.lut[kOffGapm + row_c(w1)];
         const float initY = 0x1p120f / float(pd.w);
         set_comp(T0, p, (0.f * mm1 + 0.f * g1) + initY * g1);
+        cg &= read_cg(w1);
+        eq &= read_eq(w1);
     }
-    // Constant-gap tag of each read (bit 31 of its first row word, set by
-    // mark_cg_kernel); the CG path runs only if all the wave's pairs qualify.
-    bool cg = true;
-#pragma unroll
-    for (int p = 0; p < P; ++p) cg &= (cx.rrow[p][0] >> 31) != 0;
     const bool wave_cg = __builtin_amdgcn_ballot_w64(!cg) == 0;
+    const bool wave_eq = __builtin_amdgcn_ballot_w64(!eq) == 0;
     V sumM = splat<V>(0.f), sumX = splat<V>(0.f);
     __shared__ uint2 mtab[4][P * 5 * 64];
     uint2* mt = mtab[threadIdx.x >> 6];
-    bool owner = true;   // the lane that holds the pair's last column block writes the result
-    if constexpr (SEG && P == 1) {
-        if (wave_cg)
-            run_cols<true>(a, wv, lane, blk, grp, cx, T0, sumM, sumX, mt);
-        else
-            run_cols<false>(a, wv, lane, blk, grp, cx, T0, sumM, sumX, mt);
-        owner = blk == grp - 1;
-    } else {
-        if (wave_cg)
-            run_pairs<P, BC, true>(a, wv, lane, cx, T0, sumM, sumX, mt);
-        else
-            run_pairs<P, BC, false>(a, wv, lane, cx, T0, sumM, sumX, mt);
-    }
+    if (wave_eq)
+        run_pairs<P, BC, true, true>(a, wv, lane, cx, T0, sumM, sumX, mt);
+    else if (wave_cg)
+        run_pairs<P, BC, true, false>(a, wv, lane, cx, T0, sumM, sumX, mt);
+    else
+        run_pairs<P, BC, false, false>(a, wv, lane, cx, T0, sumM, sumX, mt);
 #pragma unroll
-    for (int p = 0; p < P; ++p) {
-        if (!active[p] || !owner) continue;
-        const float raw = comp(sumM, p) + comp(sumX, p);
-        a.raw_out[pid[p]] = raw;
-        const bool resc = raw < 1e-28f;   // MIN_ACCEPTED, pairhmm_common.h:16
-        a.rescue_flag[pid[p]] = resc;
-        if (resc) a.rescue_list[atomicAdd(a.rescue_count, 1)] = pid[p];
+    for (int p = 0; p < P; ++p)
+        if (active[p]) emit(a, pid[p], comp(sumM, p) + comp(sumX, p));
+}
+
+// Column-segmented waves (run_seg). The wave's npairs pairs are the slots
+// slot0 .. slot0+npairs-1; pair g takes nb_g = ceil(H_g / BC) consecutive lanes
+// in slot order. Lanes past the last group idle (s = 0, no output).
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void phmm_seg_kernel(LaneArgs a)
+{
+    const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (wid >= a.n_waves) return;
+    const int lane = threadIdx.x & 63;
+    const LaneWave wv = load_wave(a, wid);
+    const int bc = wv.ncols;
+    __shared__ uint2 mtab[4][5 * 64];
+    uint2* mt = mtab[threadIdx.x >> 6];
+    // Lane -> (group, block): group g's lanes start at the prefix sum of nb.
+    int* gmap = reinterpret_cast<int*>(mt);   // 64 ints, reused before the match table
+    int pid_g = 0, nb_g = 0;
+    if (lane < wv.npairs) {
+        pid_g = a.order[wv.slot0 + lane];
+        nb_g = (a.pairs[pid_g].w + bc - 1) / bc;
     }
+    int start = nb_g;   // inclusive scan of nb over lanes (Hillis-Steele through LDS)
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        gmap[lane] = start;
+        __builtin_amdgcn_wave_barrier();
+        const int v = lane >= d ? gmap[lane - d] : 0;
+        __builtin_amdgcn_wave_barrier();
+        start += v;
+    }
+    start -= nb_g;
+    gmap[lane] = -1;
+    __builtin_amdgcn_wave_barrier();
+    if (lane < wv.npairs)
+        for (int t = 0; t < nb_g; ++t) {
+            gmap[start + t] = lane;
+            gmap[64 + start + t] = t;
+        }
+    __builtin_amdgcn_wave_barrier();
+    const int g = gmap[lane];
+    int s = gmap[64 + lane];
+    __builtin_amdgcn_wave_barrier();
+    int pid = a.order[wv.slot0 + (g >= 0 ? g : 0)];
+    bool owner = false;
+    if (g >= 0)
+        owner = s == (a.pairs[pid].w + bc - 1) / bc - 1;
+    else
+        s = 0;
+    LaneCtx<1> cx;
+    float T0;
+    load_pair(a, pid, cx, 0, T0);
+    const uint32_t w1 = cx.rrow[0][0];
+    const bool wave_cg = __builtin_amdgcn_ballot_w64(!read_cg(w1)) == 0;
+    const bool wave_eq = __builtin_amdgcn_ballot_w64(!read_eq(w1)) == 0;
+    float sumM = 0.f, sumX = 0.f;
+    switch (bc) {
+#define HC_SEG_CASE(W) \
+    case W: run_seg_bc<W>(a, wv, lane, s, cx, T0, sumM, sumX, mt, wave_cg, wave_eq); break;
+        HC_SEG_WIDTHS(HC_SEG_CASE)
+#undef HC_SEG_CASE
+    default: break;
+    }
+    if (owner) emit(a, pid, sumM + sumX);
 }
 
 }  // namespace
@@ -463,19 +591,30 @@ hipError_t launch_lane_f32(int id, const LaneArgs& a, hipStream_t s)
     const int grid = (a.n_waves + 3) / 4;
     const dim3 g(grid), blk(256);
     switch ((id >= 0 && id < 4) ? id : 0) {
-    case 1: hipLaunchKernelGGL((phmm_lane_kernel<1, 64, 2, false>), g, blk, 0, s, a); break;
-    case 2: hipLaunchKernelGGL((phmm_lane_kernel<1, 32, 4, false>), g, blk, 0, s, a); break;
-    case 3: hipLaunchKernelGGL((phmm_lane_kernel<2, 32, 2, false>), g, blk, 0, s, a); break;
-    default: hipLaunchKernelGGL((phmm_lane_kernel<1, 64, 3, false>), g, blk, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((phmm_lane_kernel<1, 64, 2>), g, blk, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((phmm_lane_kernel<1, 32, 4>), g, blk, 0, s, a); break;
+    case 3: hipLaunchKernelGGL((phmm_lane_kernel<2, 32, 2>), g, blk, 0, s, a); break;
+    default: hipLaunchKernelGGL((phmm_lane_kernel<1, 64, 3>), g, blk, 0, s, a); break;
     }
     return hipGetLastError();
+}
+
+bool seg_width_ok(int bc)
+{
+    switch (bc) {
+#define HC_SEG_OK(W) case W:
+        HC_SEG_WIDTHS(HC_SEG_OK)
+#undef HC_SEG_OK
+        return true;
+    default: return false;
+    }
 }
 
 hipError_t launch_lane_seg_f32(const LaneArgs& a, hipStream_t s)
 {
     if (a.n_waves <= 0) return hipSuccess;
     const int grid = (a.n_waves + 3) / 4;
-    hipLaunchKernelGGL((phmm_lane_kernel<1, 64, kSegOcc, true>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((phmm_seg_kernel<kSegOcc>), dim3(grid), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

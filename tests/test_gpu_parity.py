@@ -10,9 +10,10 @@ pytestmark = pytest.mark.gpu
 # "diag" = anti-diagonal kernel; "laneN" = lane-per-pair kernel variant N
 # (lane_kernel.hip kVariants: 0 = 64-col blocks 3 waves/SIMD (default),
 # 1 = 64-col 2 waves, 2 = 32-col 4 waves, 3 = two pairs per lane, packed f32);
-# "segall" = every lane wave with more than one column block column-segmented
-# (run_cols: one lane per 64-column block of a pair).
-KERNELS = ["diag", "lane0", "lane1", "lane2", "lane3", "segall"]
+# "seg" = the default lane path: column-segmented waves (run_seg: a pair over
+# ceil(H/BC) lanes, BC per wave) for H <= 1024, one lane per pair above;
+# "segall" = every lane pair column-segmented (up to 64 lanes per pair).
+KERNELS = ["diag", "lane0", "lane1", "lane2", "lane3", "seg", "segall"]
 
 
 @pytest.fixture(params=KERNELS)
@@ -20,7 +21,10 @@ def kernel(request, monkeypatch):
     """Force one fp32 kernel / lane-kernel variant for the test."""
     if request.param == "diag":
         monkeypatch.setenv("HC_PHMM_KERNEL", "diag")
-    elif request.param.startswith("seg"):
+    elif request.param == "seg":
+        monkeypatch.setenv("HC_PHMM_KERNEL", "lane")
+        monkeypatch.setenv("HC_PHMM_LANE_SEG", "auto")
+    elif request.param == "segall":
         monkeypatch.setenv("HC_PHMM_KERNEL", "lane")
         monkeypatch.setenv("HC_PHMM_LANE_SEG", "all")
     else:
@@ -185,11 +189,11 @@ def test_cross_regions_matches_per_region_calls(engine):
 
 
 def test_auto_segmentation_on_a_shard(engine, oracle_lib, monkeypatch):
-    """A 125k-pair S2 shard (one rank's share of configs[3] at 8 GPUs) is too
-    small to fill the chip with one-lane waves: the engine column-segments its
-    heaviest waves (one lane per 64-column block) and runs them beside the
-    rest. Same arithmetic in the same order, so the whole shard is
-    bit-identical to the unsegmented run, and a sample equals the oracle."""
+    """A 125k-pair S2 shard (one rank's share of configs[3] at 8 GPUs): the
+    engine column-segments every pair (ceil(H/BC) lanes per pair). Same
+    arithmetic in the same order as one lane per pair with the carry buffer,
+    so the whole shard is bit-identical to the unsegmented run, and a sample
+    equals the oracle."""
     b = W.config("S2", 125_000)
     bt = engine.Batch(b)
     bt.run()
@@ -207,3 +211,33 @@ def test_auto_segmentation_on_a_shard(engine, oracle_lib, monkeypatch):
         assert np.array_equal(bits(seg[k]), bits(one[k])), k
     idx = np.random.default_rng(1).choice(125_000, 3000, replace=False)
     assert_same({k: seg[k][idx] for k in seg}, oracle_lib.pairs(W.subset(b, idx), nthreads=16), "shard")
+
+
+@pytest.mark.parametrize("gaps", ["eq", "cg", "per_base"])
+@pytest.mark.parametrize("seg", ["auto", "all"])
+def test_seg_widths_and_gap_modes(engine, oracle_lib, monkeypatch, gaps, seg):
+    """Column-segmented waves over every compiled block width (H 10..1100 puts
+    pairs on BC 16..64 and 1..18 lanes) and the three cell paths: equal
+    constant gap qualities (the reference's 'I'/'I'/'+', EQ path: M*mx shared
+    with the next column's M*my), constant but unequal (CG path) and per-base
+    gap qualities (generic path). Bit-exact against the oracle."""
+    monkeypatch.setenv("HC_PHMM_KERNEL", "lane")
+    monkeypatch.setenv("HC_PHMM_LANE_SEG", seg)
+    b = W.generate(6000, (10, 1100), (5, 250), 0.02, seed=11)
+    rng = np.random.default_rng(5)
+    n = len(b["ins"])
+    if gaps == "cg":
+        b["ins"][:] = 40 + 33
+        b["dels"][:] = 25 + 33
+        b["gcp"][:] = 12 + 33
+    elif gaps == "per_base":
+        b["ins"][:] = rng.integers(33 + 5, 33 + 60, n, dtype=np.uint8)
+        b["dels"][:] = rng.integers(33 + 5, 33 + 60, n, dtype=np.uint8)
+        b["gcp"][:] = rng.integers(33 + 5, 33 + 30, n, dtype=np.uint8)
+    bt = engine.Batch(b)
+    bt.run()
+    res = bt.results()
+    st = bt.stats()
+    bt.close()
+    assert st.n_seg_waves > 0
+    assert_same(res, oracle_lib.pairs(b, nthreads=16), f"seg={seg}/{gaps}")
