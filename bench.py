@@ -176,7 +176,8 @@ def main():
     traffic, tsrc = traffic_from_profiles(args.workload, my_cells)
     roofline = dict(bound="valu", achieved=round(achieved, 3), peak=VALU_PEAK_TOPS, unit="TFLOP/s",
                     frac=round(achieved / VALU_PEAK_TOPS, 4), traffic=traffic,
-                    kernel=("phmm_lane_kernel" if st.n_lane_pairs == st.n_pairs else "phmm_diag_kernel<float,16>"),
+                    kernel=(("phmm_seg_kernel" if st.n_seg_waves > 0 else "phmm_lane_kernel")
+                            if st.n_lane_pairs == st.n_pairs else "phmm_diag_kernel<float,16>"),
                     kernel_ms=round(k_ms, 4),
                     flops_per_cell=FLOPS_PER_CELL, cells_per_launch=my_cells,
                     hbm_algorithmic_GBs=round(algorithmic_bytes(sub) / (k_ms * 1e-3) / 1e9, 2) if k_ms > 0 else None,

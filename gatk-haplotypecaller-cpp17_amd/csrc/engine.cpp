@@ -380,8 +380,8 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
         const int nb0 = (H + 63) / 64;
         int64_t best = INT64_MAX;
         for (int nb = nb0; nb <= std::min(nb0 + 1, 64); ++nb) {
-            int bc = std::max(16, ((H + nb - 1) / nb + 7) / 8 * 8);
-            while (!seg_width_ok(bc)) bc += 8;
+            int bc = std::max(16, ((H + nb - 1) / nb + 3) / 4 * 4);
+            while (!seg_width_ok(bc)) bc += 4;
             const int n = (H + bc - 1) / bc;
             const int64_t cost = int64_t(n) * bc * (R + n - 1);
             if (cost < best) {

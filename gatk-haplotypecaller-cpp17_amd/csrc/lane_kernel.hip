@@ -394,17 +394,19 @@ __device__ __forceinline__ void run_seg(const LaneArgs& a, const LaneWave& wv, i
 }
 
 // Block widths of column-segmented waves (LaneWave.ncols of a segmented wave).
-#define HC_SEG_WIDTHS(X) X(16) X(24) X(32) X(40) X(48) X(56) X(64)
+#define HC_SEG_WIDTHS(X) \
+    X(16) X(20) X(24) X(28) X(32) X(36) X(40) X(44) X(48) X(52) X(56) X(60) X(64)
 
 template <int BC>
 __device__ __forceinline__ void run_seg_bc(const LaneArgs& a, const LaneWave& wv, int lane, int s,
                                            const LaneCtx<1>& cx, float T0, float& sumM, float& sumX,
                                            uint2* __restrict__ mt, bool wave_cg, bool wave_eq)
 {
+    // Two compiled paths per width: EQ (the reference's constant 'I'/'I'/'+'
+    // gap qualities) and the generic per-row path (any gap qualities).
+    (void)wave_cg;
     if (wave_eq)
         run_seg<BC, true, true>(a, wv, lane, s, cx, T0, sumM, sumX, mt);
-    else if (wave_cg)
-        run_seg<BC, true, false>(a, wv, lane, s, cx, T0, sumM, sumX, mt);
     else
         run_seg<BC, false, false>(a, wv, lane, s, cx, T0, sumM, sumX, mt);
 }

@@ -59,9 +59,15 @@ def main():
             ent["hbm_bytes_per_launch"] = int((2 * fetch + write) * 1024)
             ent["hbm_bytes_note"] = "2*FETCH_SIZE + WRITE_SIZE (KB) x 1024, gfx950 correction"
         summary["kernels"][k] = ent
-        if "phmm" in k and (dominant is None or "float" in k or "lane" in k):
-            if "double" not in k:
-                dominant = k
+    # Dominant fp32 PairHMM kernel: column-segmented > one-lane > anti-diagonal.
+    def rank(k):
+        for r, tag in enumerate(("phmm_seg_kernel", "phmm_lane_kernel", "phmm_diag_kernel<float")):
+            if tag in k:
+                return r
+        return None
+    for k in kern:
+        if rank(k) is not None and (dominant is None or rank(k) < rank(dominant)):
+            dominant = k
     if dominant:
         summary["dominant_kernel"] = dominant
         summary["hbm_bytes_per_launch"] = summary["kernels"][dominant].get("hbm_bytes_per_launch")
