@@ -161,7 +161,8 @@ struct hc_phmm_batch {
     double* own_raw64 = nullptr;
     uint8_t* own_flag = nullptr;
     int* d_list = nullptr;
-    int* d_count = nullptr;
+    int* d_count = nullptr;       // rescue counters, one per run parity
+    int parity = 0;               // run parity: which counter this run appends to
     char* dev_base = nullptr;     // the batch's device allocation
     bool owns_dev = true;         // false: borrowed from the engine workspace
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};   // current run's triple (from ev_pool)
@@ -177,9 +178,8 @@ struct hc_phmm_batch {
 namespace {
 
 constexpr int kW64Threshold = 768;   // H above this -> one pair per wave (W = 64)
-constexpr int64_t kLaneMinPairs = 32768;   // batches this large use the lane-per-pair kernel
 constexpr int kLaneMaxH = 4096;            // longer haps stay on the anti-diagonal kernel
-constexpr int kSegMaxH = 1024;             // column-segmented lane waves up to this H (16 lanes)
+constexpr int kSegMinWavesPerSimd = 2;     // small batches: narrower seg blocks until this many waves
 
 // Lane kernel variant (kernels.hpp LaneVariant): HC_PHMM_LANE_VARIANT=<id>,
 // default 0 = {1 pair per lane, 64-column blocks, 3 waves per SIMD}.
@@ -190,9 +190,8 @@ int lane_variant_id()
 }
 
 // Column-segmented lane waves (lane_kernel.hip run_seg): HC_PHMM_LANE_SEG=
-// auto (default: haps up to kSegMaxH) | off (one lane per pair) | all (every
-// lane pair up to 64 * kSegMaxBC columns; for tests). Returns -1 auto, 0 off,
-// 1 all.
+// auto = all (default: every lane pair up to 64 * kSegMaxBC columns) | off
+// (one lane per pair with the carry buffer). Returns -1 auto, 0 off, 1 all.
 int lane_seg_policy()
 {
     const char* e = std::getenv("HC_PHMM_LANE_SEG");
@@ -200,7 +199,8 @@ int lane_seg_policy()
     return std::strcmp(e, "all") ? 0 : 1;
 }
 
-// Kernel selection: HC_PHMM_KERNEL=auto (default) | lane | diag.
+// Kernel selection: HC_PHMM_KERNEL=auto (default: lane kernels for H <= kLaneMaxH,
+// anti-diagonal above) | lane (lane kernels for every pair) | diag.
 int kernel_policy()
 {
     const char* e = std::getenv("HC_PHMM_KERNEL");
@@ -346,7 +346,7 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     std::vector<int> ord[2], lane_ord;
     lane_ord.reserve(npairs);
     const int pol = kernel_policy();
-    const bool use_lane = pol == 1 || (pol == 0 && npairs >= kLaneMinPairs);
+    const bool use_lane = pol != 2;
     for (int64_t p = 0; p < npairs; ++p) {
         if (use_lane && (pol == 1 || pd[p].w <= kLaneMaxH))
             lane_ord.push_back(int(p));
@@ -355,29 +355,28 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     }
     std::vector<uint32_t> key(npairs);
     // Lane class. Column-segmented waves (lane_kernel.hip run_seg) take every
-    // pair with H <= kSegMaxH (policy "all": H <= 64 * kSegMaxBC): a pair gets
-    // nb lanes of BC columns, BC from the compiled widths, choosing between
-    // nb0 = ceil(H/64) and nb0 + 1 lanes by modelled cost nb*BC*(R + nb - 1).
-    // Pairs are binned by (BC, R) descending and packed greedily into waves of
-    // up to 64 lanes (a short look-ahead fills a wave's last lanes). Longer
-    // haps (or policy "off") take one lane per pair with the carry buffer,
-    // binned by (H rounded up to 16, R).
+    // lane pair with H <= 64 * kSegMaxBC (policy "off": none): a pair gets nb
+    // lanes of BC columns, BC from the compiled widths, choosing between
+    // nb0 = ceil(H/cap) and nb0 + 1 lanes by modelled cost nb*BC*(R + nb - 1).
+    // The width cap is 64 unless the batch is too small to give every SIMD
+    // kSegMinWavesPerSimd waves at that width (a lone wave issues at half
+    // rate): then the widest cap that does, down to 16, so small batches are
+    // spread over more, shorter waves. Pairs are binned by (BC, R) descending
+    // and packed greedily into waves of up to 64 lanes (a short look-ahead
+    // fills a wave's last lanes). Longer haps (or policy "off") take one lane
+    // per pair with the carry buffer, binned by (H rounded up to 16, R).
     std::vector<LaneWave> lw;
     int64_t carry_rows = 0;
     const int lane_var = lane_variant_id();
     const LaneVariant& LV = lane_variant(lane_var);
     const int lane_p = LV.P;
-    const int seg_pol = lane_seg_policy();
-    const int seg_max_h = seg_pol == 0 ? 0 : (seg_pol == 1 ? 64 * kSegMaxBC : kSegMaxH);
+    const int seg_max_h = lane_seg_policy() == 0 ? 0 : 64 * kSegMaxBC;
     std::vector<int> seg_in, one_ord;
     std::vector<uint8_t> seg_bc(npairs, 0), seg_nb(npairs, 0);
-    for (int p : lane_ord) {
+    for (int p : lane_ord) (pd[p].w > seg_max_h ? one_ord : seg_in).push_back(p);
+    auto choose = [&](int p, int cap) {
         const int H = pd[p].w, R = pd[p].y;
-        if (H > seg_max_h) {
-            one_ord.push_back(p);
-            continue;
-        }
-        const int nb0 = (H + 63) / 64;
+        const int nb0 = std::min(64, (H + cap - 1) / cap);
         int64_t best = INT64_MAX;
         for (int nb = nb0; nb <= std::min(nb0 + 1, 64); ++nb) {
             int bc = std::max(16, ((H + nb - 1) / nb + 3) / 4 * 4);
@@ -390,8 +389,25 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
                 seg_nb[p] = uint8_t(n);
             }
         }
-        key[p] = (uint32_t(seg_bc[p]) << 16) | uint32_t(std::min(R, 65535));
-        seg_in.push_back(p);
+    };
+    int cap = kSegMaxBC;
+    {
+        const int64_t want = int64_t(kSegMinWavesPerSimd) * 4 * g_eng.n_cu * 64;   // lanes
+        const char* e = std::getenv("HC_PHMM_SEG_CAP");
+        if (e && *e) {
+            cap = std::max(16, std::min(kSegMaxBC, std::atoi(e)));
+        } else {
+            for (int c : {64, 48, 32, 24, 16}) {
+                cap = c;
+                int64_t lanes = 0;
+                for (int p : seg_in) lanes += std::min(64, (pd[p].w + c - 1) / c);
+                if (lanes >= want) break;
+            }
+        }
+    }
+    for (int p : seg_in) {
+        choose(p, cap);
+        key[p] = (uint32_t(seg_bc[p]) << 16) | uint32_t(std::min(pd[p].y, 65535));
     }
     sort_desc(seg_in, key);
     std::vector<int> seg_ord;
@@ -494,7 +510,7 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     const size_t o_raw64 = L.take(sizeof(double) * n1);
     const size_t o_flag = L.take(n1);
     const size_t o_list = L.take(sizeof(int) * n1);
-    const size_t o_count = L.take(sizeof(int));
+    const size_t o_count = L.take(2 * sizeof(int));
     const size_t o_carry = L.take(sizeof(float2) * size_t(carry_rows) * 64 * lane_p);
     const size_t total = L.off;
 
@@ -556,6 +572,7 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
         // The workspace staging stays valid until the call returns, so only a
         // batch-owned staging buffer needs the copy to finish here.
         hipError_t e1 = hipMemcpyAsync(dev, host, upload, hipMemcpyHostToDevice, g_eng.stream);
+        if (e1 == hipSuccess) e1 = hipMemsetAsync(dev + o_count, 0, 2 * sizeof(int), g_eng.stream);
         if (e1 == hipSuccess)
             e1 = launch_pack_rows(reinterpret_cast<const uint8_t*>(dev + o_raw), (long long)nrows,
                                   (long long)stride, reinterpret_cast<uint32_t*>(dev + o_rows), g_eng.stream);
@@ -618,8 +635,11 @@ int run(hc_phmm_batch* b, hipStream_t s)
     const auto& ev = b->ev_pool[b->ev_used++];
     for (int k = 0; k < 3; ++k) b->ev[k] = ev[k];
     HIP_TRY(hipEventRecord(b->ev[0], s));
-    HIP_TRY(hipMemsetAsync(b->d_count, 0, sizeof(int), s));
-    HIP_TRY(hipMemsetAsync(b->d_raw64, 0, sizeof(double) * std::max<int64_t>(b->n, 1), s));
+    // No memsets: the fp32 kernels zero each pair's raw f64 slot as they emit,
+    // and the rescue kernel zeroes the other parity's counter for the next run.
+    const int par = b->parity;
+    b->parity ^= 1;
+    int* count = b->d_count + par;
     if (b->n_lane > 0) {
         LaneArgs a{};
         a.pairs = b->d_pairs;
@@ -632,25 +652,30 @@ int run(hc_phmm_batch* b, hipStream_t s)
         a.raw_out = b->d_raw32;
         a.rescue_flag = b->d_flag;
         a.rescue_list = b->d_list;
-        a.rescue_count = b->d_count;
+        a.rescue_count = count;
+        a.raw64_zero = b->d_raw64;
         b->launch_waves += b->lane_waves;
         const int n_one = b->lane_waves - b->n_seg_waves;
+        const bool fork = b->n_seg_waves > 0 && n_one > 0;
         if (b->n_seg_waves > 0) {
-            // Segmented waves (the batch's heaviest pairs) on the side stream,
-            // launched first so they are dispatched first, and concurrent with
-            // the one-lane waves on `s`.
+            // Segmented waves; beside one-lane waves (long haps) they go on the
+            // side stream, launched first so they are dispatched first.
             LaneArgs g = a;
             g.waves = b->d_lane_waves;
             g.n_waves = b->n_seg_waves;
-            HIP_TRY(hipEventRecord(g_eng.fork, s));
-            HIP_TRY(hipStreamWaitEvent(g_eng.side, g_eng.fork, 0));
-            HIP_TRY(launch_lane_seg_f32(g, g_eng.side));
-            HIP_TRY(hipEventRecord(g_eng.join, g_eng.side));
+            if (fork) {
+                HIP_TRY(hipEventRecord(g_eng.fork, s));
+                HIP_TRY(hipStreamWaitEvent(g_eng.side, g_eng.fork, 0));
+            }
+            HIP_TRY(launch_lane_seg_f32(g, fork ? g_eng.side : s));
+            if (fork) HIP_TRY(hipEventRecord(g_eng.join, g_eng.side));
         }
-        a.waves = b->d_lane_waves + b->n_seg_waves;
-        a.n_waves = n_one;
-        HIP_TRY(launch_lane_f32(b->lane_variant, a, s));
-        if (b->n_seg_waves > 0) HIP_TRY(hipStreamWaitEvent(s, g_eng.join, 0));
+        if (n_one > 0) {
+            a.waves = b->d_lane_waves + b->n_seg_waves;
+            a.n_waves = n_one;
+            HIP_TRY(launch_lane_f32(b->lane_variant, a, s));
+        }
+        if (fork) HIP_TRY(hipStreamWaitEvent(s, g_eng.join, 0));
     }
     for (auto& c : b->cls) {
         if (c.n == 0) continue;
@@ -665,7 +690,8 @@ int run(hc_phmm_batch* b, hipStream_t s)
         a.raw_out = b->d_raw32;
         a.rescue_flag = b->d_flag;
         a.rescue_list = b->d_list;
-        a.rescue_count = b->d_count;
+        a.rescue_count = count;
+        a.raw64_zero = b->d_raw64;
         const int G = 64 / c.W;
         const int grid = (c.n + G - 1) / G;
         b->launch_waves += grid;
@@ -678,7 +704,8 @@ int run(hc_phmm_batch* b, hipStream_t s)
         DiagArgs a{};
         a.pairs = b->d_pairs;
         a.order = b->d_list;
-        a.n_slots_dev = b->d_count;
+        a.n_slots_dev = count;
+        a.count_reset = b->d_count + (par ^ 1);
         a.rows = b->d_rows;
         a.hapw = b->d_hapw;
         a.lut = g_eng.lut_d;
@@ -998,7 +1025,7 @@ int hc_phmm_batch_stats(hc_phmm_batch* b, hc_phmm_stats* st)
         st->run_ms = st->kernel_ms_f32 + st->kernel_ms_f64;
         b->ev_used = 0;
         int cnt = 0;
-        HIP_TRY(hipMemcpy(&cnt, b->d_count, sizeof(int), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(&cnt, b->d_count + (b->parity ^ 1), sizeof(int), hipMemcpyDeviceToHost));
         st->n_rescued = cnt;
     }
     return HC_PHMM_OK;

@@ -171,6 +171,7 @@ __global__ __launch_bounds__(64) void phmm_diag_kernel(DiagArgs a)
     const T* __restrict__ ph2pr = lut + kOffPh2pr;
     Pair2<T>* ring = reinterpret_cast<Pair2<T>*>(smem) + g * a.ring_len;
     const int n = a.n_slots_dev ? *a.n_slots_dev : a.n_slots;
+    if (a.count_reset && blockIdx.x == 0 && threadIdx.x == 0) *a.count_reset = 0;
 
     for (int wv = blockIdx.x; wv * G < n; wv += gridDim.x) {
         const int slot = wv * G + g;
@@ -232,6 +233,7 @@ __global__ __launch_bounds__(64) void phmm_diag_kernel(DiagArgs a)
             if constexpr (sizeof(T) == 4) {
                 const bool resc = raw < 1e-28f;   // MIN_ACCEPTED, pairhmm_common.h:16
                 a.rescue_flag[pid] = resc;
+                a.raw64_zero[pid] = 0.0;
                 if (resc) a.rescue_list[atomicAdd(a.rescue_count, 1)] = pid;
             }
         }

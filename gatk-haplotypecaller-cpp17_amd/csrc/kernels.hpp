@@ -46,6 +46,10 @@ struct DiagArgs {
     uint8_t* rescue_flag;     // fp32 pass: 1 if raw < 1e-28f (by pair id)
     int* rescue_list;         // fp32 pass: appended pair ids
     int* rescue_count;        // fp32 pass: append counter
+    double* raw64_zero;       // fp32 pass: raw f64 result slot of each pair, zeroed
+                              // (the rescue pass overwrites the rescued ones)
+    int* count_reset;         // fp64 pass: the other run parity's rescue counter,
+                              // zeroed for the next run (no memset per run)
 };
 
 // Lane-per-pair kernel (large batches): one lane owns one pair and sweeps it
@@ -76,6 +80,7 @@ struct LaneArgs {
     uint8_t* rescue_flag;
     int* rescue_list;
     int* rescue_count;
+    double* raw64_zero;       // as DiagArgs::raw64_zero
 };
 // Variants of the lane kernel (lane_kernel.hip kVariants): pairs per lane P
 // (1, or 2 packed in float2 halves), register block width in columns, and the

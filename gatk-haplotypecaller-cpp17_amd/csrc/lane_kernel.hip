@@ -450,6 +450,7 @@ __device__ __forceinline__ void emit(const LaneArgs& a, int pid, float raw)
     a.raw_out[pid] = raw;
     const bool resc = raw < 1e-28f;   // MIN_ACCEPTED, pairhmm_common.h:16
     a.rescue_flag[pid] = resc;
+    a.raw64_zero[pid] = 0.0;
     if (resc) a.rescue_list[atomicAdd(a.rescue_count, 1)] = pid;
 }
 

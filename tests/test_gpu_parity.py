@@ -241,3 +241,17 @@ def test_seg_widths_and_gap_modes(engine, oracle_lib, monkeypatch, gaps, seg):
     bt.close()
     assert st.n_seg_waves > 0
     assert_same(res, oracle_lib.pairs(b, nthreads=16), f"seg={seg}/{gaps}")
+
+
+def test_repeated_runs_reuse_rescue_counters(engine, oracle_lib):
+    """A prepared batch run many times: the fp32 pass appends to one of two
+    rescue counters by run parity and the rescue pass zeroes the other for the
+    next run (no memset per run); every run gives the same bits and count."""
+    b = W.generate(300, (1000, 1400), (150, 250), 0.08, seed=3)
+    ref = oracle_lib.pairs(b, nthreads=16)
+    bt = engine.Batch(b)
+    for _ in range(5):
+        bt.run()
+        assert_same(bt.results(), ref, "repeat")
+        assert bt.stats().n_rescued == int(ref["rescued"].sum()) > 0
+    bt.close()
