@@ -161,6 +161,11 @@ struct hc_phmm_batch {
     double* own_raw64 = nullptr;
     uint8_t* own_flag = nullptr;
     int* d_list = nullptr;
+    int* d_sorted = nullptr;      // fp64 pass: rescue list in class order (device-planned)
+    int* d_big = nullptr;         // fp64 pass: pairs too wide for the segmented kernel
+    int* d_big_count = nullptr;
+    Seg64Plan* d_plan = nullptr;
+    int64_t n_wide = 0;           // pairs with H > 64 * 32 (may need the anti-diagonal fp64 kernel)
     int* d_count = nullptr;       // rescue counters, one per run parity
     int parity = 0;               // run parity: which counter this run appends to
     char* dev_base = nullptr;     // the batch's device allocation
@@ -337,11 +342,13 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     std::vector<PairDesc> pd(npairs);
     int64_t cells = 0;
     int Hmax = 0;
+    int64_t n_wide = 0;
     for (int64_t p = 0; p < npairs; ++p) {
         const int r = pr[p], h = ph[p];
         pd[p] = PairDesc{int(row_off[r]), reads[r].len, int(hap_off[h]), haps[h].len};
         cells += int64_t(reads[r].len) * haps[h].len;
         Hmax = std::max(Hmax, haps[h].len);
+        n_wide += haps[h].len > 64 * 32;
     }
     std::vector<int> ord[2], lane_ord;
     lane_ord.reserve(npairs);
@@ -511,6 +518,10 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     const size_t o_flag = L.take(n1);
     const size_t o_list = L.take(sizeof(int) * n1);
     const size_t o_count = L.take(2 * sizeof(int));
+    const size_t o_sorted = L.take(sizeof(int) * n1);
+    const size_t o_big = L.take(sizeof(int) * n1);
+    const size_t o_bigc = L.take(sizeof(int));
+    const size_t o_plan = L.take(sizeof(Seg64Plan));
     const size_t o_carry = L.take(sizeof(float2) * size_t(carry_rows) * 64 * lane_p);
     const size_t total = L.off;
 
@@ -617,6 +628,11 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     b->own_flag = b->d_flag = reinterpret_cast<uint8_t*>(dev + o_flag);
     b->d_list = reinterpret_cast<int*>(dev + o_list);
     b->d_count = reinterpret_cast<int*>(dev + o_count);
+    b->d_sorted = reinterpret_cast<int*>(dev + o_sorted);
+    b->d_big = reinterpret_cast<int*>(dev + o_big);
+    b->d_big_count = reinterpret_cast<int*>(dev + o_bigc);
+    b->d_plan = reinterpret_cast<Seg64Plan*>(dev + o_plan);
+    b->n_wide = n_wide;
     b->d_carry = carry_rows ? reinterpret_cast<float2*>(dev + o_carry) : nullptr;
     *out = b;
     return HC_PHMM_OK;
@@ -699,20 +715,38 @@ int run(hc_phmm_batch* b, hipStream_t s)
     }
     HIP_TRY(hipEventRecord(b->ev[1], s));
     if (b->n > 0) {
-        // fp64 rescue (intel_pairhmm.hpp:137-139): one pair per wave, grid-stride
-        // over the device-built list, so no host round trip for its length.
-        DiagArgs a{};
-        a.pairs = b->d_pairs;
-        a.order = b->d_list;
-        a.n_slots_dev = count;
-        a.count_reset = b->d_count + (par ^ 1);
-        a.rows = b->d_rows;
-        a.hapw = b->d_hapw;
-        a.lut = g_eng.lut_d;
-        a.ring_len = b->Hmax + 2 * 64 + 16;
-        a.raw_out = b->d_raw64;
-        const int grid = int(std::min<int64_t>(b->n, 2048));
-        HIP_TRY(launch_diag_f64(64, a, grid, s));
+        // fp64 rescue (intel_pairhmm.hpp:137-139) over the device-built list, no
+        // host round trip for its length: device planning + column-segmented
+        // fp64 waves (grid-stride), then the anti-diagonal fp64 kernel for haps
+        // wider than 64 blocks of 32 (only launched if the batch has any).
+        Seg64Args r{};
+        r.pairs = b->d_pairs;
+        r.rows = b->d_rows;
+        r.hapw = b->d_hapw;
+        r.lut = g_eng.lut_d;
+        r.list = b->d_list;
+        r.count = count;
+        r.count_reset = b->d_count + (par ^ 1);
+        r.sorted = b->d_sorted;
+        r.big = b->d_big;
+        r.big_count = b->d_big_count;
+        r.plan = b->d_plan;
+        r.raw_out = b->d_raw64;
+        r.min_lanes = int64_t(2) * 4 * g_eng.n_cu * 64;
+        const int grid = int(std::min<int64_t>((b->n + 3) / 4, int64_t(2) * g_eng.n_cu));
+        HIP_TRY(launch_rescue_seg64(r, grid, s));
+        if (b->n_wide > 0) {
+            DiagArgs a{};
+            a.pairs = b->d_pairs;
+            a.order = b->d_big;
+            a.n_slots_dev = b->d_big_count;
+            a.rows = b->d_rows;
+            a.hapw = b->d_hapw;
+            a.lut = g_eng.lut_d;
+            a.ring_len = b->Hmax + 2 * 64 + 16;
+            a.raw_out = b->d_raw64;
+            HIP_TRY(launch_diag_f64(64, a, int(std::min<int64_t>(b->n_wide, 2048)), s));
+        }
     }
     HIP_TRY(hipEventRecord(b->ev[2], s));
     b->ran = true;

@@ -82,9 +82,9 @@ struct LaneArgs {
     int* rescue_count;
     double* raw64_zero;       // as DiagArgs::raw64_zero
 };
-// Variants of the lane kernel (lane_kernel.hip kVariants): pairs per lane P
-// (1, or 2 packed in float2 halves), register block width in columns, and the
-// waves per SIMD the register allocation targets. Variant 0 is the default.
+// Variants of the one-lane kernel (lane_kernel.hip kVariants): pairs per lane
+// P (1), register block width in columns, and the waves per SIMD the register
+// allocation targets. Variant 0 is the default.
 struct LaneVariant {
     int P, BC, occ;
 };
@@ -95,6 +95,36 @@ hipError_t launch_lane_f32(int variant, const LaneArgs& a, hipStream_t s);
 hipError_t launch_lane_seg_f32(const LaneArgs& a, hipStream_t s);
 bool seg_width_ok(int bc);
 constexpr int kSegMaxBC = 64;
+
+// fp64 rescue pass in column-segmented form, planned on the device
+// (lane_kernel.hip rescue_plan_kernel). Two width tiers: bc[0] for the whole
+// pass (32, or 16 / 8 when the list is short), bc[1] = 32 for the haps too
+// long for 64 lanes at bc[0]. Class c = tier * 7 + k holds pairs of 2^k lanes
+// (64 >> k pairs per wave); class 14 = haps wider than 64 blocks of 32
+// (anti-diagonal kernel, through `big`).
+constexpr int kSeg64Classes = 15;
+struct Seg64Plan {
+    int bc[2];
+    int n_class[kSeg64Classes];
+    int off_class[kSeg64Classes];   // class c's entries in `sorted` start here
+    int wave_base[kSeg64Classes];   // first wave of class c; [14] = total waves
+};
+struct Seg64Args {
+    const PairDesc* pairs;
+    const uint32_t* rows;
+    const uint32_t* hapw;
+    const double* lut;
+    const int* list;          // rescue list (fp32 pass, arbitrary order)
+    const int* count;         // its length
+    int* count_reset;         // the other run parity's counter, zeroed for the next run
+    int* sorted;              // list in class order (n entries)
+    int* big;                 // class 7 pairs
+    int* big_count;
+    Seg64Plan* plan;
+    double* raw_out;          // raw f64 sums by pair id
+    long long min_lanes;      // narrower blocks below this many lanes at bc = 32
+};
+hipError_t launch_rescue_seg64(const Seg64Args& a, int grid, hipStream_t s);
 
 // Launchers (kernels.hip). W = lanes per pair: 16, 32 or 64.
 hipError_t launch_diag_f32(int W, const DiagArgs& a, int grid, hipStream_t s);

@@ -8,12 +8,12 @@ import workloads as W
 pytestmark = pytest.mark.gpu
 
 # "diag" = anti-diagonal kernel; "laneN" = lane-per-pair kernel variant N
-# (lane_kernel.hip kVariants: 0 = 64-col blocks 3 waves/SIMD (default),
-# 1 = 64-col 2 waves, 2 = 32-col 4 waves, 3 = two pairs per lane, packed f32);
+# with the carry buffer (lane_kernel.hip kVariants: 0 = 64-col blocks 3
+# waves/SIMD, 1 = 64-col 2 waves, 2 = 32-col 4 waves);
 # "seg" = the default lane path: column-segmented waves (run_seg: a pair over
 # ceil(H/BC) lanes, BC per wave) for H <= 1024, one lane per pair above;
 # "segall" = every lane pair column-segmented (up to 64 lanes per pair).
-KERNELS = ["diag", "lane0", "lane1", "lane2", "lane3", "seg", "segall"]
+KERNELS = ["diag", "lane0", "lane1", "lane2", "seg", "segall"]
 
 
 @pytest.fixture(params=KERNELS)
@@ -255,3 +255,20 @@ def test_repeated_runs_reuse_rescue_counters(engine, oracle_lib):
         assert_same(bt.results(), ref, "repeat")
         assert bt.stats().n_rescued == int(ref["rescued"].sum()) > 0
     bt.close()
+
+
+@pytest.mark.parametrize("shape", ["short_list", "mid_list", "long_list", "wide_haps"])
+def test_fp64_rescue_tiers(engine, oracle_lib, shape):
+    """The fp64 rescue pass is planned on the device: block width 8 / 16 / 32
+    by rescue-list size (a short list is latency-bound), pairs binned into
+    2^k-lane classes, haps too wide for 64 blocks of 32 on the anti-diagonal
+    fp64 kernel. High substitution rates force most pairs into rescue."""
+    n, h, r = {"short_list": (40, (300, 900), (100, 250)),
+               "mid_list": (1500, (600, 1100), (150, 250)),
+               "long_list": (4500, (1000, 1200), (150, 250)),
+               "wide_haps": (60, (1800, 3000), (150, 250))}[shape]
+    b = W.generate(n, h, r, 0.08, seed=17)
+    ref = oracle_lib.pairs(b, nthreads=16)
+    assert ref["rescued"].sum() > n // 2
+    res = engine.pairs(b)
+    assert_same(res, ref, shape)
