@@ -633,7 +633,10 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
 
 // One-lane kernel variants: {pairs per lane, block columns, waves per SIMD}.
 // Block widths are multiples of 32 (a block starts on a match-word boundary).
-constexpr int kSegOcc = 3;     // waves per SIMD of the fp32 column-segmented kernel
+#ifndef HC_SEG_OCC
+#define HC_SEG_OCC 3
+#endif
+constexpr int kSegOcc = HC_SEG_OCC;   // waves per SIMD of the fp32 column-segmented kernel
 constexpr int kSeg64Occ = 2;   // fp64: 2 VGPRs per value
 static const LaneVariant kVariants[] = {
     {1, 64, 3}, {1, 64, 2}, {1, 32, 4},

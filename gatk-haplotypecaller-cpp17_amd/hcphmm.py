@@ -24,7 +24,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libhcpairhmm.so")
+# HC_PHMM_LIB: load another build of the library (A/B experiments only).
+LIB_PATH = os.environ.get("HC_PHMM_LIB") or os.path.join(HERE, "libhcpairhmm.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "hc_pairhmm.h")
 
 OK, EINVAL, ENODEV, EHIP, ENOMEM = 0, -1, -2, -3, -4
