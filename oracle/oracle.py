@@ -128,3 +128,58 @@ class Reference(_Lib):
 
 def reference_available() -> bool:
     return os.path.exists(REF_SO)
+
+
+# --------------------------------------------------------------------------
+# Smith-Waterman: oracle/sw_oracle.c (kind "port", in
+# liboracle.so) and the reference aligner (oracle/_ref/libref_sw.so).
+REF_SW_SO = os.path.join(HERE, "_ref", "libref_sw.so")
+SW_CIGAR_STRIDE = 4096
+
+
+class _SWLib:
+    def __init__(self, fn, nthreads_arg: bool):
+        self._fn = fn
+        self._nt = nthreads_arg
+        args = [C.c_long, _i64p, _i32p, _u8p, _i64p, _i32p, _u8p] + [C.c_int] * 6 + [_i32p, C.c_char_p, C.c_int]
+        fn.argtypes = args + ([C.c_int] if nthreads_arg else [])
+        fn.restype = C.c_int
+
+    def batch(self, b, params=(200, -150, -260, -11), overhang=9, shortcut=True, nthreads=1,
+              stride=SW_CIGAR_STRIDE):
+        """IntelSWAligner::align over a flat batch (sw_workloads layout).
+        Returns (offsets int32[n], cigars list[str])."""
+        n = len(b["ref_len"])
+        off = np.zeros(n, np.int32)
+        cig = C.create_string_buffer(max(1, n * stride))
+        refs = b["refs"] if len(b["refs"]) else np.zeros(1, np.uint8)
+        alts = b["alts"] if len(b["alts"]) else np.zeros(1, np.uint8)
+        extra = [nthreads] if self._nt else []
+        rc = self._fn(n, _ptr(b["ref_off"], _i64p), _ptr(b["ref_len"], _i32p), _ptr(refs, _u8p),
+                      _ptr(b["alt_off"], _i64p), _ptr(b["alt_len"], _i32p), _ptr(alts, _u8p),
+                      *params, overhang, int(bool(shortcut)), _ptr(off, _i32p), cig, stride, *extra)
+        if rc != 0:
+            raise RuntimeError("CIGAR buffer too small")
+        raw = cig.raw
+        cigars = [raw[k * stride:(k + 1) * stride].split(b"\0", 1)[0].decode() for k in range(n)]
+        return off, cigars
+
+
+class SWOracle(_SWLib):
+    def __init__(self, path: str = ORACLE_SO):
+        if not os.path.exists(path):
+            build(ref=False)
+        self.lib = C.CDLL(path)
+        super().__init__(self.lib.hco_sw_batch, True)
+
+
+class SWReference(_SWLib):
+    def __init__(self, path: str = REF_SW_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        self.lib = C.CDLL(path)
+        super().__init__(self.lib.ref_sw_align_batch, False)
+
+
+def sw_reference_available() -> bool:
+    return os.path.exists(REF_SW_SO)

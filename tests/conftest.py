@@ -44,3 +44,34 @@ def engine():
         hcphmm.build()
     hcphmm.init(0)
     return hcphmm
+
+
+SW_GOLDEN = os.path.join(ROOT, "tests", "golden", "sw_golden.npz")
+
+
+@pytest.fixture(scope="session")
+def sw_golden():
+    """Reference aligner outputs (tests/golden/make_sw_golden.py): per set a flat
+    batch, per case (set, params, strategy) offsets and CIGARs."""
+    g = np.load(SW_GOLDEN, allow_pickle=False)
+    d = {k: g[k] for k in g.files}
+    sets = {}
+    for k, v in d.items():
+        if "__" in k:
+            s, f = k.split("__", 1)
+            sets.setdefault(s, {})[f] = v
+    cases = []
+    for c in d["cases"]:
+        c = c.decode()
+        parts = c.split("_")
+        cases.append(dict(name=c, set=parts[0], params=tuple(int(x) for x in parts[1:5]),
+                          strategy=int(parts[5]), offset=d[c + "_offset"],
+                          cigar=[x.decode() for x in d[c + "_cigar"]]))
+    return dict(sets=sets, cases=cases)
+
+
+@pytest.fixture(scope="session")
+def sw_oracle_lib():
+    import oracle
+    oracle.build(ref=False)
+    return oracle.SWOracle()

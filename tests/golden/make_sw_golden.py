@@ -1,0 +1,61 @@
+"""Generate the Smith-Waterman golden fixtures from the REFERENCE aligner.
+
+Run in the build container (needs oracle/_ref/libref_sw.so, built by
+`make -C oracle ref` from /root/reference sources):
+
+    python tests/golden/make_sw_golden.py
+
+Writes tests/golden/sw_golden.npz: the inputs (flat layout of sw_workloads.py)
+and, per case, the reference's outputs of IntelSWAligner::align
+(intel_smithwaterman.hpp:29-44: all-match shortcut, then runSWOnePairBT_avx2,
+PairWiseSW.h:418-447):
+    <case>_offset   int32 alignment offset
+    <case>_cigar    CIGAR string (fixed-width bytes)
+Cases: the edge grid under every parameter set x overhang strategy, and
+region-shaped samples of W2 / W3 under NEW_SW_PARAMETERS + SOFTCLIP (the
+arguments graph_wrapper.hpp:235 uses).
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "gatk-haplotypecaller-cpp17_amd"))
+
+import oracle  # noqa: E402
+import sw_workloads as S  # noqa: E402
+
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "sw_golden.npz")
+
+
+def main():
+    ref = oracle.SWReference()
+    sets = {
+        "edge": S.from_pairs(S.edge_pairs()),
+        "w2": S.config("W2", 4),
+        "w3": S.config("W3", 2),
+    }
+    out = {}
+    for name, b in sets.items():
+        for k, v in b.items():
+            out[f"{name}__{k}"] = v
+    cases = [("edge", p, st) for p in S.PARAM_SETS for st in S.STRATEGIES]
+    cases += [("w2", S.NEW_SW_PARAMETERS, S.SOFTCLIP), ("w3", S.NEW_SW_PARAMETERS, S.SOFTCLIP)]
+    names = []
+    for set_name, p, st in cases:
+        off, cig = ref.batch(sets[set_name], p, st, shortcut=True)
+        case = f"{set_name}_{'_'.join(str(x) for x in p)}_{st}"
+        out[case + "_offset"] = off
+        out[case + "_cigar"] = np.array([c.encode() for c in cig])
+        names.append(case)
+    out["cases"] = np.array([n.encode() for n in names])
+    np.savez_compressed(OUT, **out)
+    print(f"wrote {OUT}: {len(names)} cases, {os.path.getsize(OUT)} bytes")
+
+
+if __name__ == "__main__":
+    main()
