@@ -821,6 +821,11 @@ int flat_views(int64_t n, const int64_t* read_off, const int32_t* R, const int64
 
 // --------------------------------------------------------------------------
 // C ABI
+namespace hcphmm {
+// Shared with sw_engine.cpp: one last-error slot per thread for the library.
+void set_last_error(const std::string& msg) { g_err = msg; }
+}  // namespace hcphmm
+
 extern "C" {
 
 int hc_phmm_version(void) { return 100; }

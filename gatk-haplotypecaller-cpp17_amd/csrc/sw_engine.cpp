@@ -1,0 +1,380 @@
+// Host engine + C ABI of the Smith-Waterman aligner (include/hc_sw.h).
+//
+// One batch = the loop of assembler/graph_wrapper.hpp:232-240 (every haplotype
+// of a region against the region's reference window), for any number of
+// regions at once:
+//   create   order pairs longest first, lay out backtrack/element space, one H2D
+//   run      sw_dp_kernel (DP + backtrack words + end point), sw_trace_kernel
+//            (getCIGAR + compaction)                              [device only]
+//   results  D2H offsets + packed CIGAR elements, "%d%c" formatting on the host
+//            (PairWiseSW.h:388-413)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/hc_pairhmm.h"
+#include "../../include/hc_sw.h"
+#include "sw_kernels.hpp"
+
+namespace hcphmm {
+void set_last_error(const std::string& msg);
+}
+
+using namespace hcsw;
+
+namespace {
+
+std::mutex g_mu;
+hipStream_t g_stream = nullptr;
+
+int fail(int code, const std::string& msg)
+{
+    hcphmm::set_last_error(msg);
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                 \
+    do {                                                                              \
+        hipError_t e_ = (expr);                                                       \
+        if (e_ != hipSuccess)                                                         \
+            return fail(HC_SW_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+int ensure_init(int device)
+{
+    if (g_stream) return HC_SW_OK;
+    const int rc = hc_phmm_init(0, device);   // device selection + gfx950 check
+    if (rc != HC_PHMM_OK) return rc;
+    HIP_TRY(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
+    return HC_SW_OK;
+}
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+struct hc_sw_batch {
+    int64_t n = 0;
+    int n1max = 0, n2max = 0;
+    int64_t cells = 0;
+    hc_sw_params params{};
+    int overhang = 9, shortcut = 1;
+    char* dev = nullptr;
+    SwPair* pairs = nullptr;
+    int32_t* order = nullptr;
+    uint8_t* refs = nullptr;
+    uint8_t* alts = nullptr;
+    SwResult* res = nullptr;
+    uint32_t* bt = nullptr;
+    uint32_t* elems = nullptr;
+    uint32_t* dense = nullptr;
+    int32_t* dense_base = nullptr;
+    int32_t* dense_count = nullptr;
+    int32_t* n_elems = nullptr;
+    int32_t* offsets = nullptr;
+    int64_t n_el_cap = 0;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    double dp_ms = 0, trace_ms = 0, run_ms = 0;
+    int64_t n_runs = 0;
+    bool ran = false;
+};
+
+namespace {
+
+void free_batch(hc_sw_batch* b)
+{
+    if (!b) return;
+    for (auto& e : b->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (b->dev) (void)hipFree(b->dev);
+    delete b;
+}
+
+int create(int64_t n, const int64_t* ref_off, const int32_t* ref_len, const uint8_t* refs,
+           const int64_t* alt_off, const int32_t* alt_len, const uint8_t* alts, hc_sw_params params,
+           int32_t overhang, int32_t shortcut, hc_sw_batch** out)
+{
+    if (!out || n < 0) return fail(HC_SW_EINVAL, "null output / negative count");
+    if (overhang < HC_SW_SOFTCLIP || overhang > HC_SW_IGNORE) return fail(HC_SW_EINVAL, "bad overhang strategy");
+    if (n > 0 && (!ref_off || !ref_len || !refs || !alt_off || !alt_len || !alts))
+        return fail(HC_SW_EINVAL, "null input array");
+    if (n > INT32_MAX / 2) return fail(HC_SW_EINVAL, "too many pairs");
+    auto* b = new (std::nothrow) hc_sw_batch;
+    if (!b) return fail(HC_SW_ENOMEM, "host allocation");
+    b->n = n;
+    b->params = params;
+    b->overhang = overhang;
+    b->shortcut = shortcut ? 1 : 0;
+
+    std::vector<SwPair> pairs(static_cast<size_t>(n));
+    int64_t ref_ext = 0, alt_ext = 0, bt_total = 0, el_total = 0;
+    for (int64_t k = 0; k < n; ++k) {
+        const int n1 = ref_len[k], n2 = alt_len[k];
+        if (n1 < 1 || n2 < 1 || n1 > HC_SW_MAX_LEN1 || n2 > HC_SW_MAX_LEN2 || ref_off[k] < 0 || alt_off[k] < 0) {
+            free_batch(b);
+            return fail(HC_SW_EINVAL, "pair " + std::to_string(k) + ": sequence length out of range [1, " +
+                                          std::to_string(HC_SW_MAX_LEN1) + "] x [1, " +
+                                          std::to_string(HC_SW_MAX_LEN2) + "] or negative offset");
+        }
+        SwPair& P = pairs[size_t(k)];
+        P.ref_off = ref_off[k];
+        P.alt_off = alt_off[k];
+        P.n1 = n1;
+        P.n2 = n2;
+        P.bt_off = bt_total;
+        P.el_off = el_total;
+        bt_total += bt_words(n1, n2);
+        el_total += n1 + n2 + 3;
+        ref_ext = std::max(ref_ext, ref_off[k] + n1);
+        alt_ext = std::max(alt_ext, alt_off[k] + n2);
+        b->n1max = std::max(b->n1max, n1);
+        b->n2max = std::max(b->n2max, n2);
+        b->cells += int64_t(n1) * n2;
+    }
+    // Longest pairs first: the tail of the launch is made of short waves.
+    std::vector<int32_t> order(static_cast<size_t>(n));
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) {
+        return int64_t(pairs[x].n1) * pairs[x].n2 > int64_t(pairs[y].n1) * pairs[y].n2;
+    });
+    b->n_el_cap = el_total;
+
+    // One device allocation: descriptors, inputs, outputs, scratch.
+    size_t off = 0;
+    auto carve = [&](size_t bytes) {
+        const size_t at = off;
+        off = align_up(off + std::max<size_t>(bytes, 1), 256);
+        return at;
+    };
+    const size_t o_pairs = carve(sizeof(SwPair) * size_t(n));
+    const size_t o_order = carve(sizeof(int32_t) * size_t(n));
+    const size_t o_refs = carve(size_t(ref_ext));
+    const size_t o_alts = carve(size_t(alt_ext));
+    const size_t in_bytes = off;
+    const size_t o_res = carve(sizeof(SwResult) * size_t(n));
+    const size_t o_bt = carve(sizeof(uint32_t) * size_t(bt_total));
+    const size_t o_el = carve(sizeof(uint32_t) * size_t(el_total));
+    const size_t o_dense = carve(sizeof(uint32_t) * size_t(el_total));
+    const size_t o_dbase = carve(sizeof(int32_t) * size_t(n));
+    const size_t o_dcount = carve(sizeof(int32_t));
+    const size_t o_nel = carve(sizeof(int32_t) * size_t(n));
+    const size_t o_offs = carve(sizeof(int32_t) * size_t(n));
+    if (hipMalloc(&b->dev, off) != hipSuccess) {
+        free_batch(b);
+        return fail(HC_SW_ENOMEM, "device allocation of " + std::to_string(off) + " bytes");
+    }
+    b->pairs = reinterpret_cast<SwPair*>(b->dev + o_pairs);
+    b->order = reinterpret_cast<int32_t*>(b->dev + o_order);
+    b->refs = reinterpret_cast<uint8_t*>(b->dev + o_refs);
+    b->alts = reinterpret_cast<uint8_t*>(b->dev + o_alts);
+    b->res = reinterpret_cast<SwResult*>(b->dev + o_res);
+    b->bt = reinterpret_cast<uint32_t*>(b->dev + o_bt);
+    b->elems = reinterpret_cast<uint32_t*>(b->dev + o_el);
+    b->dense = reinterpret_cast<uint32_t*>(b->dev + o_dense);
+    b->dense_base = reinterpret_cast<int32_t*>(b->dev + o_dbase);
+    b->dense_count = reinterpret_cast<int32_t*>(b->dev + o_dcount);
+    b->n_elems = reinterpret_cast<int32_t*>(b->dev + o_nel);
+    b->offsets = reinterpret_cast<int32_t*>(b->dev + o_offs);
+
+    // Stage the inputs in one host block, one H2D.
+    std::vector<char> stage(in_bytes);
+    std::memcpy(stage.data() + o_pairs, pairs.data(), sizeof(SwPair) * size_t(n));
+    std::memcpy(stage.data() + o_order, order.data(), sizeof(int32_t) * size_t(n));
+    if (ref_ext) std::memcpy(stage.data() + o_refs, refs, size_t(ref_ext));
+    if (alt_ext) std::memcpy(stage.data() + o_alts, alts, size_t(alt_ext));
+    for (auto& e : b->ev) {
+        if (hipEventCreate(&e) != hipSuccess) {
+            free_batch(b);
+            return fail(HC_SW_EHIP, "hipEventCreate");
+        }
+    }
+    if (hipMemcpyAsync(b->dev, stage.data(), in_bytes, hipMemcpyHostToDevice, g_stream) != hipSuccess ||
+        hipStreamSynchronize(g_stream) != hipSuccess) {
+        free_batch(b);
+        return fail(HC_SW_EHIP, "H2D of the batch inputs");
+    }
+    *out = b;
+    return HC_SW_OK;
+}
+
+int run(hc_sw_batch* b, hipStream_t s)
+{
+    if (b->n == 0) {
+        b->ran = true;
+        return HC_SW_OK;
+    }
+    SwDpArgs d{};
+    d.pairs = b->pairs;
+    d.order = b->order;
+    d.n = int(b->n);
+    d.refs = b->refs;
+    d.alts = b->alts;
+    d.bt = b->bt;
+    d.res = b->res;
+    d.match = b->params.match;
+    d.mismatch = b->params.mismatch;
+    d.open = b->params.open;
+    d.extend = b->params.extend;
+    d.overhang = b->overhang;
+    d.shortcut = b->shortcut;
+    d.n2max = b->n2max;
+    SwTraceArgs t{};
+    t.pairs = b->pairs;
+    t.res = b->res;
+    t.bt = b->bt;
+    t.n = int(b->n);
+    t.overhang = b->overhang;
+    t.elems = b->elems;
+    t.dense = b->dense;
+    t.dense_base = b->dense_base;
+    t.dense_count = b->dense_count;
+    t.n_elems = b->n_elems;
+    t.offsets = b->offsets;
+    HIP_TRY(hipEventRecord(b->ev[0], s));
+    HIP_TRY(launch_dp(d, b->n1max, s));
+    HIP_TRY(hipEventRecord(b->ev[1], s));
+    HIP_TRY(hipMemsetAsync(b->dense_count, 0, sizeof(int32_t), s));
+    HIP_TRY(launch_trace(t, s));
+    HIP_TRY(hipEventRecord(b->ev[2], s));
+    HIP_TRY(hipEventSynchronize(b->ev[2]));
+    float a = 0, c = 0, w = 0;
+    HIP_TRY(hipEventElapsedTime(&a, b->ev[0], b->ev[1]));
+    HIP_TRY(hipEventElapsedTime(&c, b->ev[1], b->ev[2]));
+    HIP_TRY(hipEventElapsedTime(&w, b->ev[0], b->ev[2]));
+    b->dp_ms += a;
+    b->trace_ms += c;
+    b->run_ms += w;
+    ++b->n_runs;
+    b->ran = true;
+    return HC_SW_OK;
+}
+
+int results(hc_sw_batch* b, int32_t* offsets, char* cigars, int32_t stride, int32_t* scores)
+{
+    if (!b->ran) return fail(HC_SW_EINVAL, "batch has not run");
+    const int64_t n = b->n;
+    if (n == 0) return HC_SW_OK;
+    if (!offsets || !cigars || stride < 2) return fail(HC_SW_EINVAL, "null output / stride < 2");
+    int32_t total = 0;
+    HIP_TRY(hipMemcpy(&total, b->dense_count, sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (total < 0 || total > b->n_el_cap) return fail(HC_SW_EHIP, "corrupt CIGAR element count");
+    std::vector<int32_t> base(static_cast<size_t>(n)), cnt(static_cast<size_t>(n));
+    std::vector<uint32_t> dense(size_t(std::max(total, 1)));
+    HIP_TRY(hipMemcpy(offsets, b->offsets, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(base.data(), b->dense_base, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(cnt.data(), b->n_elems, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost));
+    if (total) HIP_TRY(hipMemcpy(dense.data(), b->dense, sizeof(uint32_t) * size_t(total), hipMemcpyDeviceToHost));
+    if (scores) {
+        std::vector<SwResult> r(static_cast<size_t>(n));
+        HIP_TRY(hipMemcpy(r.data(), b->res, sizeof(SwResult) * size_t(n), hipMemcpyDeviceToHost));
+        for (int64_t k = 0; k < n; ++k) scores[k] = r[size_t(k)].score;
+    }
+    bool too_long = false;
+    for (int64_t k = 0; k < n; ++k) {
+        char* o = cigars + size_t(k) * size_t(stride);
+        int pos = 0;
+        // Elements are in traceback order: print them back to front (:388-413).
+        for (int e = cnt[size_t(k)] - 1; e >= 0 && pos >= 0; --e) {
+            const uint32_t v = dense[size_t(base[size_t(k)] + e)];
+            const int op = int(v & 15);
+            const char ch = op == kOpM ? 'M' : op == kOpI ? 'I' : op == kOpD ? 'D' : op == kOpS ? 'S' : 'R';
+            const int w = std::snprintf(o + pos, size_t(stride - pos), "%u%c", v >> 4, ch);
+            pos = (w < 0 || pos + w >= stride) ? -1 : pos + w;
+        }
+        if (pos < 0) {
+            too_long = true;
+            o[0] = 0;
+        } else if (cnt[size_t(k)] == 0) {
+            o[0] = 0;
+        }
+    }
+    if (too_long) return fail(HC_SW_ERANGE, "a CIGAR does not fit in the stride");
+    return HC_SW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hc_sw_init(int device)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    return ensure_init(device);
+}
+
+int hc_sw_batch_create(int64_t n, const int64_t* ref_off, const int32_t* ref_len, const uint8_t* refs,
+                       const int64_t* alt_off, const int32_t* alt_len, const uint8_t* alts, hc_sw_params params,
+                       int32_t overhang, int32_t shortcut, hc_sw_batch** out)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    const int rc = ensure_init(-1);
+    if (rc) return rc;
+    return create(n, ref_off, ref_len, refs, alt_off, alt_len, alts, params, overhang, shortcut, out);
+}
+
+int hc_sw_batch_run(hc_sw_batch* b, void* stream)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!b) return fail(HC_SW_EINVAL, "null batch");
+    return run(b, stream ? static_cast<hipStream_t>(stream) : g_stream);
+}
+
+int hc_sw_batch_results(hc_sw_batch* b, int32_t* offsets, char* cigars, int32_t stride, int32_t* scores)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!b) return fail(HC_SW_EINVAL, "null batch");
+    return results(b, offsets, cigars, stride, scores);
+}
+
+int hc_sw_batch_stats(hc_sw_batch* b, hc_sw_stats* st)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!b || !st) return fail(HC_SW_EINVAL, "null batch / stats");
+    st->n_pairs = b->n;
+    st->cells = b->cells;
+    st->n_shortcut = 0;
+    if (b->ran && b->n) {
+        std::vector<SwResult> r(size_t(b->n));
+        HIP_TRY(hipMemcpy(r.data(), b->res, sizeof(SwResult) * size_t(b->n), hipMemcpyDeviceToHost));
+        for (const auto& x : r) st->n_shortcut += x.shortcut ? 1 : 0;
+    }
+    const double k = b->n_runs ? 1.0 / double(b->n_runs) : 0.0;
+    st->dp_ms = b->dp_ms * k;
+    st->trace_ms = b->trace_ms * k;
+    st->run_ms = b->run_ms * k;
+    st->n_runs = b->n_runs;
+    b->dp_ms = b->trace_ms = b->run_ms = 0;
+    b->n_runs = 0;
+    return HC_SW_OK;
+}
+
+int hc_sw_batch_destroy(hc_sw_batch* b)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    free_batch(b);
+    return HC_SW_OK;
+}
+
+int hc_sw_align_flat(int64_t n, const int64_t* ref_off, const int32_t* ref_len, const uint8_t* refs,
+                     const int64_t* alt_off, const int32_t* alt_len, const uint8_t* alts, hc_sw_params params,
+                     int32_t overhang, int32_t shortcut, int32_t* offsets, char* cigars, int32_t stride)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    int rc = ensure_init(-1);
+    if (rc) return rc;
+    hc_sw_batch* b = nullptr;
+    rc = create(n, ref_off, ref_len, refs, alt_off, alt_len, alts, params, overhang, shortcut, &b);
+    if (rc) return rc;
+    rc = run(b, g_stream);
+    if (!rc) rc = results(b, offsets, cigars, stride, nullptr);
+    free_batch(b);
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,338 @@
+// Smith-Waterman (Gotoh, int32) with backtrack on gfx950.
+//
+// Reference: src/haplotypecaller/smithwaterman/native/PairWiseSW.h — the AVX2
+// anti-diagonal sweep smithWatermanBackTrack (:41-238, cell update MAIN_CODE
+// :4-38), the end-point scan (:201-226) and getCIGAR (:240-415).
+//
+// sw_dp_kernel: one wave per pair. The 64 lanes own 64 consecutive rows of
+// seq1 (a stripe) and sweep the seq2 columns with a one-row skew: at step t
+// lane k computes cell (64s + k + 1, t - k + 1). The upper neighbour's H and F
+// arrive from lane k-1 by DPP wave_shr:1 — the reference's _vector_shift moves
+// become one v_mov_dpp each — and lane 0 takes them from an LDS row buffer that
+// holds the previous stripe's last row (written in place by the stripe's lanes,
+// the last writer of each column being lane 63). The alt base travels the same
+// way. Each lane packs its cells' 4-bit backtrack codes (op | INSERT_EXT |
+// DELETE_EXT) into one 32-bit word per 8 steps and stores it coalesced (a wave
+// writes 256 contiguous bytes). After the last stripe the wave picks the end
+// point among the last-row (LDS row buffer) and last-column (LDS) candidates
+// with the reference's tie-breaks, in the reference's anti-diagonal order.
+//
+// sw_trace_kernel: one lane per pair walks the backtrack words from the end
+// point (getCIGAR's state machine) and writes run-length CIGAR elements.
+#include "sw_kernels.hpp"
+
+#include <climits>
+
+namespace hcsw {
+namespace {
+
+__device__ __forceinline__ int shr1(int old, int v)
+{
+    // DPP wave_shr:1: lane k receives lane k-1's v; lane 0 keeps `old`.
+    return __builtin_amdgcn_update_dpp(old, v, 0x138, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ int wave_max(int v)
+{
+    for (int o = 32; o; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
+
+__device__ __forceinline__ int wave_sum(int v)
+{
+    for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// H(x, 0) and H(0, x) for x >= 1 (PairWiseSW.h:188-197); H(0, 0) = 0 (:80).
+__device__ __forceinline__ int boundary(int overhang, int open, int extend, int x)
+{
+    return (x > 0 && (overhang == 10 || overhang == 11)) ? open + (x - 1) * extend : 0;
+}
+
+struct Lane {
+    int h;      // H(i, j) of this lane's last cell (= H(i, j-1) for the next one)
+    int e;      // E(i, j)
+    int f;      // F(i, j)
+    int diag;   // H(i-1, j-1) for the next cell
+    int ab;     // seq2 base of this lane's column
+    uint32_t acc;
+};
+
+// One cell of MAIN_CODE (PairWiseSW.h:4-38) per lane.
+//   MASK: lanes outside columns [0, n2) keep their state (skew fill / drain).
+//   LASTW: last, partial stripe — lanes past seq1's end do not write the row buffer.
+template <bool MASK, bool LASTW>
+__device__ __forceinline__ void step(Lane& L, int t, int lane, int n2, int rb, bool row_ok, int uh, int uf,
+                                     int ua, int match, int mismatch, int open, int extend, int* rowH,
+                                     int* rowF)
+{
+    const int up_h = shr1(uh, L.h);   // H(i-1, j)
+    const int up_f = shr1(uf, L.f);   // F(i-1, j)
+    L.ab = shr1(ua, L.ab);
+    const int eo = L.h + open, ee = L.e + extend;
+    const int en = max(eo, ee);
+    const int fo = up_h + open, fe = up_f + extend;
+    const int fn = max(fe, fo);
+    int hn = max(kMinCutoff, L.diag + (L.ab == rb ? match : mismatch));
+    int b = en > hn ? 1 : 0;   // INSERT
+    hn = max(hn, en);
+    b = fn > hn ? 2 : b;       // DELETE
+    hn = max(hn, fn);
+    b |= (eo > ee ? 0 : 4) | (fo > fe ? 0 : 8);   // INSERT_EXT / DELETE_EXT
+    L.acc = (L.acc << 4) | uint32_t(b);
+    L.diag = up_h;
+    if (MASK) {
+        const bool act = unsigned(t - lane) < unsigned(n2);
+        L.h = act ? hn : L.h;
+        L.e = act ? en : L.e;
+        L.f = act ? fn : L.f;
+    } else {
+        L.h = hn;
+        L.e = en;
+        L.f = fn;
+    }
+    if (!LASTW || row_ok) {
+        rowH[64 + t - lane] = L.h;
+        rowF[64 + t - lane] = L.f;
+    }
+}
+
+template <bool LASTW>
+__device__ __forceinline__ void stripe(Lane& L, int lane, int n2, int rb, bool row_ok, int T, uint32_t* btw,
+                                       int match, int mismatch, int open, int extend, int* rowH, int* rowF,
+                                       const int* altI)
+{
+    for (int t0 = 0; t0 < T; t0 += kGroup) {
+        int uh[kGroup], uf[kGroup], ua[kGroup];
+#pragma unroll
+        for (int k = 0; k < kGroup; ++k) {
+            uh[k] = rowH[64 + t0 + k];
+            uf[k] = rowF[64 + t0 + k];
+            ua[k] = altI[t0 + k];
+        }
+        if (t0 >= kStripe && t0 + kGroup <= n2) {
+#pragma unroll
+            for (int k = 0; k < kGroup; ++k)
+                step<false, LASTW>(L, t0 + k, lane, n2, rb, row_ok, uh[k], uf[k], ua[k], match, mismatch, open,
+                                   extend, rowH, rowF);
+        } else {
+#pragma unroll
+            for (int k = 0; k < kGroup; ++k)
+                step<true, LASTW>(L, t0 + k, lane, n2, rb, row_ok, uh[k], uf[k], ua[k], match, mismatch, open,
+                                  extend, rowH, rowF);
+        }
+        btw[(t0 / kGroup) * kStripe + lane] = L.acc;
+    }
+}
+
+__global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
+{
+    extern __shared__ int lds[];
+    const int lane = threadIdx.x;
+    const int p = a.order[blockIdx.x];
+    const SwPair P = a.pairs[p];
+    const int n1 = __builtin_amdgcn_readfirstlane(P.n1);
+    const int n2 = __builtin_amdgcn_readfirstlane(P.n2);
+    const uint8_t* s1 = a.refs + P.ref_off;
+    const uint8_t* s2 = a.alts + P.alt_off;
+
+    // IntelSWAligner::is_all_match (intel_smithwaterman.hpp:47-58).
+    if (a.shortcut && n1 == n2) {
+        int mm = 0;
+        for (int x = lane; x < n1; x += 64) mm += s1[x] != s2[x];
+        if (wave_sum(mm) <= 2) {
+            if (lane == 0) a.res[p] = SwResult{0, 0, 0, 1};
+            return;
+        }
+    }
+
+    const int slots = row_slots(a.n2max);
+    int* rowH = lds;
+    int* rowF = rowH + slots;
+    int* altI = rowF + slots;        // stripe_steps(n2max) + 8 entries
+    int* colC = altI + slots;        // H(i, n2), i = 1..n1
+    const int open = a.open, extend = a.extend, ovh = a.overhang;
+    const int T = stripe_steps(n2);
+
+    // Row 0: H(0, j) = boundary, F(0, j) = LOW (PairWiseSW.h:72-75,198).
+    for (int j = lane; j < kStripe + T; j += 64) {
+        rowH[j] = j >= 64 ? boundary(ovh, open, extend, j - 63) : 0;
+        rowF[j] = kLow;
+    }
+    for (int c = lane; c < T + kGroup; c += 64) altI[c] = c < n2 ? int(s2[c]) : -1;
+    __syncthreads();
+
+    const int nstripes = (n1 + kStripe - 1) / kStripe;
+    uint32_t* bt = a.bt + P.bt_off;
+    const int nw = T / kGroup;
+    for (int s = 0; s < nstripes; ++s) {
+        const int i = s * kStripe + lane + 1;
+        const bool row_ok = i <= n1;
+        Lane L;
+        L.h = boundary(ovh, open, extend, i);   // H(i, 0)
+        L.e = kLow;                              // E(i, 0) (:199)
+        L.f = kLow;
+        L.diag = boundary(ovh, open, extend, s * kStripe);   // lane 0: H(64s, 0)
+        L.ab = -1;
+        L.acc = 0;
+        const int rb = row_ok ? int(s1[i - 1]) : -2;
+        uint32_t* btw = bt + int64_t(s) * nw * kStripe;
+        if (s == nstripes - 1 && (n1 % kStripe) != 0)
+            stripe<true>(L, lane, n2, rb, row_ok, T, btw, a.match, a.mismatch, open, extend, rowH, rowF, altI);
+        else
+            stripe<false>(L, lane, n2, rb, row_ok, T, btw, a.match, a.mismatch, open, extend, rowH, rowF, altI);
+        if (row_ok) colC[i] = L.h;   // H(i, n2): frozen since the lane left column n2
+        __syncthreads();
+    }
+
+    // End point (PairWiseSW.h:201-226): candidates in anti-diagonal order d =
+    // 1..n1+n2, the last-row cell (n1, d-n1) before the last-column cell
+    // (d-n2, n2); the last row counts only for SOFTCLIP / IGNORE. Every
+    // candidate with the best score is then replayed in that order through the
+    // reference's replacement rules.
+    const bool use_row = ovh == 9 || ovh == 12;
+    const int D = n1 + n2;
+    int mx = INT_MIN;
+    for (int d0 = 1; d0 <= D; d0 += 32) {
+        const int d = d0 + (lane >> 1);
+        const bool col = lane & 1;
+        const bool ok = col ? (d > n2 && d <= D) : (use_row && d > n1 && d <= D);
+        if (ok) mx = max(mx, col ? colC[d - n2] : rowH[63 + d - n1]);
+    }
+    const int best = wave_max(mx);
+    int bi = 0, bj = 0;
+    bool have = false;
+    for (int d0 = 1; d0 <= D; d0 += 32) {
+        const int d = d0 + (lane >> 1);
+        const bool col = lane & 1;
+        const bool ok = col ? (d > n2 && d <= D) : (use_row && d > n1 && d <= D);
+        const bool tie = ok && (col ? colC[d - n2] : rowH[63 + d - n1]) == best;
+        uint64_t m = __builtin_amdgcn_ballot_w64(tie);
+        while (m) {
+            const int l = __builtin_ctzll(m);
+            m &= m - 1;
+            const int dd = d0 + (l >> 1);
+            if (l & 1) {
+                const int ci = dd - n2;
+                if (!have || bj == n2 || abs(ci - n2) <= abs(bi - bj)) { bi = ci; bj = n2; have = true; }
+            } else {
+                const int cj = dd - n1;
+                if (!have || abs(n1 - cj) < abs(bi - bj)) { bi = n1; bj = cj; have = true; }
+            }
+        }
+    }
+    if (lane == 0) a.res[p] = SwResult{best, bi, bj, 0};
+}
+
+__device__ __forceinline__ void push(uint32_t* el, int& cnt, int& op, int& len, int nop, int nlen)
+{
+    if (nop == op) {
+        len += nlen;
+    } else {
+        if (op >= 0) el[cnt++] = (uint32_t(len) << 4) | uint32_t(op);
+        op = nop;
+        len = nlen;
+    }
+}
+
+// getCIGAR (PairWiseSW.h:240-415), equal neighbours merged on the fly (the
+// reference merges them afterwards, :368-386: same result).
+__global__ __launch_bounds__(64) void sw_trace_kernel(SwTraceArgs a)
+{
+    const int p = blockIdx.x * 64 + threadIdx.x;
+    if (p >= a.n) return;
+    const SwPair P = a.pairs[p];
+    const SwResult r = a.res[p];
+    uint32_t* el = a.elems + P.el_off;
+    const int n1 = P.n1, n2 = P.n2;
+    if (r.shortcut) {
+        const int base = atomicAdd(a.dense_count, 1);
+        a.dense[base] = (uint32_t(n1) << 4) | kOpM;
+        a.dense_base[p] = base;
+        a.n_elems[p] = 1;
+        a.offsets[p] = 0;
+        return;
+    }
+    const uint32_t* bt = a.bt + P.bt_off;
+    const int nw = stripe_steps(n2) / kGroup;
+    const int ovh = a.overhang;
+    int i = r.max_i, j = r.max_j;
+    if (ovh == 10) {
+        i = n1;
+        j = n2;
+    } else if (ovh == 11) {
+        j = n2;
+    }
+    int cnt = 0, op = -1, len = 0;
+    if (j < n2) push(el, cnt, op, len, kOpS, n2 - j);
+    int state = 0;
+    while (i > 0 && j > 0) {
+        const int k = (i - 1) & (kStripe - 1), s = (i - 1) / kStripe, t = j - 1 + k;
+        const uint32_t w = bt[(int64_t(s) * nw + (t >> 3)) * kStripe + k];
+        const int b = (w >> ((7 - (t & 7)) * 4)) & 15;
+        if (state == 4) {
+            --j;
+            push(el, cnt, op, len, kOpI, 1);
+            state = b & 4;
+        } else if (state == 8) {
+            --i;
+            push(el, cnt, op, len, kOpD, 1);
+            state = b & 8;
+        } else if ((b & 3) == 0) {
+            --i;
+            --j;
+            push(el, cnt, op, len, kOpM, 1);
+            state = 0;
+        } else if ((b & 3) == 1) {
+            --j;
+            push(el, cnt, op, len, kOpI, 1);
+            state = b & 4;
+        } else {
+            --i;
+            push(el, cnt, op, len, kOpD, 1);
+            state = b & 8;
+        }
+    }
+    int offset;
+    if (ovh == 9) {
+        if (j > 0) push(el, cnt, op, len, kOpS, j);
+        offset = i;
+    } else if (ovh == 12) {
+        if (j > 0) len += j;   // the last element repeated over the overhang (:345-352)
+        offset = i - j;
+    } else {
+        if (i > 0) push(el, cnt, op, len, kOpD, i);
+        else if (j > 0) push(el, cnt, op, len, kOpI, j);
+        offset = 0;
+    }
+    if (op >= 0) el[cnt++] = (uint32_t(len) << 4) | uint32_t(op);
+    const int base = atomicAdd(a.dense_count, cnt);
+    for (int e = 0; e < cnt; ++e) a.dense[base + e] = el[e];
+    a.dense_base[p] = base;
+    a.n_elems[p] = cnt;
+    a.offsets[p] = offset;
+}
+
+}  // namespace
+
+size_t dp_lds_bytes(int n1max, int n2max)
+{
+    return sizeof(int) * (3 * size_t(row_slots(n2max)) + size_t(n1max) + 1);
+}
+
+hipError_t launch_dp(const SwDpArgs& a, int n1max, hipStream_t s)
+{
+    if (a.n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(sw_dp_kernel, dim3(a.n), dim3(64), dp_lds_bytes(n1max, a.n2max), s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_trace(const SwTraceArgs& a, hipStream_t s)
+{
+    if (a.n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(sw_trace_kernel, dim3((a.n + 63) / 64), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace hcsw

@@ -1,0 +1,98 @@
+"""GPU parity: the HIP Smith-Waterman aligner (through the C ABI) against the
+reference aligner's golden outputs and the oracle — every offset and CIGAR
+identical. Run on an MI355X: pytest -m gpu."""
+import re
+
+import numpy as np
+import pytest
+
+import sw_workloads as S
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sw():
+    import hcsw
+    hcsw.init(0)
+    return hcsw
+
+
+def test_sw_golden_every_case(sw, sw_golden):
+    for c in sw_golden["cases"]:
+        b = sw_golden["sets"][c["set"]]
+        off, cig = sw.align_flat(b, c["params"], c["strategy"], True)
+        bad = [k for k in range(len(cig)) if cig[k] != c["cigar"][k] or off[k] != c["offset"][k]]
+        assert not bad, (c["name"], len(bad), [(k, cig[k], c["cigar"][k], off[k], c["offset"][k]) for k in bad[:3]])
+
+
+@pytest.mark.parametrize("strategy", S.STRATEGIES)
+def test_sw_no_shortcut_vs_oracle(sw, sw_oracle_lib, strategy):
+    # runSWOnePairBT semantics (no all-match shortcut) on the edge grid.
+    b = S.from_pairs(S.edge_pairs(seed=5))
+    for p in (S.NEW_SW_PARAMETERS, S.STANDARD_NGS):
+        o_off, o_cig = sw_oracle_lib.batch(b, p, strategy, shortcut=False, nthreads=8)
+        off, cig = sw.align_flat(b, p, strategy, False)
+        assert np.array_equal(off, o_off) and cig == o_cig, (p, strategy)
+
+
+@pytest.mark.parametrize("name,nreg", [("W1", None), ("W2", 24), ("W3", 4)])
+def test_sw_regions_vs_oracle(sw, sw_oracle_lib, name, nreg):
+    b = S.config(name, nreg)
+    o_off, o_cig = sw_oracle_lib.batch(b, nthreads=8)
+    off, cig = sw.align_flat(b)
+    bad = [k for k in range(len(cig)) if cig[k] != o_cig[k] or off[k] != o_off[k]]
+    assert not bad, (len(bad), [(k, cig[k], o_cig[k]) for k in bad[:3]])
+
+
+def test_sw_heavy_indels_and_repeats_vs_oracle(sw, sw_oracle_lib):
+    b = S.regions(8, 64, (200, 900), seed=77, snp=0.05, indel=0.02, trim=0.6)
+    for p in S.PARAM_SETS:
+        for st in (S.SOFTCLIP, S.IGNORE):
+            o = sw_oracle_lib.batch(b, p, st, nthreads=8)
+            g = sw.align_flat(b, p, st)
+            assert np.array_equal(g[0], o[0]) and g[1] == o[1], (p, st)
+
+
+def test_sw_batch_rerun_and_full_w2_properties(sw, sw_oracle_lib):
+    """Full W2 (512 regions x 128 haps): every CIGAR consumes its whole alt,
+    reruns are identical, and a seeded sample matches the oracle."""
+    b = S.config("W2")
+    bt = sw.Batch(b)
+    bt.run()
+    off1, cig1, sc1 = bt.results(scores=True)
+    bt.run()
+    off2, cig2, sc2 = bt.results(scores=True)
+    assert np.array_equal(off1, off2) and cig1 == cig2 and np.array_equal(sc1, sc2)
+    st = bt.stats()
+    assert st["n_pairs"] == len(cig1) and st["n_shortcut"] >= 512
+    for k, c in enumerate(cig1):
+        ops = re.findall(r"(\d+)([MIDS])", c)
+        assert "".join(n + o for n, o in ops) == c
+        assert sum(int(n) for n, o in ops if o in "MIS") == b["alt_len"][k]
+        assert off1[k] + sum(int(n) for n, o in ops if o in "MD") <= b["ref_len"][k]
+    idx = np.random.default_rng(3).choice(len(cig1), 1500, replace=False)
+    sub = S.subset(b, idx)
+    o_off, o_cig = sw_oracle_lib.batch(sub, nthreads=8)
+    assert np.array_equal(off1[idx], o_off) and [cig1[k] for k in idx] == o_cig
+    bt.close()
+
+
+def test_sw_rejects_lengths_past_reference_limits(sw):
+    b = S.from_pairs([(b"A" * 1024, b"A" * 10)])
+    with pytest.raises(sw.SWError) as e:
+        sw.align_flat(b)
+    assert e.value.code == sw.EINVAL
+    b = S.from_pairs([(b"A" * 10, b"A" * 1025)])
+    with pytest.raises(sw.SWError):
+        sw.align_flat(b)
+
+
+def test_sw_aligner_mirror(sw, sw_oracle_lib):
+    al = sw.SWAligner()
+    ref = b"ACGTTGCAAGGCTTACCGATCGATCGGATCCTAGGCTAGCTAGGATCCGA" * 4
+    alt = ref[:60] + b"TTT" + ref[60:150] + ref[155:]
+    got = al.align(ref, alt)
+    o_off, o_cig = sw_oracle_lib.batch(S.from_pairs([(ref, alt)]))
+    assert got == (int(o_off[0]), o_cig[0])
+    assert al.align(ref, ref) == (0, f"{len(ref)}M")
