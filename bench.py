@@ -81,6 +81,71 @@ def traffic_from_profiles(workload, cells):
         return None, None
 
 
+SW_OPS_PER_CELL = 22       # MAIN_CODE int32 vector ops per cell (PairWiseSW.h:4-38)
+INT32_VALU_PEAK_TOPS = 39.3   # 256 CU x 4 SIMD x 16 lanes x 2.4 GHz (no packed int32 ops)
+
+
+def sw_secondary(no_cpu: bool):
+    """Smith-Waterman on W2: 512 region windows (300-600
+    bp) x 128 haplotypes, NEW_SW_PARAMETERS, SOFTCLIP, all-match shortcut — the
+    graph_wrapper.hpp:232-240 loop for 512 regions in one device pass. Device
+    pass timed with HIP events; the reference aligner (oracle/_ref, 1 thread,
+    as the reference calls it) on the first 16 regions, checked for identical
+    offsets and CIGARs."""
+    import hcsw
+    import sw_workloads as SWW
+    hcsw.init(int(os.environ.get("LOCAL_RANK", "0")) % max(1, __import__("torch").cuda.device_count()))
+    b = SWW.config("W2")
+    bt = hcsw.Batch(b)
+    for _ in range(2):
+        bt.run()
+    bt.stats()
+    for _ in range(5):
+        bt.run()
+    st = bt.stats()
+    off, cig = bt.results()
+    bt.close()
+    cells = st["cells"]
+    tcups = cells / (st["dp_ms"] * 1e-3) / 1e12
+    ent = dict(workload="W2", pairs=st["n_pairs"], shortcut_pairs=st["n_shortcut"], dp_cells=cells,
+               dp_kernel_ms=round(st["dp_ms"], 3), trace_kernel_ms=round(st["trace_ms"], 3),
+               device_pass_ms=round(st["run_ms"], 3), gcups=round(cells / (st["run_ms"] * 1e-3) / 1e9, 1),
+               roofline=dict(bound="valu-int32", achieved=round(tcups * SW_OPS_PER_CELL, 2),
+                             peak=INT32_VALU_PEAK_TOPS, unit="Top/s",
+                             frac=round(tcups * SW_OPS_PER_CELL / INT32_VALU_PEAK_TOPS, 4),
+                             note=f"{SW_OPS_PER_CELL} int32 ops/cell x DP cells / sw_dp_kernel time"))
+    # one region through the host API (the real per-region call shape)
+    one = SWW.config("W1")
+    hcsw.align_flat(one)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        hcsw.align_flat(one)
+    ent["region_415x128_call_ms"] = round((time.perf_counter() - t0) / 5 * 1e3, 3)
+    if not no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        kind = "reference"
+        try:
+            ref = oracle.SWReference()
+        except FileNotFoundError:
+            ref, kind = oracle.SWOracle(), "port"
+        nreg = 16
+        idx = np.arange(nreg * 128)
+        sub = SWW.subset(b, idx)
+        t0 = time.perf_counter()
+        r_off, r_cig = ref.batch(sub)
+        dt = time.perf_counter() - t0
+        same = np.array_equal(r_off, off[idx]) and r_cig == [cig[k] for k in idx]
+        ent["cpu_baseline"] = dict(value=round(SWW.dp_cells(sub) / dt / 1e9, 3), unit="GCUPS", cores=1, kind=kind,
+                                   sample=f"first {nreg} regions of W2 ({len(idx)} pairs), IntelSWAligner::align "
+                                          f"semantics, 1 thread", seconds=round(dt, 3))
+        ent["parity_vs_cpu_reference"] = "identical" if same else "MISMATCH"
+        t0 = time.perf_counter()
+        ref.batch(one)
+        ent["region_415x128_cpu_reference_1core_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+    return ent
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -264,6 +329,7 @@ def main():
         rc = sum(W.cells(W.region_flat(r, h)) for r, h in regs[:1]) * len(regs)
         sec["regions_64x_415x32_one_call"] = dict(regions=len(regs), cells_approx=rc, call_ms=round(dt * 1e3, 2),
                                                    gcups=round(rc / dt / 1e9, 2))
+        sec["smith_waterman"] = sw_secondary(args.no_cpu)
         out["secondary"] = sec
     if world > 1:
         out["gather"] = f"dist.gather ({'gloo, rehearsal' if gloo else 'RCCL'}) of raw_f32 + raw_f64 per step"

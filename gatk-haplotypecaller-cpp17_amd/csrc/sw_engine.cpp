@@ -342,7 +342,13 @@ int hc_sw_batch_stats(hc_sw_batch* b, hc_sw_stats* st)
     if (b->ran && b->n) {
         std::vector<SwResult> r(size_t(b->n));
         HIP_TRY(hipMemcpy(r.data(), b->res, sizeof(SwResult) * size_t(b->n), hipMemcpyDeviceToHost));
-        for (const auto& x : r) st->n_shortcut += x.shortcut ? 1 : 0;
+        std::vector<SwPair> P(static_cast<size_t>(b->n));
+        HIP_TRY(hipMemcpy(P.data(), b->pairs, sizeof(SwPair) * size_t(b->n), hipMemcpyDeviceToHost));
+        st->cells = 0;
+        for (int64_t k = 0; k < b->n; ++k) {
+            if (r[size_t(k)].shortcut) ++st->n_shortcut;
+            else st->cells += int64_t(P[size_t(k)].n1) * P[size_t(k)].n2;
+        }
     }
     const double k = b->n_runs ? 1.0 / double(b->n_runs) : 0.0;
     st->dp_ms = b->dp_ms * k;

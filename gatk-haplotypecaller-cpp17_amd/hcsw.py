@@ -109,14 +109,23 @@ def _decode(buf, n, stride):
     return [raw[k * stride:(k + 1) * stride].split(b"\0", 1)[0].decode() for k in range(n)]
 
 
+def _worst_stride(b):
+    return int(max(16, 4 * (int(b["ref_len"].max(initial=0)) + int(b["alt_len"].max(initial=0))) + 8))
+
+
 def align_flat(b, params=SW.NEW_SW_PARAMETERS, overhang=SOFTCLIP, shortcut=True, stride=None):
-    """hc_sw_align_flat over a flat batch (sw_workloads layout): (offsets, cigars)."""
+    """hc_sw_align_flat over a flat batch (sw_workloads layout): (offsets, cigars).
+    CIGARs go into `stride`-byte slots (default 512; retried at the worst case
+    when one does not fit)."""
     n = len(b["ref_len"])
-    stride = stride or int(max(16, 4 * (int(b["ref_len"].max(initial=0)) + int(b["alt_len"].max(initial=0))) + 8))
-    off = np.zeros(max(n, 1), np.int32)
-    buf = C.create_string_buffer(max(1, n * stride))
-    _check(lib().hc_sw_align_flat(*_args(b, params, overhang, shortcut), _p(off, _i32p), buf, stride))
-    return off[:n], _decode(buf, n, stride)
+    for st in ([stride] if stride else [min(512, _worst_stride(b)), _worst_stride(b)]):
+        off = np.zeros(max(n, 1), np.int32)
+        buf = C.create_string_buffer(max(1, n * st))
+        rc = lib().hc_sw_align_flat(*_args(b, params, overhang, shortcut), _p(off, _i32p), buf, st)
+        if rc != ERANGE or stride:
+            break
+    _check(rc)
+    return off[:n], _decode(buf, n, st)
 
 
 class Batch:
@@ -124,7 +133,7 @@ class Batch:
 
     def __init__(self, b, params=SW.NEW_SW_PARAMETERS, overhang=SOFTCLIP, shortcut=True):
         self.n = len(b["ref_len"])
-        self.stride = int(max(16, 4 * (int(b["ref_len"].max(initial=0)) + int(b["alt_len"].max(initial=0))) + 8))
+        self.worst = _worst_stride(b)
         h = C.c_void_p()
         _check(lib().hc_sw_batch_create(*_args(b, params, overhang, shortcut), C.byref(h)))
         self.h = h
@@ -133,12 +142,15 @@ class Batch:
         _check(lib().hc_sw_batch_run(self.h, C.c_void_p(stream) if stream else None))
 
     def results(self, scores=False):
-        off = np.zeros(max(self.n, 1), np.int32)
-        sc = np.zeros(max(self.n, 1), np.int32)
-        buf = C.create_string_buffer(max(1, self.n * self.stride))
-        _check(lib().hc_sw_batch_results(self.h, _p(off, _i32p), buf, self.stride,
-                                         _p(sc, _i32p) if scores else None))
-        out = (off[:self.n], _decode(buf, self.n, self.stride))
+        for stride in (min(512, self.worst), self.worst):
+            off = np.zeros(max(self.n, 1), np.int32)
+            sc = np.zeros(max(self.n, 1), np.int32)
+            buf = C.create_string_buffer(max(1, self.n * stride))
+            rc = lib().hc_sw_batch_results(self.h, _p(off, _i32p), buf, stride, _p(sc, _i32p) if scores else None)
+            if rc != ERANGE:
+                break
+        _check(rc)
+        out = (off[:self.n], _decode(buf, self.n, stride))
         return out + (sc[:self.n],) if scores else out
 
     def stats(self):

@@ -177,3 +177,19 @@ def edge_pairs(seed=11):
         out.append((pool[rng.integers(0, len(pool), n1)].tobytes(),
                     pool[rng.integers(0, len(pool), n2)].tobytes()))
     return out
+
+
+def shortcut_mask(batch):
+    """Pairs IntelSWAligner::align answers without the DP (intel_smithwaterman.hpp:47-58)."""
+    n = len(batch["ref_len"])
+    m = np.zeros(n, bool)
+    for k in np.nonzero(batch["ref_len"] == batch["alt_len"])[0]:
+        r, a = pair(batch, int(k))
+        m[k] = np.count_nonzero(np.frombuffer(r, np.uint8) != np.frombuffer(a, np.uint8)) <= 2
+    return m
+
+
+def dp_cells(batch) -> int:
+    """Cells of the pairs that run the DP (the all-match shortcut skips the rest)."""
+    keep = ~shortcut_mask(batch)
+    return int((batch["ref_len"][keep].astype(np.int64) * batch["alt_len"][keep].astype(np.int64)).sum())

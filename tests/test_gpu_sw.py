@@ -96,3 +96,37 @@ def test_sw_aligner_mirror(sw, sw_oracle_lib):
     o_off, o_cig = sw_oracle_lib.batch(S.from_pairs([(ref, alt)]))
     assert got == (int(o_off[0]), o_cig[0])
     assert al.align(ref, ref) == (0, f"{len(ref)}M")
+
+
+def test_sw_cpp_dropin_vs_oracle(tmp_path, sw_oracle_lib):
+    """include/hc_sw.hpp from a compiled program: the reference's per-hap loop
+    and the one-pass align_haplotypes give the oracle's offsets and CIGARs."""
+    import os
+    import struct
+    import subprocess
+    import hcphmm
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "sw_dropin"
+    libdir = os.path.dirname(hcphmm.LIB_PATH)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(root, "include"),
+                    os.path.join(root, "tests", "cpp", "sw_dropin.cpp"), "-L", libdir, "-lhcpairhmm",
+                    "-Wl,-rpath," + libdir, "-o", str(exe)], check=True)
+    b = S.config("W2", 3)
+    regions = {}
+    for k in range(len(b["ref_len"])):
+        r, a = S.pair(b, k)
+        regions.setdefault(r, []).append(a)
+    blob = struct.pack("<i", len(regions))
+    for r, alts in regions.items():
+        blob += struct.pack("<i", len(r)) + r + struct.pack("<i", len(alts))
+        for a in alts:
+            blob += struct.pack("<i", len(a)) + a
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.txt"
+    fin.write_bytes(blob)
+    subprocess.run([str(exe), str(fin), str(fout)], check=True, timeout=120)
+    lines = fout.read_text().split("\n")[:-1]
+    o_off, o_cig = sw_oracle_lib.batch(b, nthreads=8)
+    assert len(lines) == len(o_cig)
+    for k, ln in enumerate(lines):
+        a_off, a_cig, b_off, b_cig = ln.split()
+        assert int(a_off) == o_off[k] == int(b_off) and a_cig == o_cig[k] == b_cig

@@ -45,3 +45,9 @@ def test_sw_aligner_rejects_empty(built):
         hcsw.SWAligner().align(b"", b"ACGT")
     with pytest.raises(ValueError):
         hcsw.SWAligner().align(b"ACGT", b"")
+
+
+def test_sw_cpp_dropin_compiles(tmp_path):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Werror", "-I", os.path.join(root, "include"),
+                    os.path.join(root, "tests", "cpp", "sw_dropin.cpp")], check=True)
