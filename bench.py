@@ -82,7 +82,7 @@ def traffic_from_profiles(workload, cells):
 
 
 SW_OPS_PER_CELL = 22       # MAIN_CODE int32 vector ops per cell (PairWiseSW.h:4-38)
-INT32_VALU_PEAK_TOPS = 39.3   # 256 CU x 4 SIMD x 16 lanes x 2.4 GHz (no packed int32 ops)
+INT32_VALU_PEAK_TOPS = 78.6   # 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz (wave64 issues over 2 cycles; no packed int32 ops)
 
 
 def sw_secondary(no_cpu: bool):

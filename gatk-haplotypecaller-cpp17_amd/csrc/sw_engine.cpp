@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -57,6 +58,28 @@ int ensure_init(int device)
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// The DP kernel's fast variant drops the MATRIX_MIN_CUTOFF max and reads its
+// backtrack bits as signs of differences. Both are exact when every H stays
+// at or above the cutoff and every difference fits in int32. Along any
+// diagonal chain H(i,j) >= boundary + min(i,j) * min(0, match, mismatch), and
+// |H| <= |boundary| + max(n1,n2) * max|score|; E and F stay within one gap
+// score of H, or sit at LOW_INIT_VALUE (+ one extension) on the borders.
+bool fast_ok(const hc_sw_params& p, int overhang, int n1max, int n2max)
+{
+    const int64_t M = std::max(n1max, n2max);
+    const int64_t mt = p.match, mm = p.mismatch, op = p.open, ex = p.extend;
+    int64_t bmin = 0, bmax = 0;
+    if (overhang == HC_SW_INDEL || overhang == HC_SW_LEADING_INDEL) {
+        bmin = std::min({int64_t(0), op, op + (M - 1) * ex});
+        bmax = std::max({int64_t(0), op, op + (M - 1) * ex});
+    }
+    const int64_t hlow = bmin + M * std::min({int64_t(0), mt, mm});
+    const int64_t hhigh = bmax + M * std::max({int64_t(0), mt, mm});
+    if (hlow < kMinCutoff) return false;
+    const int64_t v = std::max(-hlow, hhigh) + std::abs(op) + M * std::abs(ex) + std::abs(mt) + std::abs(mm);
+    return v < (int64_t(1) << 28);
+}
+
 }  // namespace
 
 struct hc_sw_batch {
@@ -65,6 +88,7 @@ struct hc_sw_batch {
     int64_t cells = 0;
     hc_sw_params params{};
     int overhang = 9, shortcut = 1;
+    int fast = 0;
     char* dev = nullptr;
     SwPair* pairs = nullptr;
     int32_t* order = nullptr;
@@ -144,6 +168,9 @@ int create(int64_t n, const int64_t* ref_off, const int32_t* ref_len, const uint
         return int64_t(pairs[x].n1) * pairs[x].n2 > int64_t(pairs[y].n1) * pairs[y].n2;
     });
     b->n_el_cap = el_total;
+    b->fast = fast_ok(params, overhang, b->n1max, b->n2max) ? 1 : 0;
+    if (const char* e = std::getenv("HC_SW_GENERIC"))   // parity tests of the generic variant
+        if (e[0] == '1') b->fast = 0;
 
     // One device allocation: descriptors, inputs, outputs, scratch.
     size_t off = 0;
@@ -223,7 +250,9 @@ int run(hc_sw_batch* b, hipStream_t s)
     d.extend = b->params.extend;
     d.overhang = b->overhang;
     d.shortcut = b->shortcut;
+    d.n1max = b->n1max;
     d.n2max = b->n2max;
+    d.fast = b->fast;
     SwTraceArgs t{};
     t.pairs = b->pairs;
     t.res = b->res;

@@ -55,42 +55,67 @@ struct Lane {
     int e;      // E(i, j)
     int f;      // F(i, j)
     int diag;   // H(i-1, j-1) for the next cell
-    int ab;     // seq2 base of this lane's column
     uint32_t acc;
 };
 
-// One cell of MAIN_CODE (PairWiseSW.h:4-38) per lane.
-//   MASK: lanes outside columns [0, n2) keep their state (skew fill / drain).
-//   LASTW: last, partial stripe — lanes past seq1's end do not write the row buffer.
-template <bool MASK, bool LASTW>
+struct Scores {
+    int match, mismatch, open, extend;
+};
+
+// Group modes: which lanes are outside their columns [0, n2) somewhere in the group.
+enum { kBulk = 0, kFill = 1, kDrain = 2, kBoth = 3 };
+
+// One cell of MAIN_CODE (PairWiseSW.h:4-38) per lane. The backtrack nibble is
+// (MSB first) [eo > ee][fo > fe][en > hn0][fn > hn1]: "open beats extend"
+// horizontally / vertically (the reference stores their negation as
+// INSERT_EXT / DELETE_EXT) and "E wins" / "F wins" (INSERT / DELETE).
+//   FAST: the host proved every H stays above MATRIX_MIN_CUTOFF (so the
+//         cutoff max is the identity) and no difference below overflows, so
+//         each bit is the sign of a difference, shifted in by v_alignbit.
+//   MODE: lanes not yet at column 0 hold H = H(i,0) and E = LOW (fill); lanes
+//         past column n2 hold H = H(i,n2) for the end-point scan (drain).
+//         A lane's F and its values past its end feed only lanes in the same
+//         state, so nothing else needs holding.
+//   LASTW: last, partial stripe: lanes past seq1's end leave the row buffer alone.
+template <int MODE, bool LASTW, bool FAST>
 __device__ __forceinline__ void step(Lane& L, int t, int lane, int n2, int rb, bool row_ok, int uh, int uf,
-                                     int ua, int match, int mismatch, int open, int extend, int* rowH,
-                                     int* rowF)
+                                     int ab, const Scores& sc, int* rowH, int* rowF)
 {
     const int up_h = shr1(uh, L.h);   // H(i-1, j)
     const int up_f = shr1(uf, L.f);   // F(i-1, j)
-    L.ab = shr1(ua, L.ab);
-    const int eo = L.h + open, ee = L.e + extend;
+    const int eo = L.h + sc.open, ee = L.e + sc.extend;
     const int en = max(eo, ee);
-    const int fo = up_h + open, fe = up_f + extend;
+    const int fo = up_h + sc.open, fe = up_f + sc.extend;
     const int fn = max(fe, fo);
-    int hn = max(kMinCutoff, L.diag + (L.ab == rb ? match : mismatch));
-    int b = en > hn ? 1 : 0;   // INSERT
-    hn = max(hn, en);
-    b = fn > hn ? 2 : b;       // DELETE
-    hn = max(hn, fn);
-    b |= (eo > ee ? 0 : 4) | (fo > fe ? 0 : 8);   // INSERT_EXT / DELETE_EXT
-    L.acc = (L.acc << 4) | uint32_t(b);
+    int hn0 = L.diag + (ab == rb ? sc.match : sc.mismatch);
+    if (!FAST) hn0 = max(kMinCutoff, hn0);
+    const int hn1 = max(hn0, en);
+    const int hn = max(hn1, fn);
+    if (FAST) {
+        L.acc = __builtin_amdgcn_alignbit(L.acc, uint32_t(ee - eo), 31);
+        L.acc = __builtin_amdgcn_alignbit(L.acc, uint32_t(fe - fo), 31);
+        L.acc = __builtin_amdgcn_alignbit(L.acc, uint32_t(hn0 - en), 31);
+        L.acc = __builtin_amdgcn_alignbit(L.acc, uint32_t(hn1 - fn), 31);
+    } else {
+        const uint32_t b = (eo > ee ? 8u : 0u) | (fo > fe ? 4u : 0u) | (en > hn0 ? 2u : 0u) | (fn > hn1 ? 1u : 0u);
+        L.acc = (L.acc << 4) | b;
+    }
     L.diag = up_h;
-    if (MASK) {
+    L.f = fn;
+    if (MODE == kBulk) {
+        L.h = hn;
+        L.e = en;
+    } else if (MODE == kFill) {
+        const bool act = t >= lane;
+        L.h = act ? hn : L.h;
+        L.e = act ? en : L.e;
+    } else if (MODE == kDrain) {
+        L.h = (t - lane < n2) ? hn : L.h;
+        L.e = en;
+    } else {
         const bool act = unsigned(t - lane) < unsigned(n2);
         L.h = act ? hn : L.h;
         L.e = act ? en : L.e;
-        L.f = act ? fn : L.f;
-    } else {
-        L.h = hn;
-        L.e = en;
-        L.f = fn;
     }
     if (!LASTW || row_ok) {
         rowH[64 + t - lane] = L.h;
@@ -98,37 +123,49 @@ __device__ __forceinline__ void step(Lane& L, int t, int lane, int n2, int rb, b
     }
 }
 
-template <bool LASTW>
+template <int MODE, bool LASTW, bool FAST>
+__device__ __forceinline__ void group(Lane& L, int t0, int lane, int n2, int rb, bool row_ok, const Scores& sc,
+                                      int* rowH, int* rowF, const uint8_t* altB)
+{
+    // Lane 0's upper neighbours for the 8 steps (uniform addresses, 16-B reads)
+    // and every lane's haplotype base (column t - lane; altB has 64 leading pads).
+    const int4 h0 = *reinterpret_cast<const int4*>(rowH + 64 + t0);
+    const int4 h1 = *reinterpret_cast<const int4*>(rowH + 68 + t0);
+    const int4 f0 = *reinterpret_cast<const int4*>(rowF + 64 + t0);
+    const int4 f1 = *reinterpret_cast<const int4*>(rowF + 68 + t0);
+    const int uh[kGroup] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    const int uf[kGroup] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+    int ab[kGroup];
+#pragma unroll
+    for (int k = 0; k < kGroup; ++k) ab[k] = altB[64 + t0 + k - lane];
+#pragma unroll
+    for (int k = 0; k < kGroup; ++k)
+        step<MODE, LASTW, FAST>(L, t0 + k, lane, n2, rb, row_ok, uh[k], uf[k], ab[k], sc, rowH, rowF);
+}
+
+template <bool LASTW, bool FAST>
 __device__ __forceinline__ void stripe(Lane& L, int lane, int n2, int rb, bool row_ok, int T, uint32_t* btw,
-                                       int match, int mismatch, int open, int extend, int* rowH, int* rowF,
-                                       const int* altI)
+                                       const Scores& sc, int* rowH, int* rowF, const uint8_t* altB)
 {
     for (int t0 = 0; t0 < T; t0 += kGroup) {
-        int uh[kGroup], uf[kGroup], ua[kGroup];
-#pragma unroll
-        for (int k = 0; k < kGroup; ++k) {
-            uh[k] = rowH[64 + t0 + k];
-            uf[k] = rowF[64 + t0 + k];
-            ua[k] = altI[t0 + k];
-        }
-        if (t0 >= kStripe && t0 + kGroup <= n2) {
-#pragma unroll
-            for (int k = 0; k < kGroup; ++k)
-                step<false, LASTW>(L, t0 + k, lane, n2, rb, row_ok, uh[k], uf[k], ua[k], match, mismatch, open,
-                                   extend, rowH, rowF);
-        } else {
-#pragma unroll
-            for (int k = 0; k < kGroup; ++k)
-                step<true, LASTW>(L, t0 + k, lane, n2, rb, row_ok, uh[k], uf[k], ua[k], match, mismatch, open,
-                                  extend, rowH, rowF);
-        }
+        const bool fill = t0 < kStripe, drain = t0 + kGroup > n2;
+        if (!fill && !drain)
+            group<kBulk, LASTW, FAST>(L, t0, lane, n2, rb, row_ok, sc, rowH, rowF, altB);
+        else if (fill && drain)
+            group<kBoth, LASTW, FAST>(L, t0, lane, n2, rb, row_ok, sc, rowH, rowF, altB);
+        else if (fill)
+            group<kFill, LASTW, FAST>(L, t0, lane, n2, rb, row_ok, sc, rowH, rowF, altB);
+        else
+            group<kDrain, LASTW, FAST>(L, t0, lane, n2, rb, row_ok, sc, rowH, rowF, altB);
         btw[(t0 / kGroup) * kStripe + lane] = L.acc;
     }
 }
 
+template <bool FAST>
 __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
 {
-    extern __shared__ int lds[];
+    extern __shared__ int4 lds4[];
+    int* lds = reinterpret_cast<int*>(lds4);
     const int lane = threadIdx.x;
     const int p = a.order[blockIdx.x];
     const SwPair P = a.pairs[p];
@@ -150,9 +187,10 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
     const int slots = row_slots(a.n2max);
     int* rowH = lds;
     int* rowF = rowH + slots;
-    int* altI = rowF + slots;        // stripe_steps(n2max) + 8 entries
-    int* colC = altI + slots;        // H(i, n2), i = 1..n1
+    int* colC = rowF + slots;        // H(i, n2), i = 1..n1
+    uint8_t* altB = reinterpret_cast<uint8_t*>(colC + a.n1max + 1);   // 64 pads, columns, pads
     const int open = a.open, extend = a.extend, ovh = a.overhang;
+    const Scores sc{a.match, a.mismatch, open, extend};
     const int T = stripe_steps(n2);
 
     // Row 0: H(0, j) = boundary, F(0, j) = LOW (PairWiseSW.h:72-75,198).
@@ -160,7 +198,7 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
         rowH[j] = j >= 64 ? boundary(ovh, open, extend, j - 63) : 0;
         rowF[j] = kLow;
     }
-    for (int c = lane; c < T + kGroup; c += 64) altI[c] = c < n2 ? int(s2[c]) : -1;
+    for (int c = lane; c < kStripe + T + kGroup; c += 64) altB[c] = (c >= kStripe && c < kStripe + n2) ? s2[c - kStripe] : 0;
     __syncthreads();
 
     const int nstripes = (n1 + kStripe - 1) / kStripe;
@@ -174,14 +212,13 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
         L.e = kLow;                              // E(i, 0) (:199)
         L.f = kLow;
         L.diag = boundary(ovh, open, extend, s * kStripe);   // lane 0: H(64s, 0)
-        L.ab = -1;
         L.acc = 0;
-        const int rb = row_ok ? int(s1[i - 1]) : -2;
+        const int rb = row_ok ? int(s1[i - 1]) : -1;   // never equals a byte
         uint32_t* btw = bt + int64_t(s) * nw * kStripe;
         if (s == nstripes - 1 && (n1 % kStripe) != 0)
-            stripe<true>(L, lane, n2, rb, row_ok, T, btw, a.match, a.mismatch, open, extend, rowH, rowF, altI);
+            stripe<true, FAST>(L, lane, n2, rb, row_ok, T, btw, sc, rowH, rowF, altB);
         else
-            stripe<false>(L, lane, n2, rb, row_ok, T, btw, a.match, a.mismatch, open, extend, rowH, rowF, altI);
+            stripe<false, FAST>(L, lane, n2, rb, row_ok, T, btw, sc, rowH, rowF, altB);
         if (row_ok) colC[i] = L.h;   // H(i, n2): frozen since the lane left column n2
         __syncthreads();
     }
@@ -264,49 +301,53 @@ __global__ __launch_bounds__(64) void sw_trace_kernel(SwTraceArgs a)
     } else if (ovh == 11) {
         j = n2;
     }
-    int cnt = 0, op = -1, len = 0;
-    if (j < n2) push(el, cnt, op, len, kOpS, n2 - j);
+    int cnt = 0, cop = -1, len = 0;
+    if (j < n2) push(el, cnt, cop, len, kOpS, n2 - j);
     int state = 0;
     while (i > 0 && j > 0) {
         const int k = (i - 1) & (kStripe - 1), s = (i - 1) / kStripe, t = j - 1 + k;
         const uint32_t w = bt[(int64_t(s) * nw + (t >> 3)) * kStripe + k];
         const int b = (w >> ((7 - (t & 7)) * 4)) & 15;
+        // nibble [eo > ee][fo > fe][E wins][F wins] (see step): the reference's
+        // code is op | INSERT_EXT(4) | DELETE_EXT(8), the EXT bits being "not open".
+        const int op = (b & 1) ? kOpD : (b & 2) ? kOpI : kOpM;
+        const int ins_ext = (b & 8) ? 0 : 4, del_ext = (b & 4) ? 0 : 8;
         if (state == 4) {
             --j;
-            push(el, cnt, op, len, kOpI, 1);
-            state = b & 4;
+            push(el, cnt, cop, len, kOpI, 1);
+            state = ins_ext;
         } else if (state == 8) {
             --i;
-            push(el, cnt, op, len, kOpD, 1);
-            state = b & 8;
-        } else if ((b & 3) == 0) {
+            push(el, cnt, cop, len, kOpD, 1);
+            state = del_ext;
+        } else if (op == kOpM) {
             --i;
             --j;
-            push(el, cnt, op, len, kOpM, 1);
+            push(el, cnt, cop, len, kOpM, 1);
             state = 0;
-        } else if ((b & 3) == 1) {
+        } else if (op == kOpI) {
             --j;
-            push(el, cnt, op, len, kOpI, 1);
-            state = b & 4;
+            push(el, cnt, cop, len, kOpI, 1);
+            state = ins_ext;
         } else {
             --i;
-            push(el, cnt, op, len, kOpD, 1);
-            state = b & 8;
+            push(el, cnt, cop, len, kOpD, 1);
+            state = del_ext;
         }
     }
     int offset;
     if (ovh == 9) {
-        if (j > 0) push(el, cnt, op, len, kOpS, j);
+        if (j > 0) push(el, cnt, cop, len, kOpS, j);
         offset = i;
     } else if (ovh == 12) {
         if (j > 0) len += j;   // the last element repeated over the overhang (:345-352)
         offset = i - j;
     } else {
-        if (i > 0) push(el, cnt, op, len, kOpD, i);
-        else if (j > 0) push(el, cnt, op, len, kOpI, j);
+        if (i > 0) push(el, cnt, cop, len, kOpD, i);
+        else if (j > 0) push(el, cnt, cop, len, kOpI, j);
         offset = 0;
     }
-    if (op >= 0) el[cnt++] = (uint32_t(len) << 4) | uint32_t(op);
+    if (cop >= 0) el[cnt++] = (uint32_t(len) << 4) | uint32_t(cop);
     const int base = atomicAdd(a.dense_count, cnt);
     for (int e = 0; e < cnt; ++e) a.dense[base + e] = el[e];
     a.dense_base[p] = base;
@@ -318,13 +359,16 @@ __global__ __launch_bounds__(64) void sw_trace_kernel(SwTraceArgs a)
 
 size_t dp_lds_bytes(int n1max, int n2max)
 {
-    return sizeof(int) * (3 * size_t(row_slots(n2max)) + size_t(n1max) + 1);
+    return sizeof(int) * (2 * size_t(row_slots(n2max)) + size_t(n1max) + 1) + size_t(alt_slots(n2max));
 }
 
 hipError_t launch_dp(const SwDpArgs& a, int n1max, hipStream_t s)
 {
     if (a.n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(sw_dp_kernel, dim3(a.n), dim3(64), dp_lds_bytes(n1max, a.n2max), s, a);
+    if (a.fast)
+        hipLaunchKernelGGL(sw_dp_kernel<true>, dim3(a.n), dim3(64), dp_lds_bytes(n1max, a.n2max), s, a);
+    else
+        hipLaunchKernelGGL(sw_dp_kernel<false>, dim3(a.n), dim3(64), dp_lds_bytes(n1max, a.n2max), s, a);
     return hipGetLastError();
 }
 

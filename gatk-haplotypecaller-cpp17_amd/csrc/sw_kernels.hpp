@@ -24,7 +24,11 @@ __host__ __device__ inline int64_t bt_words(int n1, int n2)
 }
 // LDS row buffer entries (H or F): slot 63 + j holds column j; lanes still in
 // the skew write up to 64 slots before column 1 and up to 71 after column n2.
-__host__ __device__ inline int row_slots(int n2max) { return n2max + 2 * kStripe + kGroup; }
+// (A multiple of 4 entries, so that 16-byte reads of the buffers stay aligned.)
+__host__ __device__ inline int row_slots(int n2max) { return (n2max + 2 * kStripe + kGroup + 3) & ~3; }
+// Haplotype bases (bytes): 64 leading pads (lanes still in the skew), then the
+// columns, then pads up to the last step of a stripe.
+__host__ __device__ inline int alt_slots(int n2max) { return (kStripe + n2max + kStripe + 2 * kGroup + 3) & ~3; }
 
 struct SwPair {
     int64_t ref_off;   // seq1 bytes in refs[]
@@ -52,7 +56,8 @@ struct SwDpArgs {
     int match, mismatch, open, extend;
     int overhang;
     int shortcut;
-    int n2max;   // sizes the dynamic LDS
+    int n1max, n2max;   // size the dynamic LDS
+    int fast;    // host-proven: no cutoff, no int32 overflow (sw_engine.cpp fast_ok)
 };
 
 struct SwTraceArgs {

@@ -29,6 +29,9 @@ STANDARD_NGS = (25, -50, -110, -6)
 NEW_SW_PARAMETERS = (200, -150, -260, -11)
 ALIGNMENT_TO_BEST_HAPLOTYPE = (10, -15, -30, -5)
 PARAM_SETS = (NEW_SW_PARAMETERS, ORIGINAL_DEFAULT, STANDARD_NGS, ALIGNMENT_TO_BEST_HAPLOTYPE)
+# Not a reference parameter set: large scores that drive H down to
+# MATRIX_MIN_CUTOFF (-1e8, smithwaterman_common.h:50) so the cutoff binds.
+CUTOFF_PARAMS = (1000, -1000000, -20000000, -3000000)
 
 # Overhang strategies (native/smithwaterman_common.h:26-29)
 SOFTCLIP, INDEL, LEADING_INDEL, IGNORE = 9, 10, 11, 12

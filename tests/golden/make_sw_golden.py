@@ -45,6 +45,8 @@ def main():
             out[f"{name}__{k}"] = v
     cases = [("edge", p, st) for p in S.PARAM_SETS for st in S.STRATEGIES]
     cases += [("w2", S.NEW_SW_PARAMETERS, S.SOFTCLIP), ("w3", S.NEW_SW_PARAMETERS, S.SOFTCLIP)]
+    # scores large enough that H reaches MATRIX_MIN_CUTOFF (-1e8) on long pairs
+    cases += [("edge", S.CUTOFF_PARAMS, st) for st in (S.SOFTCLIP, S.INDEL)]
     names = []
     for set_name, p, st in cases:
         off, cig = ref.batch(sets[set_name], p, st, shortcut=True)

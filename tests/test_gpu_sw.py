@@ -18,7 +18,13 @@ def sw():
     return hcsw
 
 
-def test_sw_golden_every_case(sw, sw_golden):
+@pytest.mark.parametrize("variant", ["auto", "generic"])
+def test_sw_golden_every_case(sw, sw_golden, variant, monkeypatch):
+    # auto: the fast DP variant wherever the host proves it exact (every
+    # reference parameter set), the generic one for CUTOFF_PARAMS;
+    # generic: the cutoff + compare variant forced everywhere.
+    if variant == "generic":
+        monkeypatch.setenv("HC_SW_GENERIC", "1")
     for c in sw_golden["cases"]:
         b = sw_golden["sets"][c["set"]]
         off, cig = sw.align_flat(b, c["params"], c["strategy"], True)
