@@ -244,6 +244,7 @@ int run(hc_sw_batch* b, hipStream_t s)
     d.alts = b->alts;
     d.bt = b->bt;
     d.res = b->res;
+    d.elems = b->elems;
     d.match = b->params.match;
     d.mismatch = b->params.mismatch;
     d.open = b->params.open;

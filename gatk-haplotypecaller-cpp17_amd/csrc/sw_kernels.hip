@@ -187,8 +187,11 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
     const int slots = row_slots(a.n2max);
     int* rowH = lds;
     int* rowF = rowH + slots;
-    int* colC = rowF + slots;        // H(i, n2), i = 1..n1
-    uint8_t* altB = reinterpret_cast<uint8_t*>(colC + a.n1max + 1);   // 64 pads, columns, pads
+    uint8_t* altB = reinterpret_cast<uint8_t*>(rowF + fslots(a.n1max, a.n2max));   // 64 pads, columns, pads
+    // H(i, n2) of every row goes to this pair's CIGAR-element scratch in HBM
+    // (the trace kernel reuses it later); after the last stripe it is copied
+    // into rowF, free by then, for the end-point scan.
+    int* colG = reinterpret_cast<int*>(a.elems + P.el_off);
     const int open = a.open, extend = a.extend, ovh = a.overhang;
     const Scores sc{a.match, a.mismatch, open, extend};
     const int T = stripe_steps(n2);
@@ -219,9 +222,14 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
             stripe<true, FAST>(L, lane, n2, rb, row_ok, T, btw, sc, rowH, rowF, altB);
         else
             stripe<false, FAST>(L, lane, n2, rb, row_ok, T, btw, sc, rowH, rowF, altB);
-        if (row_ok) colC[i] = L.h;   // H(i, n2): frozen since the lane left column n2
+        if (row_ok) colG[i] = L.h;   // H(i, n2): frozen since the lane left column n2
         __syncthreads();
     }
+
+    __threadfence_block();   // this wave's colG stores complete before its lanes read them back
+    int* colC = rowF;
+    for (int x = lane + 1; x <= n1; x += 64) colC[x] = colG[x];
+    __syncthreads();
 
     // End point (PairWiseSW.h:201-226): candidates in anti-diagonal order d =
     // 1..n1+n2, the last-row cell (n1, d-n1) before the last-column cell
@@ -359,7 +367,7 @@ __global__ __launch_bounds__(64) void sw_trace_kernel(SwTraceArgs a)
 
 size_t dp_lds_bytes(int n1max, int n2max)
 {
-    return sizeof(int) * (2 * size_t(row_slots(n2max)) + size_t(n1max) + 1) + size_t(alt_slots(n2max));
+    return sizeof(int) * (size_t(row_slots(n2max)) + size_t(fslots(n1max, n2max))) + size_t(alt_slots(n2max));
 }
 
 hipError_t launch_dp(const SwDpArgs& a, int n1max, hipStream_t s)

@@ -26,6 +26,11 @@ __host__ __device__ inline int64_t bt_words(int n1, int n2)
 // the skew write up to 64 slots before column 1 and up to 71 after column n2.
 // (A multiple of 4 entries, so that 16-byte reads of the buffers stay aligned.)
 __host__ __device__ inline int row_slots(int n2max) { return (n2max + 2 * kStripe + kGroup + 3) & ~3; }
+// rowF doubles as the last-column buffer (n1 + 1 entries) after the DP.
+__host__ __device__ inline int fslots(int n1max, int n2max)
+{
+    return row_slots(n2max) > n1max + 1 ? row_slots(n2max) : ((n1max + 4) & ~3);
+}
 // Haplotype bases (bytes): 64 leading pads (lanes still in the skew), then the
 // columns, then pads up to the last step of a stripe.
 __host__ __device__ inline int alt_slots(int n2max) { return (kStripe + n2max + kStripe + 2 * kGroup + 3) & ~3; }
@@ -53,6 +58,7 @@ struct SwDpArgs {
     const uint8_t* alts;
     uint32_t* bt;
     SwResult* res;
+    uint32_t* elems;   // per-pair scratch (n1 + n2 + 3 words): last-column H during the DP
     int match, mismatch, open, extend;
     int overhang;
     int shortcut;
