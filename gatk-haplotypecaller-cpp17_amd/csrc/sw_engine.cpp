@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstdio>
+#include <cstdint>
 #include <cstring>
 #include <mutex>
 #include <numeric>
@@ -97,9 +98,7 @@ struct hc_sw_batch {
     SwResult* res = nullptr;
     uint32_t* bt = nullptr;
     uint32_t* elems = nullptr;
-    uint32_t* dense = nullptr;
-    int32_t* dense_base = nullptr;
-    int32_t* dense_count = nullptr;
+    uint16_t* slots = nullptr;
     int32_t* n_elems = nullptr;
     int32_t* offsets = nullptr;
     int64_t n_el_cap = 0;
@@ -187,9 +186,7 @@ int create(int64_t n, const int64_t* ref_off, const int32_t* ref_len, const uint
     const size_t o_res = carve(sizeof(SwResult) * size_t(n));
     const size_t o_bt = carve(sizeof(uint32_t) * size_t(bt_total));
     const size_t o_el = carve(sizeof(uint32_t) * size_t(el_total));
-    const size_t o_dense = carve(sizeof(uint32_t) * size_t(el_total));
-    const size_t o_dbase = carve(sizeof(int32_t) * size_t(n));
-    const size_t o_dcount = carve(sizeof(int32_t));
+    const size_t o_slots = carve(sizeof(uint16_t) * kSlotElems * size_t(n));
     const size_t o_nel = carve(sizeof(int32_t) * size_t(n));
     const size_t o_offs = carve(sizeof(int32_t) * size_t(n));
     if (hipMalloc(&b->dev, off) != hipSuccess) {
@@ -203,9 +200,7 @@ int create(int64_t n, const int64_t* ref_off, const int32_t* ref_len, const uint
     b->res = reinterpret_cast<SwResult*>(b->dev + o_res);
     b->bt = reinterpret_cast<uint32_t*>(b->dev + o_bt);
     b->elems = reinterpret_cast<uint32_t*>(b->dev + o_el);
-    b->dense = reinterpret_cast<uint32_t*>(b->dev + o_dense);
-    b->dense_base = reinterpret_cast<int32_t*>(b->dev + o_dbase);
-    b->dense_count = reinterpret_cast<int32_t*>(b->dev + o_dcount);
+    b->slots = reinterpret_cast<uint16_t*>(b->dev + o_slots);
     b->n_elems = reinterpret_cast<int32_t*>(b->dev + o_nel);
     b->offsets = reinterpret_cast<int32_t*>(b->dev + o_offs);
 
@@ -261,15 +256,12 @@ int run(hc_sw_batch* b, hipStream_t s)
     t.n = int(b->n);
     t.overhang = b->overhang;
     t.elems = b->elems;
-    t.dense = b->dense;
-    t.dense_base = b->dense_base;
-    t.dense_count = b->dense_count;
+    t.slots = b->slots;
     t.n_elems = b->n_elems;
     t.offsets = b->offsets;
     HIP_TRY(hipEventRecord(b->ev[0], s));
     HIP_TRY(launch_dp(d, b->n1max, s));
     HIP_TRY(hipEventRecord(b->ev[1], s));
-    HIP_TRY(hipMemsetAsync(b->dense_count, 0, sizeof(int32_t), s));
     HIP_TRY(launch_trace(t, s));
     HIP_TRY(hipEventRecord(b->ev[2], s));
     HIP_TRY(hipEventSynchronize(b->ev[2]));
@@ -291,15 +283,26 @@ int results(hc_sw_batch* b, int32_t* offsets, char* cigars, int32_t stride, int3
     const int64_t n = b->n;
     if (n == 0) return HC_SW_OK;
     if (!offsets || !cigars || stride < 2) return fail(HC_SW_EINVAL, "null output / stride < 2");
-    int32_t total = 0;
-    HIP_TRY(hipMemcpy(&total, b->dense_count, sizeof(int32_t), hipMemcpyDeviceToHost));
-    if (total < 0 || total > b->n_el_cap) return fail(HC_SW_EHIP, "corrupt CIGAR element count");
-    std::vector<int32_t> base(static_cast<size_t>(n)), cnt(static_cast<size_t>(n));
-    std::vector<uint32_t> dense(size_t(std::max(total, 1)));
+    std::vector<int32_t> cnt(static_cast<size_t>(n));
+    std::vector<uint16_t> slots(size_t(n) * kSlotElems);
     HIP_TRY(hipMemcpy(offsets, b->offsets, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(base.data(), b->dense_base, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(cnt.data(), b->n_elems, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost));
-    if (total) HIP_TRY(hipMemcpy(dense.data(), b->dense, sizeof(uint32_t) * size_t(total), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(slots.data(), b->slots, sizeof(uint16_t) * slots.size(), hipMemcpyDeviceToHost));
+    // Pairs with more than kSlotElems elements: their whole scratch (rare).
+    std::vector<uint32_t> big;
+    std::vector<size_t> big_at(static_cast<size_t>(n), SIZE_MAX);
+    std::vector<SwPair> P;
+    for (int64_t k = 0; k < n; ++k) {
+        if (cnt[size_t(k)] <= kSlotElems) continue;
+        if (P.empty()) {
+            P.resize(size_t(n));
+            HIP_TRY(hipMemcpy(P.data(), b->pairs, sizeof(SwPair) * size_t(n), hipMemcpyDeviceToHost));
+        }
+        big_at[size_t(k)] = big.size();
+        big.resize(big.size() + size_t(cnt[size_t(k)]));
+        HIP_TRY(hipMemcpy(big.data() + big_at[size_t(k)], b->elems + P[size_t(k)].el_off,
+                          sizeof(uint32_t) * size_t(cnt[size_t(k)]), hipMemcpyDeviceToHost));
+    }
     if (scores) {
         std::vector<SwResult> r(static_cast<size_t>(n));
         HIP_TRY(hipMemcpy(r.data(), b->res, sizeof(SwResult) * size_t(n), hipMemcpyDeviceToHost));
@@ -311,7 +314,8 @@ int results(hc_sw_batch* b, int32_t* offsets, char* cigars, int32_t stride, int3
         int pos = 0;
         // Elements are in traceback order: print them back to front (:388-413).
         for (int e = cnt[size_t(k)] - 1; e >= 0 && pos >= 0; --e) {
-            const uint32_t v = dense[size_t(base[size_t(k)] + e)];
+            const uint32_t v = cnt[size_t(k)] <= kSlotElems ? uint32_t(slots[size_t(k) * kSlotElems + size_t(e)])
+                                                             : big[big_at[size_t(k)] + size_t(e)];
             const int op = int(v & 15);
             const char ch = op == kOpM ? 'M' : op == kOpI ? 'I' : op == kOpD ? 'D' : op == kOpS ? 'S' : 'R';
             const int w = std::snprintf(o + pos, size_t(stride - pos), "%u%c", v >> 4, ch);

@@ -17,8 +17,9 @@
 // point among the last-row (LDS row buffer) and last-column (LDS) candidates
 // with the reference's tie-breaks, in the reference's anti-diagonal order.
 //
-// sw_trace_kernel: one lane per pair walks the backtrack words from the end
-// point (getCIGAR's state machine) and writes run-length CIGAR elements.
+// sw_trace_kernel: one wave per pair walks the backtrack from the end point
+// (getCIGAR's state machine), 64 cells per step along the current direction,
+// and writes run-length CIGAR elements.
 #include "sw_kernels.hpp"
 
 #include <climits>
@@ -270,97 +271,125 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
     if (lane == 0) a.res[p] = SwResult{best, bi, bj, 0};
 }
 
-__device__ __forceinline__ void push(uint32_t* el, int& cnt, int& op, int& len, int nop, int nlen)
+// 4-bit backtrack code of cell (i, j), 1-based (layout of sw_dp_kernel).
+__device__ __forceinline__ int bt_nibble(const uint32_t* bt, int nw, int i, int j)
 {
-    if (nop == op) {
-        len += nlen;
-    } else {
-        if (op >= 0) el[cnt++] = (uint32_t(len) << 4) | uint32_t(op);
-        op = nop;
-        len = nlen;
-    }
+    const int k = (i - 1) & (kStripe - 1), s = (i - 1) / kStripe, t = j - 1 + k;
+    const uint32_t w = bt[(int64_t(s) * nw + (t >> 3)) * kStripe + k];
+    return (w >> ((7 - (t & 7)) * 4)) & 15;
 }
 
-// getCIGAR (PairWiseSW.h:240-415), equal neighbours merged on the fly (the
-// reference merges them afterwards, :368-386: same result).
-__global__ __launch_bounds__(64) void sw_trace_kernel(SwTraceArgs a)
+// getCIGAR (PairWiseSW.h:240-415), one wave per pair. The walk is the
+// reference's state machine; the wave fetches the next 64 cells along the
+// direction the state implies (diagonal while matching, along the row in an
+// insertion, along the column in a deletion), finds with one ballot where the
+// direction changes, takes the whole run at once and applies the one cell that
+// changes it. Equal neighbours are merged on the fly (the reference merges them
+// afterwards, :368-386: same result). Elements are written CIGAR-end first,
+// to the pair's scratch and (the first kSlotElems, 16 bits each) to its slot.
+__global__ __launch_bounds__(256) void sw_trace_kernel(SwTraceArgs a)
 {
-    const int p = blockIdx.x * 64 + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (p >= a.n) return;
     const SwPair P = a.pairs[p];
     const SwResult r = a.res[p];
     uint32_t* el = a.elems + P.el_off;
-    const int n1 = P.n1, n2 = P.n2;
-    if (r.shortcut) {
-        const int base = atomicAdd(a.dense_count, 1);
-        a.dense[base] = (uint32_t(n1) << 4) | kOpM;
-        a.dense_base[p] = base;
-        a.n_elems[p] = 1;
-        a.offsets[p] = 0;
+    const int n1 = __builtin_amdgcn_readfirstlane(P.n1), n2 = __builtin_amdgcn_readfirstlane(P.n2);
+    if (__builtin_amdgcn_readfirstlane(r.shortcut)) {
+        if (lane == 0) {
+            a.slots[int64_t(p) * kSlotElems] = uint16_t((n1 << 4) | kOpM);
+            a.n_elems[p] = 1;
+            a.offsets[p] = 0;
+        }
         return;
     }
     const uint32_t* bt = a.bt + P.bt_off;
     const int nw = stripe_steps(n2) / kGroup;
     const int ovh = a.overhang;
-    int i = r.max_i, j = r.max_j;
+    int i = __builtin_amdgcn_readfirstlane(r.max_i), j = __builtin_amdgcn_readfirstlane(r.max_j);
     if (ovh == 10) {
         i = n1;
         j = n2;
     } else if (ovh == 11) {
         j = n2;
     }
-    int cnt = 0, cop = -1, len = 0;
-    if (j < n2) push(el, cnt, cop, len, kOpS, n2 - j);
+    int cnt = 0, cop = -1, len = 0;   // uniform; lane 0 stores
+    auto push = [&](int nop, int nlen) {
+        if (nop == cop) {
+            len += nlen;
+        } else {
+            if (cop >= 0 && lane == 0) el[cnt] = (uint32_t(len) << 4) | uint32_t(cop);
+            cnt += cop >= 0;
+            cop = nop;
+            len = nlen;
+        }
+    };
+    if (j < n2) push(kOpS, n2 - j);
     int state = 0;
     while (i > 0 && j > 0) {
-        const int k = (i - 1) & (kStripe - 1), s = (i - 1) / kStripe, t = j - 1 + k;
-        const uint32_t w = bt[(int64_t(s) * nw + (t >> 3)) * kStripe + k];
-        const int b = (w >> ((7 - (t & 7)) * 4)) & 15;
+        const int di = state == 4 ? 0 : lane, dj = state == 8 ? 0 : lane;
+        const int ci = i - di, cj = j - dj;
+        const bool valid = ci > 0 && cj > 0;
+        const int b = valid ? bt_nibble(bt, nw, ci, cj) : 0;
         // nibble [eo > ee][fo > fe][E wins][F wins] (see step): the reference's
         // code is op | INSERT_EXT(4) | DELETE_EXT(8), the EXT bits being "not open".
         const int op = (b & 1) ? kOpD : (b & 2) ? kOpI : kOpM;
-        const int ins_ext = (b & 8) ? 0 : 4, del_ext = (b & 4) ? 0 : 8;
-        if (state == 4) {
-            --j;
-            push(el, cnt, cop, len, kOpI, 1);
-            state = ins_ext;
-        } else if (state == 8) {
-            --i;
-            push(el, cnt, cop, len, kOpD, 1);
-            state = del_ext;
-        } else if (op == kOpM) {
-            --i;
-            --j;
-            push(el, cnt, cop, len, kOpM, 1);
-            state = 0;
-        } else if (op == kOpI) {
-            --j;
-            push(el, cnt, cop, len, kOpI, 1);
-            state = ins_ext;
+        const bool ins_ext = !(b & 8), del_ext = !(b & 4);
+        if (state == 0) {
+            const uint64_t brk = __builtin_amdgcn_ballot_w64(!(valid && op == kOpM));
+            const int k = brk ? __builtin_ctzll(brk) : 64;
+            if (k > 0) push(kOpM, k);
+            i -= k;
+            j -= k;
+            if (k < 64 && i > 0 && j > 0) {   // cell k: an insertion or deletion opens
+                const int bk = __builtin_amdgcn_readlane(b, k);
+                if (bk & 1) {
+                    --i;
+                    push(kOpD, 1);
+                    state = (bk & 4) ? 0 : 8;
+                } else {
+                    --j;
+                    push(kOpI, 1);
+                    state = (bk & 8) ? 0 : 4;
+                }
+            }
         } else {
-            --i;
-            push(el, cnt, cop, len, kOpD, 1);
-            state = del_ext;
+            // In an insertion (deletion) every cell is consumed along the row
+            // (column); the run goes on while the consumed cell's EXT bit is set.
+            const bool go = valid && (state == 4 ? ins_ext : del_ext);
+            const uint64_t brk = __builtin_amdgcn_ballot_w64(!go);
+            const int k = brk ? __builtin_ctzll(brk) : 64;
+            const bool kv = k < 64 && ((state == 4 ? j - k : i - k) > 0);
+            const int take = k + (kv ? 1 : 0);   // cell k is consumed too, and ends the run
+            push(state == 4 ? kOpI : kOpD, take);
+            if (state == 4) j -= take;
+            else i -= take;
+            if (k < 64) state = 0;
         }
     }
     int offset;
     if (ovh == 9) {
-        if (j > 0) push(el, cnt, cop, len, kOpS, j);
+        if (j > 0) push(kOpS, j);
         offset = i;
     } else if (ovh == 12) {
         if (j > 0) len += j;   // the last element repeated over the overhang (:345-352)
         offset = i - j;
     } else {
-        if (i > 0) push(el, cnt, cop, len, kOpD, i);
-        else if (j > 0) push(el, cnt, cop, len, kOpI, j);
+        if (i > 0) push(kOpD, i);
+        else if (j > 0) push(kOpI, j);
         offset = 0;
     }
-    if (cop >= 0) el[cnt++] = (uint32_t(len) << 4) | uint32_t(cop);
-    const int base = atomicAdd(a.dense_count, cnt);
-    for (int e = 0; e < cnt; ++e) a.dense[base + e] = el[e];
-    a.dense_base[p] = base;
-    a.n_elems[p] = cnt;
-    a.offsets[p] = offset;
+    if (cop >= 0) {
+        if (lane == 0) el[cnt] = (uint32_t(len) << 4) | uint32_t(cop);
+        ++cnt;
+    }
+    __threadfence_block();   // lane 0's element stores are visible to the other lanes
+    if (lane < kSlotElems && lane < cnt) a.slots[int64_t(p) * kSlotElems + lane] = uint16_t(el[lane]);
+    if (lane == 0) {
+        a.n_elems[p] = cnt;
+        a.offsets[p] = offset;
+    }
 }
 
 }  // namespace
@@ -383,7 +412,7 @@ hipError_t launch_dp(const SwDpArgs& a, int n1max, hipStream_t s)
 hipError_t launch_trace(const SwTraceArgs& a, hipStream_t s)
 {
     if (a.n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(sw_trace_kernel, dim3((a.n + 63) / 64), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(sw_trace_kernel, dim3((a.n + 3) / 4), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -73,12 +73,14 @@ struct SwTraceArgs {
     int n;
     int overhang;
     uint32_t* elems;     // per-pair scratch: (len << 4) | op, traceback order (CIGAR end first)
-    uint32_t* dense;     // the same elements packed back to back (one D2H)
-    int32_t* dense_base; // first element of pair p in dense[]
-    int32_t* dense_count;// atomic fill counter of dense[]
+    uint16_t* slots;     // the first kSlotElems elements of pair p as uint16 at p * kSlotElems
     int32_t* n_elems;
     int32_t* offsets;
 };
+
+// Fixed per-pair result slots: CIGAR elements fit 16 bits (len <= n1 + n2 < 2^11,
+// op < 16); pairs with more elements are read back from their scratch.
+constexpr int kSlotElems = 32;
 
 // CIGAR element op codes (smithwaterman_common.h:21-26).
 constexpr int kOpM = 0, kOpI = 1, kOpD = 2, kOpS = 9;
