@@ -35,6 +35,16 @@ namespace {
 std::mutex g_mu;
 hipStream_t g_stream = nullptr;
 
+// Grow-only workspace of the synchronous entry point (hc_sw_align_flat): a
+// warm call does no hipMalloc / hipHostMalloc and one H2D + one D2H.
+struct Workspace {
+    char* dev = nullptr;
+    size_t dev_bytes = 0;
+    char* host = nullptr;   // pinned
+    size_t host_bytes = 0;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+} g_ws;
+
 int fail(int code, const std::string& msg)
 {
     hcphmm::set_last_error(msg);
@@ -102,6 +112,8 @@ struct hc_sw_batch {
     int32_t* n_elems = nullptr;
     int32_t* offsets = nullptr;
     int64_t n_el_cap = 0;
+    size_t tail_off = 0, tail_bytes = 0;   // [slots | n_elems | offsets], one D2H
+    bool owns = true;                      // false: borrows g_ws
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     double dp_ms = 0, trace_ms = 0, run_ms = 0;
     int64_t n_runs = 0;
@@ -113,15 +125,41 @@ namespace {
 void free_batch(hc_sw_batch* b)
 {
     if (!b) return;
-    for (auto& e : b->ev)
-        if (e) (void)hipEventDestroy(e);
-    if (b->dev) (void)hipFree(b->dev);
+    if (b->owns) {
+        for (auto& e : b->ev)
+            if (e) (void)hipEventDestroy(e);
+        if (b->dev) (void)hipFree(b->dev);
+    }
     delete b;
+}
+
+int ws_reserve(size_t dev_bytes, size_t host_bytes)
+{
+    if (dev_bytes > g_ws.dev_bytes) {
+        if (g_ws.dev) (void)hipFree(g_ws.dev);
+        g_ws.dev = nullptr;
+        g_ws.dev_bytes = 0;
+        const size_t want = dev_bytes + dev_bytes / 4;
+        if (hipMalloc(&g_ws.dev, want) != hipSuccess) return fail(HC_SW_ENOMEM, "workspace device allocation");
+        g_ws.dev_bytes = want;
+    }
+    if (host_bytes > g_ws.host_bytes) {
+        if (g_ws.host) (void)hipHostFree(g_ws.host);
+        g_ws.host = nullptr;
+        g_ws.host_bytes = 0;
+        const size_t want = host_bytes + host_bytes / 4;
+        if (hipHostMalloc(&g_ws.host, want, hipHostMallocDefault) != hipSuccess)
+            return fail(HC_SW_ENOMEM, "workspace pinned allocation");
+        g_ws.host_bytes = want;
+    }
+    for (auto& e : g_ws.ev)
+        if (!e) HIP_TRY(hipEventCreate(&e));
+    return HC_SW_OK;
 }
 
 int create(int64_t n, const int64_t* ref_off, const int32_t* ref_len, const uint8_t* refs,
            const int64_t* alt_off, const int32_t* alt_len, const uint8_t* alts, hc_sw_params params,
-           int32_t overhang, int32_t shortcut, hc_sw_batch** out)
+           int32_t overhang, int32_t shortcut, hc_sw_batch** out, bool transient = false)
 {
     if (!out || n < 0) return fail(HC_SW_EINVAL, "null output / negative count");
     if (overhang < HC_SW_SOFTCLIP || overhang > HC_SW_IGNORE) return fail(HC_SW_EINVAL, "bad overhang strategy");
@@ -189,9 +227,33 @@ int create(int64_t n, const int64_t* ref_off, const int32_t* ref_len, const uint
     const size_t o_slots = carve(sizeof(uint16_t) * kSlotElems * size_t(n));
     const size_t o_nel = carve(sizeof(int32_t) * size_t(n));
     const size_t o_offs = carve(sizeof(int32_t) * size_t(n));
-    if (hipMalloc(&b->dev, off) != hipSuccess) {
-        free_batch(b);
-        return fail(HC_SW_ENOMEM, "device allocation of " + std::to_string(off) + " bytes");
+    b->tail_off = o_slots;
+    b->tail_bytes = off - o_slots;
+    char* stage_mem = nullptr;
+    std::vector<char> stage_vec;
+    if (transient) {
+        const int rc = ws_reserve(off, std::max(in_bytes, b->tail_bytes));
+        if (rc) {
+            free_batch(b);
+            return rc;
+        }
+        b->owns = false;
+        b->dev = g_ws.dev;
+        for (int k = 0; k < 3; ++k) b->ev[k] = g_ws.ev[k];
+        stage_mem = g_ws.host;
+    } else {
+        if (hipMalloc(&b->dev, off) != hipSuccess) {
+            free_batch(b);
+            return fail(HC_SW_ENOMEM, "device allocation of " + std::to_string(off) + " bytes");
+        }
+        for (auto& e : b->ev) {
+            if (hipEventCreate(&e) != hipSuccess) {
+                free_batch(b);
+                return fail(HC_SW_EHIP, "hipEventCreate");
+            }
+        }
+        stage_vec.resize(in_bytes);
+        stage_mem = stage_vec.data();
     }
     b->pairs = reinterpret_cast<SwPair*>(b->dev + o_pairs);
     b->order = reinterpret_cast<int32_t*>(b->dev + o_order);
@@ -205,19 +267,13 @@ int create(int64_t n, const int64_t* ref_off, const int32_t* ref_len, const uint
     b->offsets = reinterpret_cast<int32_t*>(b->dev + o_offs);
 
     // Stage the inputs in one host block, one H2D.
-    std::vector<char> stage(in_bytes);
-    std::memcpy(stage.data() + o_pairs, pairs.data(), sizeof(SwPair) * size_t(n));
-    std::memcpy(stage.data() + o_order, order.data(), sizeof(int32_t) * size_t(n));
-    if (ref_ext) std::memcpy(stage.data() + o_refs, refs, size_t(ref_ext));
-    if (alt_ext) std::memcpy(stage.data() + o_alts, alts, size_t(alt_ext));
-    for (auto& e : b->ev) {
-        if (hipEventCreate(&e) != hipSuccess) {
-            free_batch(b);
-            return fail(HC_SW_EHIP, "hipEventCreate");
-        }
-    }
-    if (hipMemcpyAsync(b->dev, stage.data(), in_bytes, hipMemcpyHostToDevice, g_stream) != hipSuccess ||
-        hipStreamSynchronize(g_stream) != hipSuccess) {
+    char* stage = stage_mem;
+    std::memcpy(stage + o_pairs, pairs.data(), sizeof(SwPair) * size_t(n));
+    std::memcpy(stage + o_order, order.data(), sizeof(int32_t) * size_t(n));
+    if (ref_ext) std::memcpy(stage + o_refs, refs, size_t(ref_ext));
+    if (alt_ext) std::memcpy(stage + o_alts, alts, size_t(alt_ext));
+    if (hipMemcpyAsync(b->dev, stage, in_bytes, hipMemcpyHostToDevice, g_stream) != hipSuccess ||
+        (!transient && hipStreamSynchronize(g_stream) != hipSuccess)) {
         free_batch(b);
         return fail(HC_SW_EHIP, "H2D of the batch inputs");
     }
@@ -283,11 +339,21 @@ int results(hc_sw_batch* b, int32_t* offsets, char* cigars, int32_t stride, int3
     const int64_t n = b->n;
     if (n == 0) return HC_SW_OK;
     if (!offsets || !cigars || stride < 2) return fail(HC_SW_EINVAL, "null output / stride < 2");
-    std::vector<int32_t> cnt(static_cast<size_t>(n));
-    std::vector<uint16_t> slots(size_t(n) * kSlotElems);
-    HIP_TRY(hipMemcpy(offsets, b->offsets, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(cnt.data(), b->n_elems, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(slots.data(), b->slots, sizeof(uint16_t) * slots.size(), hipMemcpyDeviceToHost));
+    // [slots | n_elems | offsets] are contiguous on the device: one D2H.
+    std::vector<char> tail_vec;
+    char* tail = nullptr;
+    if (!b->owns && g_ws.host_bytes >= b->tail_bytes) {
+        tail = g_ws.host;
+    } else {
+        tail_vec.resize(b->tail_bytes);
+        tail = tail_vec.data();
+    }
+    HIP_TRY(hipMemcpy(tail, b->dev + b->tail_off, b->tail_bytes, hipMemcpyDeviceToHost));
+    const uint16_t* slotv = reinterpret_cast<const uint16_t*>(tail);
+    const int32_t* cntv = reinterpret_cast<const int32_t*>(tail + (reinterpret_cast<char*>(b->n_elems) - (b->dev + b->tail_off)));
+    const int32_t* offv = reinterpret_cast<const int32_t*>(tail + (reinterpret_cast<char*>(b->offsets) - (b->dev + b->tail_off)));
+    std::memcpy(offsets, offv, sizeof(int32_t) * size_t(n));
+    std::vector<int32_t> cnt(cntv, cntv + n);
     // Pairs with more than kSlotElems elements: their whole scratch (rare).
     std::vector<uint32_t> big;
     std::vector<size_t> big_at(static_cast<size_t>(n), SIZE_MAX);
@@ -314,7 +380,7 @@ int results(hc_sw_batch* b, int32_t* offsets, char* cigars, int32_t stride, int3
         int pos = 0;
         // Elements are in traceback order: print them back to front (:388-413).
         for (int e = cnt[size_t(k)] - 1; e >= 0 && pos >= 0; --e) {
-            const uint32_t v = cnt[size_t(k)] <= kSlotElems ? uint32_t(slots[size_t(k) * kSlotElems + size_t(e)])
+            const uint32_t v = cnt[size_t(k)] <= kSlotElems ? uint32_t(slotv[size_t(k) * kSlotElems + size_t(e)])
                                                              : big[big_at[size_t(k)] + size_t(e)];
             const int op = int(v & 15);
             const char ch = op == kOpM ? 'M' : op == kOpI ? 'I' : op == kOpD ? 'D' : op == kOpS ? 'S' : 'R';
@@ -409,7 +475,7 @@ int hc_sw_align_flat(int64_t n, const int64_t* ref_off, const int32_t* ref_len, 
     int rc = ensure_init(-1);
     if (rc) return rc;
     hc_sw_batch* b = nullptr;
-    rc = create(n, ref_off, ref_len, refs, alt_off, alt_len, alts, params, overhang, shortcut, &b);
+    rc = create(n, ref_off, ref_len, refs, alt_off, alt_len, alts, params, overhang, shortcut, &b, true);
     if (rc) return rc;
     rc = run(b, g_stream);
     if (!rc) rc = results(b, offsets, cigars, stride, nullptr);

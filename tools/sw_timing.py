@@ -14,3 +14,10 @@ for name in sys.argv[1:] or ["W2"]:
     st.update(name=name, create_s=t_create, results_s=t_res,
               tcups_dp=st["cells"] / (st["dp_ms"] * 1e-3) / 1e12, gcups_run=st["cells"] / (st["run_ms"] * 1e-3) / 1e9)
     print(json.dumps(st), flush=True)
+# one region through the synchronous host API (hc_sw_align_flat)
+one = S.config("W1")
+hcsw.align_flat(one)
+t = time.time()
+for _ in range(20):
+    hcsw.align_flat(one)
+print(json.dumps({"region_415x128_call_ms": (time.time() - t) / 20 * 1e3}))
