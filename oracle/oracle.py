@@ -183,3 +183,46 @@ class SWReference(_SWLib):
 
 def sw_reference_available() -> bool:
     return os.path.exists(REF_SW_SO)
+
+
+# --------------------------------------------------------------------------
+# Genotyper numeric core: oracle/gt_oracle.c (in
+# liboracle.so) and the reference's MathUtils (oracle/_ref/libref_math.so).
+REF_MATH_SO = os.path.join(HERE, "_ref", "libref_math.so")
+
+
+class GTOracle:
+    def __init__(self, path: str = ORACLE_SO):
+        if not os.path.exists(path):
+            build(ref=False)
+        self.lib = C.CDLL(path)
+        self.lib.hco_approx_log10_sum_log10.argtypes = [C.c_double, C.c_double]
+        self.lib.hco_approx_log10_sum_log10.restype = C.c_double
+        self.lib.hco_gt_site.argtypes = [_f64p, C.c_int, _i32p, C.c_int, _i32p, C.c_int, _f64p, _i32p, _i32p]
+
+    def approx(self, a: float, b: float) -> float:
+        return self.lib.hco_approx_log10_sum_log10(a, b)
+
+    def site(self, L, keep, hap_allele, n_alleles):
+        L = np.ascontiguousarray(L, np.float64)
+        keep = np.ascontiguousarray(keep, np.int32)
+        amap = np.ascontiguousarray(hap_allele, np.int32)
+        gl = np.zeros(n_alleles * (n_alleles + 1) // 2, np.float64)
+        gi, gq = C.c_int32(), C.c_int32()
+        self.lib.hco_gt_site(_ptr(L, _f64p), L.shape[1], _ptr(keep, _i32p), len(keep), _ptr(amap, _i32p),
+                             n_alleles, _ptr(gl, _f64p), C.byref(gi), C.byref(gq))
+        return gl, gi.value, gq.value
+
+
+class MathReference:
+    """The reference's MathUtils::approximate_log10_sum_log10, compiled in place."""
+
+    def __init__(self, path: str = REF_MATH_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        self.lib = C.CDLL(path)
+        self.lib.ref_approx_log10_sum_log10.argtypes = [C.c_double, C.c_double]
+        self.lib.ref_approx_log10_sum_log10.restype = C.c_double
+
+    def approx(self, a: float, b: float) -> float:
+        return self.lib.ref_approx_log10_sum_log10(a, b)

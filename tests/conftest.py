@@ -75,3 +75,37 @@ def sw_oracle_lib():
     import oracle
     oracle.build(ref=False)
     return oracle.SWOracle()
+
+
+GT_GOLDEN = os.path.join(ROOT, "tests", "golden", "gt_golden.npz")
+
+
+@pytest.fixture(scope="session")
+def gt_golden():
+    """tests/golden/make_gt_golden.py: reference MathUtils outputs + site pins."""
+    g = np.load(GT_GOLDEN, allow_pickle=False)
+    d = {k: g[k] for k in g.files}
+    sets = {}
+    for name in ("std", "inf"):
+        mats = [d[f"{name}_mat{k}"] for k in range(int(d[f"{name}_n_mats"]))]
+        sites, ko, mo, go = [], 0, 0, 0
+        exp = []
+        for s in range(len(d[f"{name}_site_m"])):
+            m = int(d[f"{name}_site_m"][s])
+            A = int(d[f"{name}_site_A"][s])
+            nk = int(d[f"{name}_keep_n"][s])
+            nh = mats[m].shape[1]
+            G = A * (A + 1) // 2
+            sites.append(dict(m=m, n_alleles=A, keep=d[f"{name}_keep"][ko:ko + nk],
+                              hap_allele=d[f"{name}_amap"][mo:mo + nh]))
+            exp.append((d[f"{name}_gl"][go:go + G], int(d[f"{name}_gi"][s]), int(d[f"{name}_gq"][s])))
+            ko, mo, go = ko + nk, mo + nh, go + G
+        sets[name] = (mats, sites, exp)
+    return dict(approx=(d["approx_a"], d["approx_b"], d["approx_out"]), sets=sets)
+
+
+@pytest.fixture(scope="session")
+def gt_oracle_lib():
+    import oracle
+    oracle.build(ref=False)
+    return oracle.GTOracle()
