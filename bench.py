@@ -146,6 +146,54 @@ def sw_secondary(no_cpu: bool):
     return ent
 
 
+def gt_secondary(no_cpu: bool):
+    """Genotyper numeric core: 512 regions (415 reads x
+    32 haps, normalised log10 likelihoods) x 16 variant sites, one call of
+    hc_gt_genotype_sites with host buffers (the matrices' upload included); the
+    oracle (C restatement, 1 thread) on the same sites beside it, compared bit
+    for bit."""
+    import hcgt
+    import gt_workloads as GW
+    mats, sites = GW.sites(n_regions=512, sites_per_region=16, reads=(415, 415), haps=(32, 32), seed=63)
+    prep = hcgt.Prepared(mats, sites)
+    prep.run()
+    t0 = time.perf_counter()
+    reps = 5
+    for _ in range(reps):
+        prep.run()
+    dt = (time.perf_counter() - t0) / reps
+    got = prep.results()
+    ent = dict(regions=len(mats), sites=len(sites), call_ms=round(dt * 1e3, 3),
+               note="host matrices in, per-site genotype likelihoods / GT / GQ out; 54 MB of likelihoods uploaded per call")
+    if not no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        orc = oracle.GTOracle()
+        import ctypes as C
+        _f, _i = C.POINTER(C.c_double), C.POINTER(C.c_int32)
+        args = []
+        for s in sites:   # marshal first: time the C loop, not ctypes
+            L = mats[s["m"]]
+            A = s["n_alleles"]
+            gl = np.zeros(A * (A + 1) // 2)
+            gi, gq = C.c_int32(), C.c_int32()
+            args.append(((L.ctypes.data_as(_f), L.shape[1], s["keep"].ctypes.data_as(_i), len(s["keep"]),
+                          s["hap_allele"].ctypes.data_as(_i), A, gl.ctypes.data_as(_f), C.byref(gi), C.byref(gq)),
+                         gl, gi, gq))
+        fn = orc.lib.hco_gt_site
+        t0 = time.perf_counter()
+        for a, *_ in args:
+            fn(*a)
+        dc = time.perf_counter() - t0
+        exp = [(gl, gi.value, gq.value) for _, gl, gi, gq in args]
+        same = all(np.array_equal(g[0].view(np.uint64), e[0].view(np.uint64)) and g[1] == e[1] and g[2] == e[2]
+                   for g, e in zip(got, exp))
+        ent["cpu_baseline"] = dict(value=round(dc * 1e3, 1), unit="ms", cores=1, kind="port",
+                                   sample="same sites, oracle/gt_oracle.c (genotyper.hpp is not buildable here)")
+        ent["parity_vs_cpu_oracle"] = "bit-exact" if same else "MISMATCH"
+    return ent
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -330,6 +378,7 @@ def main():
         sec["regions_64x_415x32_one_call"] = dict(regions=len(regs), cells_approx=rc, call_ms=round(dt * 1e3, 2),
                                                    gcups=round(rc / dt / 1e9, 2))
         sec["smith_waterman"] = sw_secondary(args.no_cpu)
+        sec["genotyper"] = gt_secondary(args.no_cpu)
         out["secondary"] = sec
     if world > 1:
         out["gather"] = f"dist.gather ({'gloo, rehearsal' if gloo else 'RCCL'}) of raw_f32 + raw_f64 per step"

@@ -129,9 +129,12 @@ int run(const hc_gt_site* sites, int32_t n)
     // A matrix pointer shared by sites must describe the same shape.
     for (int32_t s = 0; s < n; ++s) {
         const hc_gt_site& x = sites[s];
-        for (const auto* m : mats)
-            if (m->L == x.L && (m->n_reads != x.n_reads || m->n_haps != x.n_haps))
-                return fail(HC_PHMM_EINVAL, "sites sharing a matrix disagree on its shape");
+        const hc_gt_site* m = mats[size_t(std::lower_bound(mats.begin(), mats.end(), x.L,
+                                                           [&](const hc_gt_site* a, const double* b) {
+                                                               return mat_at[a->L] < mat_at[b];
+                                                           }) - mats.begin())];
+        if (m->n_reads != x.n_reads || m->n_haps != x.n_haps)
+            return fail(HC_PHMM_EINVAL, "sites sharing a matrix disagree on its shape");
     }
     // Layout: [sites | L | keep | amap] uploaded, then [gl | gi | gq] read back, then scratch.
     const size_t o_sites = 0;

@@ -51,27 +51,40 @@ def declared_symbols(header: str = HEADER):
     return sorted(set(re.findall(r"^\s*int\s+(hc_gt_\w+)\s*\(", open(header).read(), re.M)))
 
 
+class Prepared:
+    """The C structs of a call, built once (the bench times run() alone)."""
+
+    def __init__(self, mats, sites):
+        self.mats = [np.ascontiguousarray(m, np.float64) for m in mats]
+        self.n = len(sites)
+        self.arr = (Site * max(self.n, 1))()
+        self.keep_alive, self.outs = [], []
+        for k, s in enumerate(sites):
+            m = self.mats[s["m"]]
+            keep = np.ascontiguousarray(s["keep"], np.int32)
+            amap = np.ascontiguousarray(s["hap_allele"], np.int32)
+            A = int(s["n_alleles"])
+            gl = np.zeros(A * (A + 1) // 2, np.float64)
+            gi = np.zeros(1, np.int32)
+            gq = np.zeros(1, np.int32)
+            self.keep_alive += [keep, amap]
+            self.outs.append((gl, gi, gq))
+            self.arr[k] = Site(m.ctypes.data_as(_f64p), m.shape[0], m.shape[1],
+                               keep.ctypes.data_as(_i32p) if len(keep) else None, len(keep),
+                               amap.ctypes.data_as(_i32p), A, gl.ctypes.data_as(_f64p),
+                               gi.ctypes.data_as(_i32p), gq.ctypes.data_as(_i32p))
+
+    def run(self):
+        rc = lib().hc_gt_genotype_sites(self.arr, self.n)
+        if rc != 0:
+            msg = lib().hc_phmm_last_error()
+            raise GTError(rc, msg.decode() if msg else "")
+
+    def results(self):
+        return [(gl.copy(), int(gi[0]), int(gq[0])) for gl, gi, gq in self.outs]
+
+
 def genotype_sites(mats, sites):
-    mats = [np.ascontiguousarray(m, np.float64) for m in mats]
-    n = len(sites)
-    arr = (Site * max(n, 1))()
-    keep_alive, outs = [], []
-    for k, s in enumerate(sites):
-        m = mats[s["m"]]
-        keep = np.ascontiguousarray(s["keep"], np.int32)
-        amap = np.ascontiguousarray(s["hap_allele"], np.int32)
-        A = int(s["n_alleles"])
-        gl = np.zeros(A * (A + 1) // 2, np.float64)
-        gi = np.zeros(1, np.int32)
-        gq = np.zeros(1, np.int32)
-        keep_alive += [keep, amap]
-        outs.append((gl, gi, gq))
-        arr[k] = Site(m.ctypes.data_as(_f64p), m.shape[0], m.shape[1],
-                      keep.ctypes.data_as(_i32p) if len(keep) else None, len(keep),
-                      amap.ctypes.data_as(_i32p), A, gl.ctypes.data_as(_f64p),
-                      gi.ctypes.data_as(_i32p), gq.ctypes.data_as(_i32p))
-    rc = lib().hc_gt_genotype_sites(arr, n)
-    if rc != 0:
-        msg = lib().hc_phmm_last_error()
-        raise GTError(rc, msg.decode() if msg else "")
-    return [(gl, int(gi[0]), int(gq[0])) for gl, gi, gq in outs]
+    p = Prepared(mats, sites)
+    p.run()
+    return p.results()
