@@ -284,22 +284,27 @@ void free_batch(hc_phmm_batch* b)
     delete b;
 }
 
-// LSD radix sort of `idx` by a 32-bit key, DESCENDING, stable: 11-bit digits
+// LSD radix sort of `idx` by a 32-bit key, DESCENDING, stable: the keys are
+// gathered once next to the indices ((~key << 32) | index, sorted ascending on
+// the high word), so every pass streams one contiguous array; 11-bit digits
 // (cache-resident counters), passes above the largest key's top bit skipped.
 void sort_desc(std::vector<int>& idx, const std::vector<uint32_t>& key)
 {
     if (idx.size() < 2) return;
     uint32_t kmax = 0;
     for (int p : idx) kmax = std::max(kmax, key[p]);
-    std::vector<int> tmp(idx.size());
+    const size_t n = idx.size();
+    std::vector<uint64_t> v(n), tmp(n);
+    for (size_t k = 0; k < n; ++k) v[k] = (uint64_t(kmax - key[idx[k]]) << 32) | uint32_t(idx[k]);
     constexpr int kBits = 11, kBuckets = 1 << kBits;
     for (int shift = 0; shift < 32 && (kmax >> shift) != 0; shift += kBits) {
         size_t cnt[kBuckets + 1] = {};
-        for (int p : idx) ++cnt[(kBuckets - 1 - ((key[p] >> shift) & (kBuckets - 1))) + 1];
+        for (uint64_t x : v) ++cnt[((x >> (32 + shift)) & (kBuckets - 1)) + 1];
         for (int k = 1; k <= kBuckets; ++k) cnt[k] += cnt[k - 1];
-        for (int p : idx) tmp[cnt[kBuckets - 1 - ((key[p] >> shift) & (kBuckets - 1))]++] = p;
-        idx.swap(tmp);
+        for (uint64_t x : v) tmp[cnt[(x >> (32 + shift)) & (kBuckets - 1)]++] = x;
+        v.swap(tmp);
     }
+    for (size_t k = 0; k < n; ++k) idx[k] = int(uint32_t(v[k]));
 }
 
 // Bump allocator over one device region: 256-B aligned segments.
@@ -343,13 +348,25 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
     int64_t cells = 0;
     int Hmax = 0;
     int64_t n_wide = 0;
-    for (int64_t p = 0; p < npairs; ++p) {
-        const int r = pr[p], h = ph[p];
-        pd[p] = PairDesc{int(row_off[r]), reads[r].len, int(hap_off[h]), haps[h].len};
-        cells += int64_t(reads[r].len) * haps[h].len;
-        Hmax = std::max(Hmax, haps[h].len);
-        n_wide += haps[h].len > 64 * 32;
+    {
+        std::mutex mu;
+        parallel_for(npairs, [&](int64_t lo, int64_t hi) {
+            int64_t c = 0, w = 0;
+            int hm = 0;
+            for (int64_t p = lo; p < hi; ++p) {
+                const int r = pr[p], h = ph[p];
+                pd[p] = PairDesc{int(row_off[r]), reads[r].len, int(hap_off[h]), haps[h].len};
+                c += int64_t(reads[r].len) * haps[h].len;
+                hm = std::max(hm, haps[h].len);
+                w += haps[h].len > 64 * 32;
+            }
+            std::lock_guard<std::mutex> lk(mu);
+            cells += c;
+            Hmax = std::max(Hmax, hm);
+            n_wide += w;
+        }, 1 << 16);
     }
+    tm.mark("bin: descriptors");
     std::vector<int> ord[2], lane_ord;
     lane_ord.reserve(npairs);
     const int pol = kernel_policy();
@@ -404,55 +421,81 @@ int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
         if (e && *e) {
             cap = std::max(16, std::min(kSegMaxBC, std::atoi(e)));
         } else {
-            for (int c : {64, 48, 32, 24, 16}) {
-                cap = c;
-                int64_t lanes = 0;
-                for (int p : seg_in) lanes += std::min(64, (pd[p].w + c - 1) / c);
-                if (lanes >= want) break;
+            constexpr int kCaps[5] = {64, 48, 32, 24, 16};
+            int64_t lanes[5] = {};
+            std::mutex mu;
+            parallel_for(int64_t(seg_in.size()), [&](int64_t lo, int64_t hi) {
+                int64_t part[5] = {};
+                for (int64_t k = lo; k < hi; ++k) {
+                    const int w = pd[seg_in[k]].w;
+                    for (int c = 0; c < 5; ++c) part[c] += std::min(64, (w + kCaps[c] - 1) / kCaps[c]);
+                }
+                std::lock_guard<std::mutex> lk(mu);
+                for (int c = 0; c < 5; ++c) lanes[c] += part[c];
+            }, 1 << 16);
+            for (int c = 0; c < 5; ++c) {
+                cap = kCaps[c];
+                if (lanes[c] >= want) break;
             }
         }
     }
-    for (int p : seg_in) {
-        choose(p, cap);
-        key[p] = (uint32_t(seg_bc[p]) << 16) | uint32_t(std::min(pd[p].y, 65535));
-    }
+    tm.mark("bin: classify + cap");
+    parallel_for(int64_t(seg_in.size()), [&](int64_t lo, int64_t hi) {
+        for (int64_t k = lo; k < hi; ++k) {
+            const int p = seg_in[k];
+            choose(p, cap);
+            key[p] = (uint32_t(seg_bc[p]) << 16) | uint32_t(std::min(pd[p].y, 65535));
+        }
+    }, 1 << 15);
+    tm.mark("bin: choose");
     sort_desc(seg_in, key);
+    tm.mark("bin: seg sort");
     std::vector<int> seg_ord;
     seg_ord.reserve(seg_in.size());
     {
-        std::vector<uint8_t> used(seg_in.size(), 0);
-        size_t i = 0;
+        // The packer walks the sorted list; gather what it reads per pair.
         const size_t ns = seg_in.size();
+        std::vector<uint8_t> bcs(ns), nbs(ns), used(ns, 0);
+        std::vector<int> ys(ns);
+        parallel_for(int64_t(ns), [&](int64_t lo, int64_t hi) {
+            for (int64_t k = lo; k < hi; ++k) {
+                const int p = seg_in[k];
+                bcs[k] = seg_bc[p];
+                nbs[k] = seg_nb[p];
+                ys[k] = pd[p].y;
+            }
+        }, 1 << 16);
+        size_t i = 0;
         constexpr size_t kLook = 64;
         while (i < ns) {
             if (used[i]) {
                 ++i;
                 continue;
             }
-            const int bc = seg_bc[seg_in[i]];
+            const int bc = bcs[i];
             LaneWave w{};
             w.slot0 = int(seg_ord.size());
             w.ncols = bc;
             w.rmin = INT32_MAX;
             int free = 64;
             for (size_t j = i; j < ns && j < i + kLook && free > 0; ++j) {
-                const int p = seg_in[j];
-                if (used[j] || seg_bc[p] != bc) {
+                if (used[j] || bcs[j] != bc) {
                     if (!used[j]) break;
                     continue;
                 }
-                if (seg_nb[p] > free) continue;
+                if (nbs[j] > free) continue;
                 used[j] = 1;
-                free -= seg_nb[p];
-                seg_ord.push_back(p);
+                free -= nbs[j];
+                seg_ord.push_back(seg_in[j]);
                 ++w.npairs;
-                w.rmax = std::max(w.rmax, pd[p].y);
-                w.rmin = std::min(w.rmin, pd[p].y);
-                w.nsteps = std::max(w.nsteps, pd[p].y + seg_nb[p] - 1);
+                w.rmax = std::max(w.rmax, ys[j]);
+                w.rmin = std::min(w.rmin, ys[j]);
+                w.nsteps = std::max(w.nsteps, ys[j] + nbs[j] - 1);
             }
             lw.push_back(w);
         }
     }
+    tm.mark("bin: seg pack");
     const int n_seg_waves = int(lw.size());
     const int n_seg_slots = int(seg_ord.size());
     auto cols16 = [&](int p) { return (pd[p].w + 15) / 16 * 16; };
@@ -792,8 +835,11 @@ int results(hc_phmm_batch* b, double* loglik, float* raw32, double* raw64, uint8
 
 int run_sync(hc_phmm_batch* b, double* loglik, float* raw32, double* raw64, uint8_t* resc)
 {
+    PhaseTimer tm;
     int rc = run(b, nullptr);
+    tm.mark("run (launch)");
     if (rc == HC_PHMM_OK) rc = results(b, loglik, raw32, raw64, resc);
+    tm.mark("results+finish");
     return rc;
 }
 
