@@ -94,7 +94,7 @@ def sw_secondary(no_cpu: bool):
     offsets and CIGARs."""
     import hcsw
     import sw_workloads as SWW
-    hcsw.init(int(os.environ.get("LOCAL_RANK", "0")) % max(1, __import__("torch").cuda.device_count()))
+    hcsw.init(-1)   # the device the PairHMM engine was initialised on
     b = SWW.config("W2")
     bt = hcsw.Batch(b)
     for _ in range(2):
@@ -254,12 +254,19 @@ def main():
     g32 = [torch.empty(nmax, dtype=torch.float32, device=gdev) for _ in range(world)] if (world > 1 and rank == 0) else None
     g64 = [torch.empty(nmax, dtype=torch.float64, device=gdev) for _ in range(world)] if (world > 1 and rank == 0) else None
 
+    # The device pass and the gather run on one created stream: the library
+    # enqueues on it (a created stream's handle is non-zero; 0 would select the
+    # library's own stream, unordered with torch's), and RCCL / the gloo copy
+    # to host then wait for the pass.
+    stream = torch.cuda.Stream(device=dev)
+
     def step():
-        bt.run(torch.cuda.current_stream().cuda_stream)
-        if world > 1:
-            s32, s64 = (raw32.cpu(), raw64.cpu()) if gloo else (raw32, raw64)
-            dist.gather(s32, gather_list=g32, dst=0)   # RCCL gather over xGMI
-            dist.gather(s64, gather_list=g64, dst=0)
+        with torch.cuda.stream(stream):
+            bt.run(stream.cuda_stream)
+            if world > 1:
+                s32, s64 = (raw32.cpu(), raw64.cpu()) if gloo else (raw32, raw64)
+                dist.gather(s32, gather_list=g32, dst=0)   # RCCL gather over xGMI
+                dist.gather(s64, gather_list=g64, dst=0)
 
     for _ in range(args.warmup):
         step()

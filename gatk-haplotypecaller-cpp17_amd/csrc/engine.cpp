@@ -1,18 +1,25 @@
 // Host engine + C ABI of libhcpairhmm.so (include/hc_pairhmm.h).
 //
-// Flow of one batch (the reference's computeLikelihoodsNative,
-// intel_pairhmm.hpp:115-152, split into plan and execute):
-//   plan     pack reads into 32-bit row words and haps into match tables,
-//            length-bin the pairs (W class by H, then stripes, then H), H2D
-//   execute  fp32 anti-diagonal kernel per W class -> raw f32 + rescue list
-//            fp64 kernel over the rescue list (raw < 1e-28f)      [device only]
-//   finish   D2H, then glibc log10f/log10 exactly as intel_pairhmm.hpp:137-143
+// The reference's computeLikelihoodsNative (intel_pairhmm.hpp:115-152) split
+// into plan / execute / finish over one or more device slots:
+//   plan     (host) length-bin the pairs and pack them into waves; stage the
+//            raw inputs in pinned memory, 2 bytes per read base (+3 only for
+//            reads whose gap qualities vary) and 1 per hap base
+//   execute  (device) H2D, pack rows + hap match tables, fp32 kernels ->
+//            raw f32 + rescue list, fp64 rescue over the list, D2H of results
+//   finish   (host) glibc log10f / log10 exactly as intel_pairhmm.hpp:137-143,
+//            scattered into the caller's outputs
+// A call is cut into parts: contiguous pair ranges (or region blocks) of equal
+// cells, dealt round-robin over the device slots and, for large calls, over
+// several chunks per slot, so the host planning of part k+1 overlaps the
+// device work of part k. Each part in flight holds a grow-only workspace
+// (device + pinned host), reused across calls.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <array>
-#include <chrono>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -20,19 +27,26 @@
 #include <mutex>
 #include <numeric>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "../../include/hc_pairhmm.h"
 #include "kernels.hpp"
 #include "luts.hpp"
+#include "pool.hpp"
 
 using namespace hcphmm;
+
+namespace hcphmm {
+// Shared with sw_engine.cpp / gt_engine.cpp.
+void set_last_error(const std::string& msg);
+int primary_device();   // HIP ordinal of the first device slot, -1 if not initialised
+void sw_release();      // sw_engine.cpp: drop the aligner's stream and workspace
+void gt_release();      // gt_engine.cpp: drop the genotyper's stream and buffers
+}  // namespace hcphmm
 
 namespace {
 
 thread_local std::string g_err;
-std::mutex g_mu;
 
 int fail(int code, const std::string& msg)
 {
@@ -47,77 +61,182 @@ int fail(int code, const std::string& msg)
             return fail(HC_PHMM_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-struct Engine {
-    bool ready = false;
-    int device = -1;
+// ---------------------------------------------------------------------------
+// Device slots.
+
+// Grow-only workspace of one part in flight: device memory (upload image,
+// packed rows and tables, outputs, scratch) and pinned host memory (upload
+// image, then the D2H'd results).
+struct Slot {
+    char* dev = nullptr;
+    size_t dev_cap = 0;
+    char* host = nullptr;
+    size_t host_cap = 0;
+    bool busy = false;
+};
+
+struct Device {
+    int ordinal = 0;
     int n_cu = 256;   // compute units (4 SIMDs each): sizes the lane-wave latency ceiling
     hipStream_t stream = nullptr;
-    hipStream_t side = nullptr;                  // segmented lane waves run here, concurrently
+    hipStream_t side = nullptr;                  // segmented waves beside one-lane waves
     hipEvent_t fork = nullptr, join = nullptr;   // side-stream fork / join (timing disabled)
     float* lut_f = nullptr;
     double* lut_d = nullptr;
+    std::vector<Slot*> slots;
+    double outstanding = 0;   // cells submitted and not yet collected
 };
-Engine g_eng;
 
-// ConvertChar (pairhmm_common.h:26-44).
-inline int base_code(uint8_t b)
+std::mutex g_mu;   // device list, slot pools, outstanding counters
+std::vector<Device*> g_devs;
+
+void release_device(Device* d)
 {
-    switch (b) {
-    case 'C': return 1;
-    case 'T': return 2;
-    case 'G': return 3;
-    case 'N': return 4;
-    default: return 0;
+    if (!d) return;
+    (void)hipSetDevice(d->ordinal);
+    if (d->stream) (void)hipStreamSynchronize(d->stream);
+    for (Slot* s : d->slots) {
+        if (s->dev) (void)hipFree(s->dev);
+        if (s->host) (void)hipHostFree(s->host);
+        delete s;
     }
+    if (d->lut_f) (void)hipFree(d->lut_f);
+    if (d->lut_d) (void)hipFree(d->lut_d);
+    if (d->fork) (void)hipEventDestroy(d->fork);
+    if (d->join) (void)hipEventDestroy(d->join);
+    if (d->side) (void)hipStreamDestroy(d->side);
+    if (d->stream) (void)hipStreamDestroy(d->stream);
+    delete d;
 }
 
-int ensure_init(int device)
+int init_device(Device& d)
 {
-    if (g_eng.ready) return HC_PHMM_OK;
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
-        return fail(HC_PHMM_ENODEV, "no HIP device visible");
-    int dev = device;
-    if (dev < 0) HIP_TRY(hipGetDevice(&dev));
-    if (dev >= n) return fail(HC_PHMM_ENODEV, "device ordinal out of range");
-    HIP_TRY(hipSetDevice(dev));
+    HIP_TRY(hipSetDevice(d.ordinal));
     hipDeviceProp_t prop;
-    HIP_TRY(hipGetDeviceProperties(&prop, dev));
+    HIP_TRY(hipGetDeviceProperties(&prop, d.ordinal));
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-        return fail(HC_PHMM_ENODEV, std::string("device is ") + prop.gcnArchName + ", need gfx950");
+        return fail(HC_PHMM_ENODEV, std::string("device ") + std::to_string(d.ordinal) + " is " +
+                                        prop.gcnArchName + ", need gfx950");
     HIP_TRY(configure_kernels());
-    g_eng.n_cu = std::max(1, prop.multiProcessorCount);
-    HIP_TRY(hipStreamCreateWithFlags(&g_eng.stream, hipStreamNonBlocking));
-    HIP_TRY(hipStreamCreateWithFlags(&g_eng.side, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreateWithFlags(&g_eng.fork, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&g_eng.join, hipEventDisableTiming));
+    d.n_cu = std::max(1, prop.multiProcessorCount);
+    HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&d.side, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&d.fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&d.join, hipEventDisableTiming));
     const Luts& L = luts();
-    HIP_TRY(hipMalloc(&g_eng.lut_f, sizeof(float) * kTableLen));
-    HIP_TRY(hipMalloc(&g_eng.lut_d, sizeof(double) * kTableLen));
-    HIP_TRY(hipMemcpy(g_eng.lut_f, L.dev_f.data(), sizeof(float) * kTableLen, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(g_eng.lut_d, L.dev_d.data(), sizeof(double) * kTableLen, hipMemcpyHostToDevice));
-    g_eng.device = dev;
-    g_eng.ready = true;
+    HIP_TRY(hipMalloc(&d.lut_f, sizeof(float) * kTableLen));
+    HIP_TRY(hipMalloc(&d.lut_d, sizeof(double) * kTableLen));
+    HIP_TRY(hipMemcpy(d.lut_f, L.dev_f.data(), sizeof(float) * kTableLen, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d.lut_d, L.dev_d.data(), sizeof(double) * kTableLen, hipMemcpyHostToDevice));
     return HC_PHMM_OK;
 }
 
-template <typename F>
-void parallel_for(int64_t n, F&& f, int64_t grain = 4096)
+// Resolve a device list (-1 = current device; empty = every visible device).
+int resolve_devices(const int32_t* devices, int32_t n, std::vector<int>& out)
 {
-    unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const int64_t nt = std::min<int64_t>(std::min<int64_t>(hw, 16), (n + grain - 1) / grain);
-    if (nt <= 1) {
-        f(int64_t(0), n);
-        return;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return fail(HC_PHMM_ENODEV, "no HIP device visible");
+    out.clear();
+    if (!devices || n <= 0) {
+        for (int k = 0; k < count; ++k) out.push_back(k);
+        return HC_PHMM_OK;
     }
-    std::vector<std::thread> th;
-    const int64_t chunk = (n + nt - 1) / nt;
-    for (int64_t t = 0; t < nt; ++t) {
-        const int64_t b = t * chunk, e = std::min(n, b + chunk);
-        if (b < e) th.emplace_back([&, b, e] { f(b, e); });
+    for (int32_t k = 0; k < n; ++k) {
+        int dev = devices[k];
+        if (dev < 0) HIP_TRY(hipGetDevice(&dev));
+        if (dev >= count) return fail(HC_PHMM_ENODEV, "device ordinal " + std::to_string(dev) + " out of range");
+        out.push_back(dev);
     }
-    for (auto& x : th) x.join();
+    return HC_PHMM_OK;
 }
+
+// Under g_mu.
+int init_devices_locked(const int32_t* devices, int32_t n, bool any_ok)
+{
+    if (!g_devs.empty()) {
+        if (any_ok) return HC_PHMM_OK;
+        std::vector<int> want;
+        const int rc = resolve_devices(devices, n, want);
+        if (rc) return rc;
+        bool same = want.size() == g_devs.size();
+        for (size_t k = 0; same && k < want.size(); ++k) same = want[k] == g_devs[k]->ordinal;
+        if (same) return HC_PHMM_OK;
+        std::string have;
+        for (const Device* d : g_devs) have += (have.empty() ? "" : ",") + std::to_string(d->ordinal);
+        return fail(HC_PHMM_EINVAL, "engine already initialised on device(s) " + have +
+                                        "; call hc_phmm_shutdown() before selecting others");
+    }
+    std::vector<int> want;
+    int rc = resolve_devices(devices, n, want);
+    if (rc) return rc;
+    std::vector<Device*> made;
+    for (int o : want) {
+        auto* d = new Device();
+        d->ordinal = o;
+        made.push_back(d);
+        rc = init_device(*d);
+        if (rc) {
+            for (Device* x : made) release_device(x);
+            return rc;
+        }
+    }
+    g_devs = made;
+    (void)hipSetDevice(g_devs[0]->ordinal);
+    return HC_PHMM_OK;
+}
+
+int ensure_init()
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    const int32_t cur = -1;
+    return init_devices_locked(&cur, 1, true);
+}
+
+Slot* take_slot(Device& d)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (Slot* s : d.slots)
+        if (!s->busy) {
+            s->busy = true;
+            return s;
+        }
+    auto* s = new Slot();
+    s->busy = true;
+    d.slots.push_back(s);
+    return s;
+}
+
+void give_slot(Slot* s)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    s->busy = false;
+}
+
+// Grow a slot (caller's device current). Growing drops the old contents.
+int slot_reserve(Slot& s, size_t dev_bytes, size_t host_bytes)
+{
+    if (dev_bytes > s.dev_cap) {
+        if (s.dev) HIP_TRY(hipFree(s.dev));
+        s.dev = nullptr;
+        s.dev_cap = 0;
+        const size_t cap = std::max(dev_bytes + dev_bytes / 4, size_t(16) << 20);
+        if (hipMalloc(&s.dev, cap) != hipSuccess) return fail(HC_PHMM_ENOMEM, "device workspace");
+        s.dev_cap = cap;
+    }
+    if (host_bytes > s.host_cap) {
+        if (s.host) HIP_TRY(hipHostFree(s.host));
+        s.host = nullptr;
+        s.host_cap = 0;
+        const size_t cap = std::max(host_bytes + host_bytes / 4, size_t(4) << 20);
+        if (hipHostMalloc(&s.host, cap, hipHostMallocPortable) != hipSuccess)
+            return fail(HC_PHMM_ENOMEM, "pinned staging buffer");
+        s.host_cap = cap;
+    }
+    return HC_PHMM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Inputs.
 
 struct ReadView {
     int32_t len;
@@ -128,12 +247,91 @@ struct HapView {
     const uint8_t* bases;
 };
 
+// Where a call's reads and haps live: flat pools (pair p = read p x hap p) or
+// struct arrays (hc_phmm_read / hc_phmm_hap).
+struct Src {
+    const int64_t* read_off = nullptr;
+    const int32_t* R = nullptr;
+    const int64_t* hap_off = nullptr;
+    const int32_t* H = nullptr;
+    const uint8_t *rs = nullptr, *q = nullptr, *ins = nullptr, *del = nullptr, *gcp = nullptr, *hap = nullptr;
+    const hc_phmm_read* reads = nullptr;
+    const hc_phmm_hap* haps = nullptr;
+
+    ReadView read(int64_t k) const
+    {
+        if (reads) {
+            const hc_phmm_read& r = reads[k];
+            return ReadView{r.length, (const uint8_t*)r.bases, (const uint8_t*)r.q, (const uint8_t*)r.i,
+                            (const uint8_t*)r.d, (const uint8_t*)r.c};
+        }
+        const int64_t o = read_off[k];
+        return ReadView{R[k], rs + o, q + o, ins + o, del + o, gcp + o};
+    }
+    HapView hapv(int64_t k) const
+    {
+        if (haps) return HapView{haps[k].length, (const uint8_t*)haps[k].bases};
+        return HapView{H[k], hap + hap_off[k]};
+    }
+    int32_t read_len(int64_t k) const { return reads ? reads[k].length : R[k]; }
+    int32_t hap_len(int64_t k) const { return haps ? haps[k].length : H[k]; }
+};
+
+// Cross-product block: reads [r0, r0+nr) x haps [h0, h0+nh) of the Src, results
+// to out[r * ostride + h] (read-major, as hc_phmm_cross / a region).
+struct Block {
+    int64_t r0;
+    int32_t nr;
+    int64_t h0;
+    int32_t nh;
+    double* out;
+    int64_t ostride;
+};
+
+// Caller outputs of flat (pair) calls; any may be null.
+struct Outputs {
+    double* loglik = nullptr;
+    float* raw32 = nullptr;
+    double* raw64 = nullptr;
+    uint8_t* resc = nullptr;
+};
+
+// What one part computes: flat pairs [lo, hi) (read p x hap p), or blocks.
+struct PartSpec {
+    bool flat = true;
+    int64_t lo = 0, hi = 0;
+    std::vector<Block> blocks;
+};
+
+// HC_PHMM_TRACE=1: per-phase host timings on stderr.
+struct PhaseTimer {
+    bool on;
+    std::chrono::steady_clock::time_point t0;
+    PhaseTimer() : on(std::getenv("HC_PHMM_TRACE") != nullptr), t0(std::chrono::steady_clock::now()) {}
+    void mark(const char* what)
+    {
+        if (!on) return;
+        const auto t1 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[hc_phmm] %-22s %8.3f ms\n", what,
+                     std::chrono::duration<double, std::milli>(t1 - t0).count());
+        t0 = t1;
+    }
+};
+
+int64_t env_i64(const char* name, int64_t dflt)
+{
+    const char* e = std::getenv(name);
+    return (e && *e) ? std::atoll(e) : dflt;
+}
+
 }  // namespace
 
-// --------------------------------------------------------------------------
-// Prepared batch: every device array of one batch lives in one allocation,
-// filled by one H2D copy from one pinned staging buffer.
-struct hc_phmm_batch {
+// ---------------------------------------------------------------------------
+// A part prepared on one device: every device array lives in one allocation,
+// filled by one H2D from one pinned staging image.
+struct Part {
+    Device* dev = nullptr;
+    PartSpec spec;
     int64_t n = 0;          // pairs
     int64_t cells = 0;
     int Hmax = 0;
@@ -143,11 +341,10 @@ struct hc_phmm_batch {
         int ring_len = 0;
         int* d_order = nullptr;
     } cls[2];
-    // Lane-per-pair class (large batches).
     int n_lane = 0;
     int n_seg_waves = 0;
     int lane_waves = 0;
-    int lane_variant = 0;   // lane kernel variant (kernels.hpp LaneVariant)
+    int lane_variant = 0;
     int* d_lane_order = nullptr;
     LaneWave* d_lane_waves = nullptr;
     float2* d_carry = nullptr;
@@ -157,47 +354,54 @@ struct hc_phmm_batch {
     float* d_raw32 = nullptr;     // current output targets (own or bound)
     double* d_raw64 = nullptr;
     uint8_t* d_flag = nullptr;
-    float* own_raw32 = nullptr;   // library-owned output buffers
+    float* own_raw32 = nullptr;   // outputs in the part's allocation: [raw32 | raw64 | flag]
     double* own_raw64 = nullptr;
     uint8_t* own_flag = nullptr;
+    size_t res_bytes = 0;         // bytes of that contiguous output block
+    size_t res_o64 = 0, res_ofl = 0;
     int* d_list = nullptr;
-    int* d_sorted = nullptr;      // fp64 pass: rescue list in class order (device-planned)
-    int* d_big = nullptr;         // fp64 pass: pairs too wide for the segmented kernel
+    int* d_sorted = nullptr;
+    int* d_big = nullptr;
     int* d_big_count = nullptr;
     Seg64Plan* d_plan = nullptr;
-    int64_t n_wide = 0;           // pairs with H > 64 * 32 (may need the anti-diagonal fp64 kernel)
-    int* d_count = nullptr;       // rescue counters, one per run parity
-    int parity = 0;               // run parity: which counter this run appends to
-    char* dev_base = nullptr;     // the batch's device allocation
-    bool owns_dev = true;         // false: borrowed from the engine workspace
-    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};   // current run's triple (from ev_pool)
-    // Event triples of every run since the last stats() call (reused pool), so
-    // stats() reports the average kernel time over a whole timed region.
+    int64_t n_wide = 0;
+    int* d_count = nullptr;
+    int parity = 0;
+    char* dev_base = nullptr;
+    Slot* slot = nullptr;         // borrowed workspace (jobs), else dev_base is owned
+    char* host_res = nullptr;     // pinned results image (slot) after the D2H
+    size_t upload_bytes = 0;
+    hipEvent_t pack_ev[2] = {nullptr, nullptr};
+    hipEvent_t done = nullptr;    // jobs: D2H complete
     std::vector<std::array<hipEvent_t, 3>> ev_pool;
     size_t ev_used = 0;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     hipStream_t last_stream = nullptr;
     int64_t launch_waves = 0;
     bool ran = false;
 };
 
+struct hc_phmm_batch {
+    std::vector<Part*> parts;   // one per device slot
+    int64_t n = 0;
+};
+
+struct hc_phmm_job {
+    std::vector<Part*> parts;
+    Outputs out;
+    std::vector<double> cells_per_part;
+};
+
 namespace {
 
-constexpr int kW64Threshold = 768;   // H above this -> one pair per wave (W = 64)
-constexpr int kLaneMaxH = 4096;            // longer haps stay on the anti-diagonal kernel
-constexpr int kSegWavesPerSimd = 3;        // resident seg waves per SIMD (phmm_seg_kernel occupancy)
-constexpr int kSegMinWavesPerSimd = 2;     // small batches: narrower seg blocks until this many waves
+constexpr int kW64Threshold = 768;     // anti-diagonal kernel: H above this -> one pair per wave
+constexpr int kLaneMaxH = 4096;        // longer haps stay on the anti-diagonal kernel (policy "auto")
+constexpr int kSegWavesPerSimd = 3;    // resident seg waves per SIMD (phmm_seg_kernel occupancy)
+constexpr int kSegMinWavesPerSimd = 2; // small batches: narrower seg blocks until this many waves
 
-// Lane kernel variant (kernels.hpp LaneVariant): HC_PHMM_LANE_VARIANT=<id>,
-// default 0 = {1 pair per lane, 64-column blocks, 3 waves per SIMD}.
-int lane_variant_id()
-{
-    const char* e = std::getenv("HC_PHMM_LANE_VARIANT");
-    return (e && *e) ? std::atoi(e) : 0;
-}
+int lane_variant_id() { return int(env_i64("HC_PHMM_LANE_VARIANT", 0)); }
 
-// Column-segmented lane waves (lane_kernel.hip run_seg): HC_PHMM_LANE_SEG=
-// auto = all (default: every lane pair up to 64 * kSegMaxBC columns) | off
-// (one lane per pair with the carry buffer). Returns -1 auto, 0 off, 1 all.
+// HC_PHMM_LANE_SEG = auto (default) | all | off. Returns -1 auto, 0 off, 1 all.
 int lane_seg_policy()
 {
     const char* e = std::getenv("HC_PHMM_LANE_SEG");
@@ -205,8 +409,7 @@ int lane_seg_policy()
     return std::strcmp(e, "all") ? 0 : 1;
 }
 
-// Kernel selection: HC_PHMM_KERNEL=auto (default: lane kernels for H <= kLaneMaxH,
-// anti-diagonal above) | lane (lane kernels for every pair) | diag.
+// HC_PHMM_KERNEL = auto (lane kernels for H <= kLaneMaxH) | lane | diag.
 int kernel_policy()
 {
     const char* e = std::getenv("HC_PHMM_KERNEL");
@@ -215,80 +418,22 @@ int kernel_policy()
     return 2;
 }
 
-// HC_PHMM_TRACE=1: per-phase host timings of plan/results on stderr.
-struct PhaseTimer {
-    bool on;
-    std::chrono::steady_clock::time_point t0;
-    PhaseTimer() : on(std::getenv("HC_PHMM_TRACE") != nullptr), t0(std::chrono::steady_clock::now()) {}
-    void mark(const char* what)
-    {
-        if (!on) return;
-        const auto t1 = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "[hc_phmm] %-18s %8.3f ms\n", what,
-                     std::chrono::duration<double, std::milli>(t1 - t0).count());
-        t0 = t1;
-    }
-};
-
-// Grow-only buffers reused by the synchronous entry points (no per-call
-// hipMalloc / hipHostMalloc once warm).
-struct Workspace {
-    char* dev = nullptr;
-    size_t dev_cap = 0;
-    char* host = nullptr;   // pinned
-    size_t host_cap = 0;
-    hc_phmm_batch* batch = nullptr;   // batch shell reused for its event pool
-};
-Workspace g_ws;
-
-int ws_dev(size_t bytes, char** out)
+void free_part(Part* p)
 {
-    if (bytes > g_ws.dev_cap) {
-        if (g_ws.dev) HIP_TRY(hipFree(g_ws.dev));
-        g_ws.dev = nullptr;
-        g_ws.dev_cap = 0;
-        const size_t cap = std::max(bytes + bytes / 4, size_t(64) << 20);
-        if (hipMalloc(&g_ws.dev, cap) != hipSuccess) return fail(HC_PHMM_ENOMEM, "device workspace");
-        g_ws.dev_cap = cap;
-    }
-    *out = g_ws.dev;
-    return HC_PHMM_OK;
-}
-
-int ws_host(size_t bytes, char** out)
-{
-    if (bytes > g_ws.host_cap) {
-        if (g_ws.host) HIP_TRY(hipHostFree(g_ws.host));
-        g_ws.host = nullptr;
-        g_ws.host_cap = 0;
-        const size_t cap = std::max(bytes + bytes / 4, size_t(16) << 20);
-        if (hipHostMalloc(&g_ws.host, cap, hipHostMallocDefault) != hipSuccess)
-            return fail(HC_PHMM_ENOMEM, "pinned staging buffer");
-        g_ws.host_cap = cap;
-    }
-    *out = g_ws.host;
-    return HC_PHMM_OK;
-}
-
-void release_batch_memory(hc_phmm_batch* b)
-{
-    if (b->owns_dev) (void)hipFree(b->dev_base);
-    b->dev_base = nullptr;
-}
-
-void free_batch(hc_phmm_batch* b)
-{
-    if (!b) return;
-    release_batch_memory(b);
-    for (auto& t : b->ev_pool)
+    if (!p) return;
+    if (p->dev) (void)hipSetDevice(p->dev->ordinal);
+    if (p->slot) give_slot(p->slot);
+    else if (p->dev_base) (void)hipFree(p->dev_base);
+    for (auto& t : p->ev_pool)
         for (auto& e : t) (void)hipEventDestroy(e);
-    delete b;
+    for (auto& e : p->pack_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (p->done) (void)hipEventDestroy(p->done);
+    delete p;
 }
 
-// LSD radix sort of `idx` by a 32-bit key, DESCENDING, stable: the keys are
-// gathered once next to the indices ((~key << 32) | index, sorted ascending on
-// the high word), so every pass streams one contiguous array; 11-bit digits
-// (cache-resident counters), passes above the largest key's top bit skipped.
+// LSD radix sort of `idx` by a 32-bit key, DESCENDING, stable (fallback of
+// the counting sort when the key range is wide).
 void sort_desc(std::vector<int>& idx, const std::vector<uint32_t>& key)
 {
     if (idx.size() < 2) return;
@@ -308,7 +453,60 @@ void sort_desc(std::vector<int>& idx, const std::vector<uint32_t>& key)
     for (size_t k = 0; k < n; ++k) idx[k] = int(uint32_t(v[k]));
 }
 
-// Bump allocator over one device region: 256-B aligned segments.
+// Stable parallel counting sort of `idx` by bucket(p) DESCENDING, buckets < nb.
+template <typename B>
+void counting_sort_desc(std::vector<int>& idx, int nb, B bucket)
+{
+    const int64_t n = int64_t(idx.size());
+    if (n < 2) return;
+    const int T = int(std::min<int64_t>(64, std::max<int64_t>(1, n / 8192)));
+    const int64_t chunk = (n + T - 1) / T;
+    std::vector<int64_t> hist(static_cast<size_t>(T) * nb, 0);
+    WorkerPool::get().run(T, [&](int t) {
+        int64_t* h = hist.data() + size_t(t) * nb;
+        for (int64_t k = t * chunk, e = std::min(n, k + chunk); k < e; ++k) ++h[bucket(idx[k])];
+    });
+    int64_t run = 0;
+    for (int b = nb - 1; b >= 0; --b)
+        for (int t = 0; t < T; ++t) {
+            int64_t& h = hist[size_t(t) * nb + b];
+            const int64_t c = h;
+            h = run;
+            run += c;
+        }
+    std::vector<int> out(static_cast<size_t>(n));
+    WorkerPool::get().run(T, [&](int t) {
+        int64_t* h = hist.data() + size_t(t) * nb;
+        for (int64_t k = t * chunk, e = std::min(n, k + chunk); k < e; ++k) out[h[bucket(idx[k])]++] = idx[k];
+    });
+    idx.swap(out);
+}
+
+// Parallel exclusive prefix sum of f(k), k in [0, n), into out[0..n].
+template <typename F>
+void prefix_sum(int64_t n, std::vector<int64_t>& out, F f)
+{
+    out.assign(size_t(n) + 1, 0);
+    if (n <= 0) return;
+    const int T = int(std::min<int64_t>(32, std::max<int64_t>(1, n / 16384)));
+    const int64_t chunk = (n + T - 1) / T;
+    std::vector<int64_t> part(static_cast<size_t>(T) + 1, 0);
+    WorkerPool::get().run(T, [&](int t) {
+        int64_t s = 0;
+        for (int64_t k = t * chunk, e = std::min(n, k + chunk); k < e; ++k) {
+            out[size_t(k) + 1] = s += f(k);
+        }
+        part[size_t(t) + 1] = s;
+    });
+    for (int t = 1; t <= T; ++t) part[size_t(t)] += part[size_t(t) - 1];
+    WorkerPool::get().run(T, [&](int t) {
+        const int64_t add = part[size_t(t)];
+        if (add)
+            for (int64_t k = t * chunk, e = std::min(n, k + chunk); k < e; ++k) out[size_t(k) + 1] += add;
+    });
+}
+
+// Bump allocator over one region: 256-B aligned segments.
 struct Layout {
     size_t off = 0;
     size_t take(size_t bytes)
@@ -319,404 +517,557 @@ struct Layout {
     }
 };
 
-// Pack reads/haps once each, pairs refer to them (cross product reuses both).
-// borrow_ws: place the device arrays in the engine workspace (synchronous
-// calls) instead of a batch-owned allocation.
-int plan(const std::vector<ReadView>& reads, const std::vector<HapView>& haps,
-         int64_t npairs, const int32_t* pr, const int32_t* ph, bool borrow_ws,
-         hc_phmm_batch** out)
+// The part's reads / haps in part-local order, and the (read, hap) of each
+// part-local pair.
+struct Local {
+    const Src* src;
+    const PartSpec* spec;
+    int64_t nr = 0, nh = 0, np = 0;
+    std::vector<int64_t> blk_r, blk_h, blk_p;   // per block: first local read / hap / pair
+
+    Local(const Src& s, const PartSpec& p) : src(&s), spec(&p)
+    {
+        if (p.flat) {
+            nr = nh = np = p.hi - p.lo;
+            return;
+        }
+        for (const Block& b : p.blocks) {
+            blk_r.push_back(nr);
+            blk_h.push_back(nh);
+            blk_p.push_back(np);
+            nr += b.nr;
+            nh += b.nh;
+            np += int64_t(b.nr) * b.nh;
+        }
+        blk_p.push_back(np);
+    }
+    int64_t read_id(int64_t lr) const   // Src read index of local read lr
+    {
+        if (spec->flat) return spec->lo + lr;
+        const size_t b = size_t(std::upper_bound(blk_r.begin(), blk_r.end(), lr) - blk_r.begin()) - 1;
+        return spec->blocks[b].r0 + (lr - blk_r[b]);
+    }
+    int64_t hap_id(int64_t lh) const
+    {
+        if (spec->flat) return spec->lo + lh;
+        const size_t b = size_t(std::upper_bound(blk_h.begin(), blk_h.end(), lh) - blk_h.begin()) - 1;
+        return spec->blocks[b].h0 + (lh - blk_h[b]);
+    }
+    // f(k, local read, local hap) for pairs k in [lo, hi).
+    template <typename F>
+    void pairs(int64_t lo, int64_t hi, F&& f) const
+    {
+        if (lo >= hi) return;
+        if (spec->flat) {
+            for (int64_t k = lo; k < hi; ++k) f(k, k, k);
+            return;
+        }
+        size_t b = size_t(std::upper_bound(blk_p.begin(), blk_p.end(), lo) - blk_p.begin()) - 1;
+        int64_t k = lo;
+        while (k < hi) {
+            const Block& B = spec->blocks[b];
+            const int64_t base = blk_p[b], end = std::min(hi, blk_p[b + 1]);
+            int64_t r = (k - base) / B.nh, h = (k - base) % B.nh;
+            for (; k < end; ++k) {
+                f(k, blk_r[b] + r, blk_h[b] + h);
+                if (++h == B.nh) {
+                    h = 0;
+                    ++r;
+                }
+            }
+            ++b;
+        }
+    }
+};
+
+// Plan one part on device d: host binning + staging, then the H2D, device
+// packing and (with_run) the device pass and the D2H of the results, all
+// enqueued on d's stream. slot == nullptr: the part owns its memory (batches).
+int plan_part(Device& d, const Src& src, const PartSpec& spec, Slot* slot, bool with_run, Part** out);
+int run_part(Part* b, hipStream_t s);
+
+int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool with_run, Part** out)
 {
-    for (const auto& r : reads)
-        if (r.len <= 0 || r.len > HC_PHMM_MAX_READ_LEN || !r.bases || !r.q || !r.i || !r.d || !r.c)
-            return fail(HC_PHMM_EINVAL, "read with invalid length or null array");
-    for (const auto& h : haps)
-        if (h.len <= 0 || h.len > HC_PHMM_MAX_HAP_LEN || !h.bases)
-            return fail(HC_PHMM_EINVAL, "haplotype with invalid length (1.." +
-                                            std::to_string(HC_PHMM_MAX_HAP_LEN) + ") or null bases");
+    PhaseTimer tm;
+    Local loc(src, spec);
+    const int64_t nr = loc.nr, nh = loc.nh, npairs = loc.np;
     if (npairs > (int64_t(1) << 31) - 1) return fail(HC_PHMM_EINVAL, "too many pairs for one batch");
 
-    PhaseTimer tm;
-    const int64_t nr = reads.size(), nh = haps.size();
-    std::vector<int64_t> row_off(nr + 1, 0), hap_off(nh + 1, 0);
-    for (int64_t r = 0; r < nr; ++r) row_off[r + 1] = row_off[r] + reads[r].len;
-    for (int64_t h = 0; h < nh; ++h) hap_off[h + 1] = hap_off[h] + hap_table_words(haps[h].len);
-    if (row_off[nr] > INT32_MAX || hap_off[nh] > INT32_MAX)
-        return fail(HC_PHMM_EINVAL, "batch too large (row or hap pool exceeds 2^31 words)");
+    // Reads: validate, lengths -> row offsets, gap-quality constancy.
+    std::vector<int64_t> row_off, gap_off;
+    std::vector<int32_t> gapw(static_cast<size_t>(nr));
+    std::atomic<int> bad_read{0}, bad_hap{0};
+    prefix_sum(nr, row_off, [&](int64_t r) -> int64_t {
+        const ReadView v = src.read(loc.read_id(r));
+        if (v.len <= 0 || v.len > HC_PHMM_MAX_READ_LEN || !v.bases || !v.q || !v.i || !v.d || !v.c) {
+            bad_read.store(1);
+            gapw[size_t(r)] = 0;
+            return 0;
+        }
+        // constant gap qualities: every row's (i, d, c) equals the first row's
+        const uint8_t i0 = v.i[0], d0 = v.d[0], c0 = v.c[0];
+        bool cg = true;
+        for (int k = 1; k < v.len && cg; ++k) cg = (v.i[k] == i0) & (v.d[k] == d0) & (v.c[k] == c0);
+        gapw[size_t(r)] = cg ? int32_t((i0 & 127) | ((d0 & 127) << 7) | ((c0 & 127) << 14)) : -1;
+        return v.len;
+    });
+    if (bad_read.load()) return fail(HC_PHMM_EINVAL, "read with invalid length or null array");
+    prefix_sum(nr, gap_off, [&](int64_t r) -> int64_t {
+        return gapw[size_t(r)] < 0 ? int64_t(row_off[size_t(r) + 1] - row_off[size_t(r)]) : 0;
+    });
+    std::vector<int64_t> hap_w, hap_b;   // table words / byte offsets
+    prefix_sum(nh, hap_w, [&](int64_t h) -> int64_t {
+        const HapView v = src.hapv(loc.hap_id(h));
+        if (v.len <= 0 || v.len > HC_PHMM_MAX_HAP_LEN || !v.bases) {
+            bad_hap.store(1);
+            return 0;
+        }
+        return hap_table_words(v.len);
+    });
+    if (bad_hap.load())
+        return fail(HC_PHMM_EINVAL, "haplotype with invalid length (1.." + std::to_string(HC_PHMM_MAX_HAP_LEN) +
+                                        ") or null bases");
+    prefix_sum(nh, hap_b, [&](int64_t h) -> int64_t { return src.hap_len(loc.hap_id(h)); });
+    const int64_t nrows = row_off[size_t(nr)], ngap = gap_off[size_t(nr)];
+    if (nrows > INT32_MAX || hap_w[size_t(nh)] > INT32_MAX || hap_b[size_t(nh)] > INT32_MAX || ngap > INT32_MAX)
+        return fail(HC_PHMM_EINVAL, "batch too large (row or hap pool exceeds 2^31)");
+    tm.mark("reads/haps scan");
 
-    tm.mark("offsets");
-    // Descriptors and length binning.
-    std::vector<PairDesc> pd(npairs);
-    int64_t cells = 0;
-    int Hmax = 0;
-    int64_t n_wide = 0;
-    {
-        std::mutex mu;
-        parallel_for(npairs, [&](int64_t lo, int64_t hi) {
-            int64_t c = 0, w = 0;
-            int hm = 0;
-            for (int64_t p = lo; p < hi; ++p) {
-                const int r = pr[p], h = ph[p];
-                pd[p] = PairDesc{int(row_off[r]), reads[r].len, int(hap_off[h]), haps[h].len};
-                c += int64_t(reads[r].len) * haps[h].len;
-                hm = std::max(hm, haps[h].len);
-                w += haps[h].len > 64 * 32;
-            }
-            std::lock_guard<std::mutex> lk(mu);
-            cells += c;
-            Hmax = std::max(Hmax, hm);
-            n_wide += w;
-        }, 1 << 16);
+    // Staging layout (upload part first; waves last, their count is known later).
+    Layout U;
+    const size_t o_pairs = U.take(sizeof(PairDesc) * size_t(npairs));
+    const size_t o_rd = U.take(sizeof(int4) * size_t(nr));
+    const size_t o_hd = U.take(sizeof(int4) * size_t(nh));
+    const size_t o_ord = U.take(sizeof(int) * size_t(npairs));
+    const size_t o_bases = U.take(size_t(nrows) + 16);
+    const size_t o_quals = U.take(size_t(nrows) + 16);
+    const size_t gap_stride = (size_t(ngap) + 16 + 15) & ~size_t(15);
+    const size_t o_gaps = U.take(ngap ? 3 * gap_stride : 0);
+    const size_t o_hb = U.take(size_t(hap_b[size_t(nh)]) + 16);
+    const size_t o_lw = U.off;   // LaneWave array, sized after packing
+
+    // Pinned staging: upper bound for the waves (one per seg pair at most, plus
+    // one-lane waves) and the results image after the upload.
+    const size_t waves_max = sizeof(LaneWave) * (size_t(npairs) + 1);
+    const size_t n1 = size_t(std::max<int64_t>(npairs, 1));
+    const size_t res_o64 = (sizeof(float) * n1 + 255) & ~size_t(255);
+    const size_t res_ofl = res_o64 + ((sizeof(double) * n1 + 255) & ~size_t(255));
+    const size_t res_bytes = res_ofl + n1;
+    const size_t host_upload_cap = o_lw + waves_max;
+    const size_t host_res_off = (host_upload_cap + 255) & ~size_t(255);
+    char* host = nullptr;
+    std::vector<char> dummy;
+    bool own_host = false;
+    if (slot) {
+        const int rc = slot_reserve(*slot, 0, host_res_off + res_bytes);
+        if (rc) return rc;
+        host = slot->host;
+    } else {
+        if (hipHostMalloc(&host, std::max<size_t>(host_upload_cap, 1), hipHostMallocPortable) != hipSuccess)
+            return fail(HC_PHMM_ENOMEM, "pinned staging buffer");
+        own_host = true;
     }
-    tm.mark("bin: descriptors");
-    std::vector<int> ord[2], lane_ord;
-    lane_ord.reserve(npairs);
+    struct HostGuard {
+        char* p;
+        bool own;
+        ~HostGuard()
+        {
+            if (own && p) (void)hipHostFree(p);
+        }
+    } hguard{host, own_host};
+    tm.mark("staging alloc");
+
+    // Pair descriptors straight into the staging image; classification.
+    PairDesc* pd = reinterpret_cast<PairDesc*>(host + o_pairs);
     const int pol = kernel_policy();
     const bool use_lane = pol != 2;
-    for (int64_t p = 0; p < npairs; ++p) {
-        if (use_lane && (pol == 1 || pd[p].w <= kLaneMaxH))
-            lane_ord.push_back(int(p));
-        else
-            ord[pd[p].w > kW64Threshold ? 1 : 0].push_back(int(p));
-    }
-    std::vector<uint32_t> key(npairs);
-    // Lane class. Column-segmented waves (lane_kernel.hip run_seg) take every
-    // lane pair with H <= 64 * kSegMaxBC (policy "off": none): a pair gets nb
-    // lanes of BC columns, BC from the compiled widths, choosing between
-    // nb0 = ceil(H/cap) and nb0 + 1 lanes by modelled cost nb*BC*(R + nb - 1).
-    // The width cap is 64 unless the batch is too small to give every SIMD
-    // kSegMinWavesPerSimd waves at that width (a lone wave issues at half
-    // rate): then the widest cap that does, down to 16, so small batches are
-    // spread over more, shorter waves. Pairs are binned by (BC, R) descending
-    // and packed greedily into waves of up to 64 lanes (a short look-ahead
-    // fills a wave's last lanes). Longer haps (or policy "off") take one lane
-    // per pair with the carry buffer, binned by (H rounded up to 16, R).
-    std::vector<LaneWave> lw;
-    int64_t carry_rows = 0;
-    const int lane_var = lane_variant_id();
-    const LaneVariant& LV = lane_variant(lane_var);
-    const int lane_p = LV.P;
     const int seg_max_h = lane_seg_policy() == 0 ? 0 : 64 * kSegMaxBC;
-    std::vector<int> seg_in, one_ord;
-    std::vector<uint8_t> seg_bc(npairs, 0), seg_nb(npairs, 0);
-    for (int p : lane_ord) (pd[p].w > seg_max_h ? one_ord : seg_in).push_back(p);
-    auto choose = [&](int p, int cap) {
-        const int H = pd[p].w, R = pd[p].y;
-        const int nb0 = std::min(64, (H + cap - 1) / cap);
-        int64_t best = INT64_MAX;
-        for (int nb = nb0; nb <= std::min(nb0 + 1, 64); ++nb) {
-            int bc = std::max(16, ((H + nb - 1) / nb + 3) / 4 * 4);
-            while (!seg_width_ok(bc)) bc += 4;
-            const int n = (H + bc - 1) / bc;
-            const int64_t cost = int64_t(n) * bc * (R + n - 1);
-            if (cost < best) {
-                best = cost;
-                seg_bc[p] = uint8_t(bc);
-                seg_nb[p] = uint8_t(n);
-            }
+    // class: 0 seg, 1 one-lane, 2 diag W16, 3 diag W64
+    std::vector<uint8_t> cls(static_cast<size_t>(npairs));
+    std::atomic<int64_t> cells_a{0}, wide_a{0};
+    std::atomic<int> hmax_a{0};
+    constexpr int kCaps[5] = {64, 48, 32, 24, 16};
+    std::array<std::atomic<int64_t>, 5> lanes_at{};
+    std::array<std::atomic<int64_t>, 4> cls_n{};
+    for (auto& x : lanes_at) x = 0;
+    for (auto& x : cls_n) x = 0;
+    parallel_for(npairs, [&](int64_t lo, int64_t hi) {
+        int64_t c = 0, w = 0, lanes[5] = {}, cn[4] = {};
+        int hm = 0;
+        loc.pairs(lo, hi, [&](int64_t k, int64_t r, int64_t h) {
+            const int R = int(row_off[size_t(r) + 1] - row_off[size_t(r)]);
+            const int H = int(hap_b[size_t(h) + 1] - hap_b[size_t(h)]);
+            pd[k] = PairDesc{int(row_off[size_t(r)]), R, int(hap_w[size_t(h)]), H};
+            c += int64_t(R) * H;
+            hm = std::max(hm, H);
+            w += H > 64 * 32;
+            int cl;
+            if (use_lane && (pol == 1 || H <= kLaneMaxH))
+                cl = H > seg_max_h ? 1 : 0;
+            else
+                cl = H > kW64Threshold ? 3 : 2;
+            cls[size_t(k)] = uint8_t(cl);
+            ++cn[cl];
+            if (cl == 0)
+                for (int q = 0; q < 5; ++q) lanes[q] += std::min(64, (H + kCaps[q] - 1) / kCaps[q]);
+        });
+        cells_a += c;
+        wide_a += w;
+        int cur = hmax_a.load();
+        while (hm > cur && !hmax_a.compare_exchange_weak(cur, hm)) {
         }
-    };
+        for (int q = 0; q < 5; ++q) lanes_at[q] += lanes[q];
+        for (int q = 0; q < 4; ++q) cls_n[q] += cn[q];
+    }, 1 << 14);
+    tm.mark("descriptors");
+
+    // Column-segmented waves (lane_kernel.hip run_seg): a pair gets nb lanes of
+    // BC columns, BC from the compiled widths, choosing between nb0 =
+    // ceil(H/cap) and nb0 + 1 lanes by modelled cost nb*BC*(R + nb - 1). The
+    // width cap is 64 unless the batch is too small to give every SIMD
+    // kSegMinWavesPerSimd waves at that width (a lone wave issues at half
+    // rate): then the widest cap that does, down to 16. Pairs are binned by
+    // (BC, R) descending and packed greedily into waves of up to 64 lanes (a
+    // short look-ahead fills a wave's last lanes).
     int cap = kSegMaxBC;
     {
-        const int64_t want = int64_t(kSegMinWavesPerSimd) * 4 * g_eng.n_cu * 64;   // lanes
-        const char* e = std::getenv("HC_PHMM_SEG_CAP");
-        if (e && *e) {
-            cap = std::max(16, std::min(kSegMaxBC, std::atoi(e)));
+        const int64_t want = int64_t(kSegMinWavesPerSimd) * 4 * dv.n_cu * 64;   // lanes
+        const int64_t forced = env_i64("HC_PHMM_SEG_CAP", 0);
+        if (forced > 0) {
+            cap = int(std::max<int64_t>(16, std::min<int64_t>(kSegMaxBC, forced)));
         } else {
-            constexpr int kCaps[5] = {64, 48, 32, 24, 16};
-            int64_t lanes[5] = {};
-            std::mutex mu;
-            parallel_for(int64_t(seg_in.size()), [&](int64_t lo, int64_t hi) {
-                int64_t part[5] = {};
-                for (int64_t k = lo; k < hi; ++k) {
-                    const int w = pd[seg_in[k]].w;
-                    for (int c = 0; c < 5; ++c) part[c] += std::min(64, (w + kCaps[c] - 1) / kCaps[c]);
-                }
-                std::lock_guard<std::mutex> lk(mu);
-                for (int c = 0; c < 5; ++c) lanes[c] += part[c];
-            }, 1 << 16);
             for (int c = 0; c < 5; ++c) {
                 cap = kCaps[c];
-                if (lanes[c] >= want) break;
+                if (lanes_at[c].load() >= want) break;
             }
         }
     }
-    tm.mark("bin: classify + cap");
+    std::vector<int> seg_in(static_cast<size_t>(cls_n[0].load())), one_ord, ord2[2];
+    one_ord.reserve(size_t(cls_n[1].load()));
+    ord2[0].reserve(size_t(cls_n[2].load()));
+    ord2[1].reserve(size_t(cls_n[3].load()));
+    {
+        size_t ns = 0;
+        for (int64_t k = 0; k < npairs; ++k) {
+            switch (cls[size_t(k)]) {
+            case 0: seg_in[ns++] = int(k); break;
+            case 1: one_ord.push_back(int(k)); break;
+            case 2: ord2[0].push_back(int(k)); break;
+            default: ord2[1].push_back(int(k)); break;
+            }
+        }
+    }
+    std::vector<uint8_t> seg_bc(static_cast<size_t>(npairs), 0), seg_nb(static_cast<size_t>(npairs), 0);
+    std::atomic<int> rmin_a{INT32_MAX}, rmax_a{0};
     parallel_for(int64_t(seg_in.size()), [&](int64_t lo, int64_t hi) {
-        for (int64_t k = lo; k < hi; ++k) {
-            const int p = seg_in[k];
-            choose(p, cap);
-            key[p] = (uint32_t(seg_bc[p]) << 16) | uint32_t(std::min(pd[p].y, 65535));
-        }
-    }, 1 << 15);
-    tm.mark("bin: choose");
-    sort_desc(seg_in, key);
-    tm.mark("bin: seg sort");
-    std::vector<int> seg_ord;
-    seg_ord.reserve(seg_in.size());
-    {
-        // The packer walks the sorted list; gather what it reads per pair.
-        const size_t ns = seg_in.size();
-        std::vector<uint8_t> bcs(ns), nbs(ns), used(ns, 0);
-        std::vector<int> ys(ns);
-        parallel_for(int64_t(ns), [&](int64_t lo, int64_t hi) {
-            for (int64_t k = lo; k < hi; ++k) {
-                const int p = seg_in[k];
-                bcs[k] = seg_bc[p];
-                nbs[k] = seg_nb[p];
-                ys[k] = pd[p].y;
-            }
-        }, 1 << 16);
-        size_t i = 0;
-        constexpr size_t kLook = 64;
-        while (i < ns) {
-            if (used[i]) {
-                ++i;
-                continue;
-            }
-            const int bc = bcs[i];
-            LaneWave w{};
-            w.slot0 = int(seg_ord.size());
-            w.ncols = bc;
-            w.rmin = INT32_MAX;
-            int free = 64;
-            for (size_t j = i; j < ns && j < i + kLook && free > 0; ++j) {
-                if (used[j] || bcs[j] != bc) {
-                    if (!used[j]) break;
-                    continue;
+        int rlo = INT32_MAX, rhi = 0;
+        for (int64_t q = lo; q < hi; ++q) {
+            const int p = seg_in[size_t(q)];
+            const int H = pd[p].w, R = pd[p].y;
+            const int nb0 = std::min(64, (H + cap - 1) / cap);
+            int64_t best = INT64_MAX;
+            for (int nb = nb0; nb <= std::min(nb0 + 1, 64); ++nb) {
+                int bc = std::max(kSegMinBC, ((H + nb - 1) / nb + 3) / 4 * 4);
+                while (!seg_width_ok(bc)) bc += 4;
+                const int nbb = (H + bc - 1) / bc;
+                const int64_t cost = int64_t(nbb) * bc * (R + nbb - 1);
+                if (cost < best) {
+                    best = cost;
+                    seg_bc[size_t(p)] = uint8_t(bc);
+                    seg_nb[size_t(p)] = uint8_t(nbb);
                 }
-                if (nbs[j] > free) continue;
-                used[j] = 1;
-                free -= nbs[j];
-                seg_ord.push_back(seg_in[j]);
-                ++w.npairs;
-                w.rmax = std::max(w.rmax, ys[j]);
-                w.rmin = std::min(w.rmin, ys[j]);
-                w.nsteps = std::max(w.nsteps, ys[j] + nbs[j] - 1);
             }
-            lw.push_back(w);
+            rlo = std::min(rlo, R);
+            rhi = std::max(rhi, R);
+        }
+        int cur = rmin_a.load();
+        while (rlo < cur && !rmin_a.compare_exchange_weak(cur, rlo)) {
+        }
+        cur = rmax_a.load();
+        while (rhi > cur && !rmax_a.compare_exchange_weak(cur, rhi)) {
+        }
+    }, 1 << 14);
+    tm.mark("seg choose");
+    if (!seg_in.empty()) {
+        const int rlo = rmin_a.load(), rspan = rmax_a.load() - rlo + 1;
+        const int nbk = (kSegMaxBC / 4 + 1) * rspan;
+        if (nbk <= (1 << 18)) {
+            counting_sort_desc(seg_in, nbk, [&](int p) { return (seg_bc[size_t(p)] / 4) * rspan + (pd[p].y - rlo); });
+        } else {
+            std::vector<uint32_t> key(static_cast<size_t>(npairs));
+            for (int p : seg_in) key[size_t(p)] = (uint32_t(seg_bc[size_t(p)]) << 16) | uint32_t(std::min(pd[p].y, 65535));
+            sort_desc(seg_in, key);
         }
     }
-    // Dispatch order. Packing walks pairs by (BC, R), so a short BC=64 wave
-    // precedes a long BC=60 one. The bulk keeps that order (co-resident waves
-    // share one width's code: measured 2 % faster on S2 than a global sort);
-    // the shortest waves filling the last tail_rounds rounds of wave slots go
-    // last, longest first (LPT, duration ~ BC * nsteps), so the chip drains
-    // evenly. Waves address their pairs through slot0: no pair moves.
+    tm.mark("seg sort");
+    // Greedy packing in independent segments of the sorted list (one per task;
+    // a segment boundary costs at most one partly filled wave).
+    const int64_t ns = int64_t(seg_in.size());
+    std::vector<int> seg_ord(static_cast<size_t>(ns));
+    std::vector<LaneWave> lw;
     {
-        int tail_rounds = 2;
-        if (const char* e = std::getenv("HC_PHMM_TAIL_ROUNDS")) tail_rounds = std::max(0, std::atoi(e));   // A/B
+        const int T = int(std::min<int64_t>(64, std::max<int64_t>(1, ns / 16384)));
+        const int64_t chunk = (ns + T - 1) / T;
+        std::vector<std::vector<LaneWave>> part_w(static_cast<size_t>(T));
+        WorkerPool::get().run(T, [&](int t) {
+            const int64_t b = t * chunk, e = std::min(ns, b + chunk);
+            if (b >= e) return;
+            const int64_t m = e - b;
+            std::vector<uint8_t> used(static_cast<size_t>(m), 0);
+            auto& W = part_w[size_t(t)];
+            int64_t slot_n = b;
+            constexpr int64_t kLook = 64;
+            for (int64_t i = 0; i < m; ++i) {
+                if (used[size_t(i)]) continue;
+                const int bc = seg_bc[size_t(seg_in[size_t(b + i)])];
+                LaneWave w{};
+                w.slot0 = int(slot_n);
+                w.ncols = bc;
+                w.rmin = INT32_MAX;
+                int free = 64;
+                for (int64_t j = i; j < m && j < i + kLook && free > 0; ++j) {
+                    if (used[size_t(j)]) continue;
+                    const int p = seg_in[size_t(b + j)];
+                    if (seg_bc[size_t(p)] != bc) break;
+                    if (seg_nb[size_t(p)] > free) continue;
+                    used[size_t(j)] = 1;
+                    free -= seg_nb[size_t(p)];
+                    seg_ord[size_t(slot_n++)] = p;
+                    ++w.npairs;
+                    w.rmax = std::max(w.rmax, pd[p].y);
+                    w.rmin = std::min(w.rmin, pd[p].y);
+                    w.nsteps = std::max(w.nsteps, pd[p].y + seg_nb[size_t(p)] - 1);
+                }
+                W.push_back(w);
+            }
+        });
+        size_t nw = 0;
+        for (auto& W : part_w) nw += W.size();
+        lw.reserve(nw);
+        for (auto& W : part_w) lw.insert(lw.end(), W.begin(), W.end());
+    }
+    // Dispatch order: the bulk in packing order (co-resident waves share one
+    // width's code), the shortest waves filling the last tail_rounds rounds of
+    // wave slots last, longest first (LPT, duration ~ BC * nsteps), so the chip
+    // drains evenly. Waves address their pairs through slot0: no pair moves.
+    {
+        const int64_t tail_rounds = std::max<int64_t>(0, env_i64("HC_PHMM_TAIL_ROUNDS", 2));
         const size_t nw = lw.size();
-        const size_t K = std::min(nw, size_t(tail_rounds) * 4 * g_eng.n_cu * kSegWavesPerSimd);
+        const size_t K = std::min(nw, size_t(tail_rounds) * 4 * size_t(dv.n_cu) * kSegWavesPerSimd);
         auto cost = [&](size_t k) { return int64_t(lw[k].ncols) * lw[k].nsteps; };
-        std::vector<uint32_t> id(nw);
-        for (size_t k = 0; k < nw; ++k) id[k] = uint32_t(k);
-        if (K < nw)
-            std::nth_element(id.begin(), id.begin() + K, id.end(), [&](uint32_t x, uint32_t y) {
+        if (K > 0 && K < nw) {
+            std::vector<uint32_t> id(nw);
+            std::iota(id.begin(), id.end(), 0u);
+            std::nth_element(id.begin(), id.begin() + long(K), id.end(), [&](uint32_t x, uint32_t y) {
                 return cost(x) != cost(y) ? cost(x) < cost(y) : x < y;
             });
-        std::vector<uint8_t> in_tail(nw, 0);
-        for (size_t k = 0; k < K; ++k) in_tail[id[k]] = 1;
-        std::vector<LaneWave> ordered;
-        ordered.reserve(nw);
-        for (size_t k = 0; k < nw; ++k)
-            if (!in_tail[k]) ordered.push_back(lw[k]);
-        const size_t t0 = ordered.size();
-        for (size_t k = 0; k < nw; ++k)
-            if (in_tail[k]) ordered.push_back(lw[k]);
-        std::stable_sort(ordered.begin() + t0, ordered.end(), [](const LaneWave& x, const LaneWave& y) {
-            return int64_t(x.ncols) * x.nsteps > int64_t(y.ncols) * y.nsteps;
-        });
-        lw.swap(ordered);
+            std::vector<uint8_t> in_tail(nw, 0);
+            for (size_t k = 0; k < K; ++k) in_tail[id[k]] = 1;
+            std::vector<LaneWave> ordered;
+            ordered.reserve(nw);
+            for (size_t k = 0; k < nw; ++k)
+                if (!in_tail[k]) ordered.push_back(lw[k]);
+            const size_t t0 = ordered.size();
+            for (size_t k = 0; k < nw; ++k)
+                if (in_tail[k]) ordered.push_back(lw[k]);
+            std::stable_sort(ordered.begin() + long(t0), ordered.end(), [](const LaneWave& x, const LaneWave& y) {
+                return int64_t(x.ncols) * x.nsteps > int64_t(y.ncols) * y.nsteps;
+            });
+            lw.swap(ordered);
+        }
     }
-    tm.mark("bin: seg pack");
+    tm.mark("seg pack");
     const int n_seg_waves = int(lw.size());
     const int n_seg_slots = int(seg_ord.size());
-    auto cols16 = [&](int p) { return (pd[p].w + 15) / 16 * 16; };
-    for (int p : one_ord) key[p] = (uint32_t(cols16(p)) << 16) | uint32_t(std::min(pd[p].y, 65535));
-    sort_desc(one_ord, key);
-    const size_t per_wave = size_t(64) * lane_p;
-    for (size_t s0 = 0; s0 < one_ord.size(); s0 += per_wave) {
-        LaneWave w{};
-        w.slot0 = n_seg_slots + int(s0);
-        w.rmin = INT32_MAX;
-        for (size_t k = s0; k < std::min(one_ord.size(), s0 + per_wave); ++k) {
-            const int p = one_ord[k];
-            w.rmax = std::max(w.rmax, pd[p].y);
-            w.rmin = std::min(w.rmin, pd[p].y);
-            w.ncols = std::max(w.ncols, cols16(p));
+    // One lane per pair with the carry buffer (haps longer than the segmented
+    // kernel's reach, or policy "off"): binned by (H rounded up to 16, R).
+    const int lane_var = lane_variant_id();
+    const LaneVariant& LV = lane_variant(lane_var);
+    int64_t carry_rows = 0;
+    {
+        std::vector<uint32_t> key(static_cast<size_t>(npairs));
+        auto cols16 = [&](int p) { return (pd[p].w + 15) / 16 * 16; };
+        for (int p : one_ord) key[size_t(p)] = (uint32_t(cols16(p)) << 16) | uint32_t(std::min(pd[p].y, 65535));
+        sort_desc(one_ord, key);
+        const size_t per_wave = size_t(64) * LV.P;
+        for (size_t s0 = 0; s0 < one_ord.size(); s0 += per_wave) {
+            LaneWave w{};
+            w.slot0 = n_seg_slots + int(s0);
+            w.rmin = INT32_MAX;
+            for (size_t k = s0; k < std::min(one_ord.size(), s0 + per_wave); ++k) {
+                const int p = one_ord[k];
+                w.rmax = std::max(w.rmax, pd[p].y);
+                w.rmin = std::min(w.rmin, pd[p].y);
+                w.ncols = std::max(w.ncols, cols16(p));
+            }
+            w.carry_row = carry_rows;
+            if (w.ncols > LV.BC) carry_rows += w.rmax + 1;
+            lw.push_back(w);
         }
-        w.carry_row = carry_rows;
-        if (w.ncols > LV.BC) carry_rows += w.rmax + 1;
-        lw.push_back(w);
-    }
-    lane_ord = std::move(seg_ord);
-    lane_ord.insert(lane_ord.end(), one_ord.begin(), one_ord.end());
-    // Anti-diagonal classes: W by H; (stripes, H) descending so the G pairs
-    // sharing a wave have equal stripe counts and similar H, heaviest first.
-    const int Wc[2] = {16, 64};
-    int ring_len[2];
-    for (int c = 0; c < 2; ++c) {
-        const int W = Wc[c];
-        int hm = 0;
-        for (int p : ord[c]) {
-            key[p] = (uint32_t((pd[p].y + W - 1) / W) << 16) | uint32_t(pd[p].w);
-            hm = std::max(hm, pd[p].w);
+        // Anti-diagonal classes: W by H; (stripes, H) descending so the G pairs
+        // sharing a wave have equal stripe counts and similar H, heaviest first.
+        const int Wc[2] = {16, 64};
+        for (int c = 0; c < 2; ++c) {
+            for (int p : ord2[c]) key[size_t(p)] = (uint32_t((pd[p].y + Wc[c] - 1) / Wc[c]) << 16) | uint32_t(pd[p].w);
+            sort_desc(ord2[c], key);
         }
-        sort_desc(ord[c], key);
-        ring_len[c] = hm + 2 * W + 16;
     }
+    const int Hmax = hmax_a.load();
+    tm.mark("one-lane/diag bins");
 
-    tm.mark("binning");
-    // One device region: uploaded arrays first, then outputs and scratch.
-    // Host uploads raw bytes; the device packs rows and hap tables
-    // (pack_kernels.hip), so the host work is memcpy.
-    std::vector<int64_t> hb_off(nh + 1, 0);
-    for (int64_t h = 0; h < nh; ++h) hb_off[h + 1] = hb_off[h] + haps[h].len;
-    const size_t nrows = size_t(row_off[nr]);
-    const size_t stride = (nrows + 16 + 15) & ~size_t(15);   // one byte plane, padded
+    // Staging fill: order, wave list, read descriptors + bytes, hap bytes.
+    int* ordp = reinterpret_cast<int*>(host + o_ord);
+    std::memcpy(ordp, seg_ord.data(), sizeof(int) * seg_ord.size());
+    std::memcpy(ordp + seg_ord.size(), one_ord.data(), sizeof(int) * one_ord.size());
+    const size_t o_ord0 = seg_ord.size() + one_ord.size();
+    std::memcpy(ordp + o_ord0, ord2[0].data(), sizeof(int) * ord2[0].size());
+    std::memcpy(ordp + o_ord0 + ord2[0].size(), ord2[1].data(), sizeof(int) * ord2[1].size());
+    std::memcpy(host + o_lw, lw.data(), sizeof(LaneWave) * lw.size());
+    const size_t upload = o_lw + sizeof(LaneWave) * lw.size();
+    int4* rdesc = reinterpret_cast<int4*>(host + o_rd);
+    uint8_t* hb = reinterpret_cast<uint8_t*>(host + o_bases);
+    uint8_t* hq = reinterpret_cast<uint8_t*>(host + o_quals);
+    uint8_t* hg = reinterpret_cast<uint8_t*>(host + o_gaps);
+    parallel_for(nr, [&](int64_t b, int64_t e) {
+        for (int64_t r = b; r < e; ++r) {
+            const ReadView v = src.read(loc.read_id(r));
+            const size_t o = size_t(row_off[size_t(r)]);
+            std::memcpy(hb + o, v.bases, size_t(v.len));
+            std::memcpy(hq + o, v.q, size_t(v.len));
+            const int32_t g = gapw[size_t(r)];
+            int go = 0;
+            if (g < 0) {
+                go = int(gap_off[size_t(r)]);
+                std::memcpy(hg + go, v.i, size_t(v.len));
+                std::memcpy(hg + gap_stride + size_t(go), v.d, size_t(v.len));
+                std::memcpy(hg + 2 * gap_stride + size_t(go), v.c, size_t(v.len));
+            }
+            rdesc[r] = make_int4(int(o), v.len, g, go);
+        }
+    }, 256);
+    int4* hdesc = reinterpret_cast<int4*>(host + o_hd);
+    uint8_t* hbytes = reinterpret_cast<uint8_t*>(host + o_hb);
+    parallel_for(nh, [&](int64_t b, int64_t e) {
+        for (int64_t h = b; h < e; ++h) {
+            const HapView v = src.hapv(loc.hap_id(h));
+            std::memcpy(hbytes + hap_b[size_t(h)], v.bases, size_t(v.len));
+            hdesc[h] = make_int4(int(hap_b[size_t(h)]), v.len, int(hap_w[size_t(h)]), 0);
+        }
+    }, 256);
+    tm.mark("staging fill");
+
+    // Device region: the upload image, then packed rows / tables, outputs, scratch.
     Layout L;
-    const size_t o_pairs = L.take(sizeof(PairDesc) * npairs);
-    const size_t o_raw = L.take(5 * stride);
-    const size_t o_hb = L.take(size_t(hb_off[nh]) + 16);
-    const size_t o_hd = L.take(sizeof(int4) * nh);
-    const size_t o_t0 = L.take(sizeof(long long) * nh);
-    const size_t o_rd = L.take(sizeof(int2) * nr);
-    const size_t o_ord0 = L.take(sizeof(int) * ord[0].size());
-    const size_t o_ord1 = L.take(sizeof(int) * ord[1].size());
-    const size_t o_lord = L.take(sizeof(int) * lane_ord.size());
-    const size_t o_lw = L.take(sizeof(LaneWave) * lw.size());
-    const size_t upload = L.off;
-    const size_t o_rows = L.take(sizeof(uint32_t) * (nrows + 16));
-    const size_t o_hapw = L.take(sizeof(uint32_t) * (hap_off[nh] + 1));
-    const size_t n1 = size_t(std::max<int64_t>(npairs, 1));
-    const size_t o_raw32 = L.take(sizeof(float) * n1);
-    const size_t o_raw64 = L.take(sizeof(double) * n1);
-    const size_t o_flag = L.take(n1);
+    L.off = (upload + 255) & ~size_t(255);
+    const size_t o_rows = L.take(sizeof(uint32_t) * (size_t(nrows) + 16));
+    const size_t o_hapw = L.take(sizeof(uint32_t) * (size_t(hap_w[size_t(nh)]) + 1));
+    const size_t o_res = L.take(res_bytes);
     const size_t o_list = L.take(sizeof(int) * n1);
     const size_t o_count = L.take(2 * sizeof(int));
     const size_t o_sorted = L.take(sizeof(int) * n1);
     const size_t o_big = L.take(sizeof(int) * n1);
     const size_t o_bigc = L.take(sizeof(int));
     const size_t o_plan = L.take(sizeof(Seg64Plan));
-    const size_t o_carry = L.take(sizeof(float2) * size_t(carry_rows) * 64 * lane_p);
+    const size_t o_carry = L.take(sizeof(float2) * size_t(carry_rows) * 64 * LV.P);
     const size_t total = L.off;
 
-    char* host = nullptr;
-    bool own_host = false;
-    int rc = HC_PHMM_OK;
-    if (borrow_ws) {
-        rc = ws_host(upload, &host);
-    } else {
-        if (hipHostMalloc(&host, std::max<size_t>(upload, 1), hipHostMallocDefault) != hipSuccess)
-            rc = fail(HC_PHMM_ENOMEM, "pinned staging buffer");
-        own_host = true;
-    }
-    if (rc) return rc;
-    tm.mark("staging alloc");
-
-    // Fill the staging image (parallel over reads and haps).
-    std::memcpy(host + o_pairs, pd.data(), sizeof(PairDesc) * npairs);
-    uint8_t* raw = reinterpret_cast<uint8_t*>(host + o_raw);
-    int2* rdesc = reinterpret_cast<int2*>(host + o_rd);
-    parallel_for(nr, [&](int64_t b, int64_t e) {
-        for (int64_t r = b; r < e; ++r) {
-            const ReadView& v = reads[r];
-            const size_t o = size_t(row_off[r]);
-            std::memcpy(raw + o, v.bases, v.len);
-            std::memcpy(raw + stride + o, v.q, v.len);
-            std::memcpy(raw + 2 * stride + o, v.i, v.len);
-            std::memcpy(raw + 3 * stride + o, v.d, v.len);
-            std::memcpy(raw + 4 * stride + o, v.c, v.len);
-            rdesc[r] = make_int2(int(o), v.len);
-        }
-    }, 1024);
-    uint8_t* hb = reinterpret_cast<uint8_t*>(host + o_hb);
-    int4* hd = reinterpret_cast<int4*>(host + o_hd);
-    long long* t0 = reinterpret_cast<long long*>(host + o_t0);
-    parallel_for(nh, [&](int64_t b, int64_t e) {
-        for (int64_t h = b; h < e; ++h) {
-            std::memcpy(hb + hb_off[h], haps[h].bases, haps[h].len);
-            hd[h] = make_int4(int(hb_off[h]), haps[h].len, int(hap_off[h]), 0);
-            t0[h] = hap_off[h] / 5;
-        }
-    }, 1024);
-    std::memcpy(host + o_ord0, ord[0].data(), sizeof(int) * ord[0].size());
-    std::memcpy(host + o_ord1, ord[1].data(), sizeof(int) * ord[1].size());
-    std::memcpy(host + o_lord, lane_ord.data(), sizeof(int) * lane_ord.size());
-    std::memcpy(host + o_lw, lw.data(), sizeof(LaneWave) * lw.size());
-
-    tm.mark("pack");
-    auto* b = new hc_phmm_batch();
+    auto* b = new Part();
+    b->dev = &dv;
+    b->spec = spec;
+    b->slot = slot;
     char* dev = nullptr;
-    if (borrow_ws) {
-        rc = ws_dev(total, &dev);
-        b->owns_dev = false;
+    int rc = HC_PHMM_OK;
+    if (slot) {
+        rc = slot_reserve(*slot, total, 0);
+        dev = slot->dev;
     } else if (hipMalloc(&dev, total) != hipSuccess) {
         rc = fail(HC_PHMM_ENOMEM, "device allocation failed (" + std::to_string(total >> 20) + " MiB)");
     }
-    if (rc == HC_PHMM_OK) {
-        b->dev_base = dev;
-        // The workspace staging stays valid until the call returns, so only a
-        // batch-owned staging buffer needs the copy to finish here.
-        hipError_t e1 = hipMemcpyAsync(dev, host, upload, hipMemcpyHostToDevice, g_eng.stream);
-        if (e1 == hipSuccess) e1 = hipMemsetAsync(dev + o_count, 0, 2 * sizeof(int), g_eng.stream);
-        if (e1 == hipSuccess)
-            e1 = launch_pack_rows(reinterpret_cast<const uint8_t*>(dev + o_raw), (long long)nrows,
-                                  (long long)stride, reinterpret_cast<uint32_t*>(dev + o_rows), g_eng.stream);
-        if (e1 == hipSuccess && !std::getenv("HC_PHMM_NO_CG"))   // A/B switch for the CG path
-            e1 = launch_mark_cg(reinterpret_cast<uint32_t*>(dev + o_rows), reinterpret_cast<const int2*>(dev + o_rd),
-                                int(nr), g_eng.stream);
-        if (e1 == hipSuccess)
-            e1 = launch_hap_tables(reinterpret_cast<const uint8_t*>(dev + o_hb),
-                                   reinterpret_cast<const int4*>(dev + o_hd), int(nh),
-                                   reinterpret_cast<const long long*>(dev + o_t0), hap_off[nh] / 5,
-                                   reinterpret_cast<uint32_t*>(dev + o_hapw), g_eng.stream);
-        const hipError_t e2 = (e1 == hipSuccess && own_host) ? hipStreamSynchronize(g_eng.stream) : e1;
-        if (e2 != hipSuccess) rc = fail(HC_PHMM_EHIP, std::string("H2D: ") + hipGetErrorString(e2));
-    }
-    if (own_host) (void)hipHostFree(host);
-    tm.mark("device alloc+H2D");
-    if (rc != HC_PHMM_OK) {
-        free_batch(b);
+    if (rc) {
+        b->slot = nullptr;   // the caller returns the slot
+        free_part(b);
         return rc;
     }
+    b->dev_base = dev;
     b->n = npairs;
-    b->cells = cells;
+    b->cells = cells_a.load();
     b->Hmax = Hmax;
-    b->n_lane = int(lane_ord.size());
+    b->n_lane = int(seg_ord.size() + one_ord.size());
     b->n_seg_waves = n_seg_waves;
     b->lane_variant = lane_var;
     b->lane_waves = int(lw.size());
+    b->upload_bytes = upload;
     b->d_pairs = reinterpret_cast<PairDesc*>(dev + o_pairs);
     b->d_rows = reinterpret_cast<uint32_t*>(dev + o_rows);
     b->d_hapw = reinterpret_cast<uint32_t*>(dev + o_hapw);
+    const int Wc[2] = {16, 64};
+    int* d_ord = reinterpret_cast<int*>(dev + o_ord);
+    b->d_lane_order = d_ord;
+    b->cls[0].d_order = d_ord + o_ord0;
+    b->cls[1].d_order = d_ord + o_ord0 + ord2[0].size();
     for (int c = 0; c < 2; ++c) {
         b->cls[c].W = Wc[c];
-        b->cls[c].n = int(ord[c].size());
-        b->cls[c].ring_len = ring_len[c];
+        b->cls[c].n = int(ord2[c].size());
+        int hm = 0;
+        for (int p : ord2[c]) hm = std::max(hm, pd[p].w);
+        b->cls[c].ring_len = hm + 2 * Wc[c] + 16;
     }
-    b->cls[0].d_order = reinterpret_cast<int*>(dev + o_ord0);
-    b->cls[1].d_order = reinterpret_cast<int*>(dev + o_ord1);
-    b->d_lane_order = reinterpret_cast<int*>(dev + o_lord);
     b->d_lane_waves = reinterpret_cast<LaneWave*>(dev + o_lw);
-    b->own_raw32 = b->d_raw32 = reinterpret_cast<float*>(dev + o_raw32);
-    b->own_raw64 = b->d_raw64 = reinterpret_cast<double*>(dev + o_raw64);
-    b->own_flag = b->d_flag = reinterpret_cast<uint8_t*>(dev + o_flag);
+    b->res_bytes = res_bytes;
+    b->res_o64 = res_o64;
+    b->res_ofl = res_ofl;
+    b->own_raw32 = b->d_raw32 = reinterpret_cast<float*>(dev + o_res);
+    b->own_raw64 = b->d_raw64 = reinterpret_cast<double*>(dev + o_res + res_o64);
+    b->own_flag = b->d_flag = reinterpret_cast<uint8_t*>(dev + o_res + res_ofl);
     b->d_list = reinterpret_cast<int*>(dev + o_list);
     b->d_count = reinterpret_cast<int*>(dev + o_count);
     b->d_sorted = reinterpret_cast<int*>(dev + o_sorted);
     b->d_big = reinterpret_cast<int*>(dev + o_big);
     b->d_big_count = reinterpret_cast<int*>(dev + o_bigc);
     b->d_plan = reinterpret_cast<Seg64Plan*>(dev + o_plan);
-    b->n_wide = n_wide;
+    b->n_wide = wide_a.load();
     b->d_carry = carry_rows ? reinterpret_cast<float2*>(dev + o_carry) : nullptr;
+    if (slot) b->host_res = host + host_res_off;
+
+    hipStream_t s = dv.stream;
+    auto enqueue = [&]() -> int {
+        for (auto& e : b->pack_ev) HIP_TRY(hipEventCreate(&e));
+        HIP_TRY(hipMemcpyAsync(dev, host, upload, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemsetAsync(b->d_count, 0, 2 * sizeof(int), s));
+        HIP_TRY(hipEventRecord(b->pack_ev[0], s));
+        HIP_TRY(launch_pack_reads(reinterpret_cast<const uint8_t*>(dev + o_bases),
+                                  reinterpret_cast<const uint8_t*>(dev + o_quals),
+                                  reinterpret_cast<const uint8_t*>(dev + o_gaps), (long long)gap_stride,
+                                  reinterpret_cast<const int4*>(dev + o_rd), int(nr), b->d_rows, s));
+        HIP_TRY(launch_hap_tables(reinterpret_cast<const uint8_t*>(dev + o_hb), reinterpret_cast<const int4*>(dev + o_hd),
+                                  int(nh), b->d_hapw, s));
+        HIP_TRY(hipEventRecord(b->pack_ev[1], s));
+        if (with_run) {
+            const int r = run_part(b, s);
+            if (r) return r;
+            HIP_TRY(hipMemcpyAsync(b->host_res, dev + o_res, res_bytes, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipEventCreateWithFlags(&b->done, hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(b->done, s));
+        }
+        // A part-owned staging buffer is freed on return: the copy must be done.
+        if (own_host) HIP_TRY(hipStreamSynchronize(s));
+        return HC_PHMM_OK;
+    };
+    rc = enqueue();
+    tm.mark("enqueue");
+    if (rc) {
+        (void)hipStreamSynchronize(s);
+        b->slot = nullptr;
+        free_part(b);
+        return rc;
+    }
     *out = b;
     return HC_PHMM_OK;
 }
 
-int run(hc_phmm_batch* b, hipStream_t s)
+int run_part(Part* b, hipStream_t s)
 {
-    if (!s) s = g_eng.stream;
+    Device& dv = *b->dev;
     b->last_stream = s;
     b->launch_waves = 0;
     if (b->ev_used == b->ev_pool.size()) {
@@ -728,7 +1079,7 @@ int run(hc_phmm_batch* b, hipStream_t s)
     for (int k = 0; k < 3; ++k) b->ev[k] = ev[k];
     HIP_TRY(hipEventRecord(b->ev[0], s));
     // No memsets: the fp32 kernels zero each pair's raw f64 slot as they emit,
-    // and the rescue kernel zeroes the other parity's counter for the next run.
+    // and the rescue planner zeroes the other parity's counter for the next run.
     const int par = b->parity;
     b->parity ^= 1;
     int* count = b->d_count + par;
@@ -740,7 +1091,7 @@ int run(hc_phmm_batch* b, hipStream_t s)
         a.carry = b->d_carry;
         a.rows = b->d_rows;
         a.hapw = b->d_hapw;
-        a.lut = g_eng.lut_f;
+        a.lut = dv.lut_f;
         a.raw_out = b->d_raw32;
         a.rescue_flag = b->d_flag;
         a.rescue_list = b->d_list;
@@ -756,18 +1107,18 @@ int run(hc_phmm_batch* b, hipStream_t s)
             g.waves = b->d_lane_waves;
             g.n_waves = b->n_seg_waves;
             if (fork) {
-                HIP_TRY(hipEventRecord(g_eng.fork, s));
-                HIP_TRY(hipStreamWaitEvent(g_eng.side, g_eng.fork, 0));
+                HIP_TRY(hipEventRecord(dv.fork, s));
+                HIP_TRY(hipStreamWaitEvent(dv.side, dv.fork, 0));
             }
-            HIP_TRY(launch_lane_seg_f32(g, fork ? g_eng.side : s));
-            if (fork) HIP_TRY(hipEventRecord(g_eng.join, g_eng.side));
+            HIP_TRY(launch_lane_seg_f32(g, fork ? dv.side : s));
+            if (fork) HIP_TRY(hipEventRecord(dv.join, dv.side));
         }
         if (n_one > 0) {
             a.waves = b->d_lane_waves + b->n_seg_waves;
             a.n_waves = n_one;
             HIP_TRY(launch_lane_f32(b->lane_variant, a, s));
         }
-        if (fork) HIP_TRY(hipStreamWaitEvent(s, g_eng.join, 0));
+        if (fork) HIP_TRY(hipStreamWaitEvent(s, dv.join, 0));
     }
     for (auto& c : b->cls) {
         if (c.n == 0) continue;
@@ -777,7 +1128,7 @@ int run(hc_phmm_batch* b, hipStream_t s)
         a.n_slots = c.n;
         a.rows = b->d_rows;
         a.hapw = b->d_hapw;
-        a.lut = g_eng.lut_f;
+        a.lut = dv.lut_f;
         a.ring_len = c.ring_len;
         a.raw_out = b->d_raw32;
         a.rescue_flag = b->d_flag;
@@ -799,7 +1150,7 @@ int run(hc_phmm_batch* b, hipStream_t s)
         r.pairs = b->d_pairs;
         r.rows = b->d_rows;
         r.hapw = b->d_hapw;
-        r.lut = g_eng.lut_d;
+        r.lut = dv.lut_d;
         r.list = b->d_list;
         r.count = count;
         r.count_reset = b->d_count + (par ^ 1);
@@ -808,8 +1159,8 @@ int run(hc_phmm_batch* b, hipStream_t s)
         r.big_count = b->d_big_count;
         r.plan = b->d_plan;
         r.raw_out = b->d_raw64;
-        r.min_lanes = int64_t(2) * 4 * g_eng.n_cu * 64;
-        const int grid = int(std::min<int64_t>((b->n + 3) / 4, int64_t(2) * g_eng.n_cu));
+        r.min_lanes = int64_t(2) * 4 * dv.n_cu * 64;
+        const int grid = int(std::min<int64_t>((b->n + 3) / 4, int64_t(2) * dv.n_cu));
         HIP_TRY(launch_rescue_seg64(r, grid, s));
         if (b->n_wide > 0) {
             DiagArgs a{};
@@ -818,7 +1169,7 @@ int run(hc_phmm_batch* b, hipStream_t s)
             a.n_slots_dev = b->d_big_count;
             a.rows = b->d_rows;
             a.hapw = b->d_hapw;
-            a.lut = g_eng.lut_d;
+            a.lut = dv.lut_d;
             a.ring_len = b->Hmax + 2 * 64 + 16;
             a.raw_out = b->d_raw64;
             HIP_TRY(launch_diag_f64(64, a, int(std::min<int64_t>(b->n_wide, 2048)), s));
@@ -829,69 +1180,288 @@ int run(hc_phmm_batch* b, hipStream_t s)
     return HC_PHMM_OK;
 }
 
-int results(hc_phmm_batch* b, double* loglik, float* raw32, double* raw64, uint8_t* resc)
+// log10 finish (intel_pairhmm.hpp:137-143, glibc log10 / log10f as in the
+// reference) of a part's results, scattered into the caller's outputs.
+void finish_part(const Part& P, const float* f, const double* d, const uint8_t* fl, const Outputs& o)
 {
-    if (!b->ran) return fail(HC_PHMM_EINVAL, "batch has not been run");
-    const int64_t n = b->n;
-    if (n == 0) return HC_PHMM_OK;
-    // D2H into the pinned workspace: [raw32 | raw64 | flags]. Drain the stream
-    // first: growing the workspace frees the staging an earlier H2D read.
-    HIP_TRY(hipStreamSynchronize(b->last_stream));
-    char* host = nullptr;
-    const size_t o64 = (sizeof(float) * n + 15) & ~size_t(15);
-    const size_t ofl = o64 + sizeof(double) * n;
-    int rc = ws_host(ofl + n, &host);
-    if (rc) return rc;
-    hipStream_t s = b->last_stream;
-    HIP_TRY(hipMemcpyAsync(host, b->d_raw32, sizeof(float) * n, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(host + o64, b->d_raw64, sizeof(double) * n, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(host + ofl, b->d_flag, n, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    const float* f = reinterpret_cast<const float*>(host);
-    const double* d = reinterpret_cast<const double*>(host + o64);
-    const uint8_t* fl = reinterpret_cast<const uint8_t*>(host + ofl);
-    if (raw32) std::memcpy(raw32, f, sizeof(float) * n);
-    if (raw64) std::memcpy(raw64, d, sizeof(double) * n);
-    if (resc) std::memcpy(resc, fl, n);
-    if (loglik) {
-        // intel_pairhmm.hpp:137-143, glibc log10 / log10f as in the reference.
-        const Luts& L = luts();
-        const float l10f = L.log10_init_f;
-        const double l10d = L.log10_init_d;
-        parallel_for(n, [&](int64_t lo, int64_t hi) {
-            for (int64_t p = lo; p < hi; ++p)
-                loglik[p] = fl[p] ? std::log10(d[p]) - l10d : double(std::log10(f[p]) - l10f);
-        }, 1 << 15);
+    const Luts& L = luts();
+    const float l10f = L.log10_init_f;
+    const double l10d = L.log10_init_d;
+    auto ll = [&](int64_t k) { return fl[k] ? std::log10(d[k]) - l10d : double(std::log10(f[k]) - l10f); };
+    if (P.spec.flat) {
+        const int64_t id0 = P.spec.lo;
+        parallel_for(P.n, [&](int64_t lo, int64_t hi) {
+            for (int64_t k = lo; k < hi; ++k) {
+                if (o.loglik) o.loglik[id0 + k] = ll(k);
+                if (o.raw32) o.raw32[id0 + k] = f[k];
+                if (o.raw64) o.raw64[id0 + k] = d[k];
+                if (o.resc) o.resc[id0 + k] = fl[k];
+            }
+        }, 1 << 13);
+        return;
     }
+    // Blocks: pair k of block b is (r, h) = divmod(k - base, nh).
+    std::vector<int64_t> base(P.spec.blocks.size() + 1, 0);
+    for (size_t b = 0; b < P.spec.blocks.size(); ++b)
+        base[b + 1] = base[b] + int64_t(P.spec.blocks[b].nr) * P.spec.blocks[b].nh;
+    parallel_for(P.n, [&](int64_t lo, int64_t hi) {
+        size_t b = size_t(std::upper_bound(base.begin(), base.end(), lo) - base.begin()) - 1;
+        int64_t k = lo;
+        while (k < hi) {
+            const Block& B = P.spec.blocks[b];
+            const int64_t end = std::min(hi, base[b + 1]);
+            int64_t r = (k - base[b]) / B.nh, h = (k - base[b]) % B.nh;
+            for (; k < end; ++k) {
+                B.out[r * B.ostride + h] = ll(k);
+                if (++h == B.nh) {
+                    h = 0;
+                    ++r;
+                }
+            }
+            ++b;
+        }
+    }, 1 << 13);
+}
+
+// ---------------------------------------------------------------------------
+// Splitting a call into parts.
+
+// Cut a sequence of units with weights into `nparts` contiguous ranges of
+// (nearly) equal weight: returns nparts + 1 boundaries.
+std::vector<int64_t> equal_cuts(const std::vector<int64_t>& prefix, int nparts)
+{
+    const int64_t n = int64_t(prefix.size()) - 1;
+    const int64_t tot = prefix.back();
+    std::vector<int64_t> cut(static_cast<size_t>(nparts) + 1, 0);
+    cut[size_t(nparts)] = n;
+    for (int j = 1; j < nparts; ++j) {
+        const int64_t target = (tot * j + nparts / 2) / nparts;
+        int64_t c = int64_t(std::lower_bound(prefix.begin(), prefix.end(), target) - prefix.begin());
+        cut[size_t(j)] = std::max(cut[size_t(j) - 1], std::min(n, c));
+    }
+    return cut;
+}
+
+// How many parts for `cells` over the configured devices: one part per device
+// above HC_PHMM_SHARD_MIN_CELLS, and chunks of about HC_PHMM_CHUNK_CELLS per
+// part above that, so planning overlaps the device passes.
+int part_count(int64_t cells, int ndev)
+{
+    const int64_t shard_min = env_i64("HC_PHMM_SHARD_MIN_CELLS", int64_t(2000000000));
+    const int64_t chunk = std::max<int64_t>(1, env_i64("HC_PHMM_CHUNK_CELLS", int64_t(12000000000)));
+    if (cells < shard_min) return 1;
+    const int64_t per_dev = (cells + ndev - 1) / ndev;
+    const int64_t chunks = std::max<int64_t>(1, (per_dev + chunk / 2) / chunk);
+    return int(std::min<int64_t>(int64_t(ndev) * chunks, 4096));
+}
+
+Device* least_loaded()
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    Device* best = g_devs[0];
+    for (Device* d : g_devs)
+        if (d->outstanding < best->outstanding) best = d;
+    return best;
+}
+
+// Plan + enqueue every part of a call (device of part j = j mod #devices, or
+// the least loaded device for a one-part call); returns the job.
+int submit(const Src& src, const std::vector<PartSpec>& specs, const std::vector<double>& part_cells,
+           const Outputs& out, hc_phmm_job** job)
+{
+    auto* J = new hc_phmm_job();
+    J->out = out;
+    const int G = int(g_devs.size());
+    Device* solo = specs.size() == 1 ? least_loaded() : nullptr;
+    for (size_t j = 0; j < specs.size(); ++j) {
+        Device& d = solo ? *solo : *g_devs[j % size_t(G)];
+        int rc = hipSetDevice(d.ordinal) == hipSuccess ? HC_PHMM_OK : fail(HC_PHMM_EHIP, "hipSetDevice");
+        Slot* sl = rc ? nullptr : take_slot(d);
+        Part* p = nullptr;
+        if (!rc) rc = plan_part(d, src, specs[j], sl, true, &p);
+        if (rc) {
+            if (sl) give_slot(sl);
+            for (Part* q : J->parts) {
+                (void)hipSetDevice(q->dev->ordinal);
+                (void)hipStreamSynchronize(q->dev->stream);
+                free_part(q);
+            }
+            delete J;
+            return rc;
+        }
+        {
+            std::lock_guard<std::mutex> lk(g_mu);
+            d.outstanding += part_cells[j];
+        }
+        J->parts.push_back(p);
+        J->cells_per_part.push_back(part_cells[j]);
+    }
+    *job = J;
     return HC_PHMM_OK;
 }
 
-int run_sync(hc_phmm_batch* b, double* loglik, float* raw32, double* raw64, uint8_t* resc)
+int collect(hc_phmm_job* J)
 {
-    PhaseTimer tm;
-    int rc = run(b, nullptr);
-    tm.mark("run (launch)");
-    if (rc == HC_PHMM_OK) rc = results(b, loglik, raw32, raw64, resc);
-    tm.mark("results+finish");
+    int rc = HC_PHMM_OK;
+    for (size_t j = 0; j < J->parts.size(); ++j) {
+        Part* p = J->parts[j];
+        if (rc == HC_PHMM_OK) {
+            (void)hipSetDevice(p->dev->ordinal);
+            const hipError_t e = hipEventSynchronize(p->done);
+            if (e != hipSuccess) {
+                rc = fail(HC_PHMM_EHIP, std::string("device pass: ") + hipGetErrorString(e));
+            } else {
+                const char* h = p->host_res;
+                finish_part(*p, reinterpret_cast<const float*>(h), reinterpret_cast<const double*>(h + p->res_o64),
+                            reinterpret_cast<const uint8_t*>(h + p->res_ofl), J->out);
+            }
+        } else {
+            (void)hipSetDevice(p->dev->ordinal);
+            (void)hipEventSynchronize(p->done);
+        }
+        {
+            std::lock_guard<std::mutex> lk(g_mu);
+            p->dev->outstanding -= J->cells_per_part[j];
+        }
+        free_part(p);
+    }
+    delete J;
     return rc;
 }
 
-int flat_views(int64_t n, const int64_t* read_off, const int32_t* R, const int64_t* hap_off,
-               const int32_t* H, const uint8_t* rs, const uint8_t* q, const uint8_t* ins,
-               const uint8_t* del, const uint8_t* gcp, const uint8_t* hap,
-               std::vector<ReadView>& rv, std::vector<HapView>& hv, std::vector<int32_t>& idx)
+// Flat pairs [0, n): cut into parts of equal cells.
+int submit_flat(const Src& src, int64_t n, const Outputs& out, hc_phmm_job** job)
 {
-    if (n < 0) return fail(HC_PHMM_EINVAL, "negative pair count");
-    if (n > 0 && (!read_off || !R || !hap_off || !H || !rs || !q || !ins || !del || !gcp || !hap))
-        return fail(HC_PHMM_EINVAL, "null input array");
-    rv.resize(n);
-    hv.resize(n);
-    idx.resize(n);
-    for (int64_t p = 0; p < n; ++p) {
-        const int64_t o = read_off[p];
-        rv[p] = ReadView{R[p], rs + o, q + o, ins + o, del + o, gcp + o};
-        hv[p] = HapView{H[p], hap + hap_off[p]};
-        idx[p] = int32_t(p);
+    std::vector<int64_t> pre;
+    prefix_sum(n, pre, [&](int64_t p) { return int64_t(src.R[p] > 0 ? src.R[p] : 0) * (src.H[p] > 0 ? src.H[p] : 0); });
+    const int np = part_count(pre.back(), int(g_devs.size()));
+    const std::vector<int64_t> cut = equal_cuts(pre, np);
+    std::vector<PartSpec> specs;
+    std::vector<double> pc;
+    for (int j = 0; j < np; ++j) {
+        if (cut[size_t(j)] == cut[size_t(j) + 1] && np > 1) continue;
+        PartSpec s;
+        s.flat = true;
+        s.lo = cut[size_t(j)];
+        s.hi = cut[size_t(j) + 1];
+        specs.push_back(s);
+        pc.push_back(double(pre[size_t(s.hi)] - pre[size_t(s.lo)]));
+    }
+    return submit(src, specs, pc, out, job);
+}
+
+// Cross-product blocks (regions): a block larger than one part's share is cut
+// into read ranges; then contiguous runs of blocks form parts of equal cells.
+int submit_blocks(const Src& src, std::vector<Block> blocks, hc_phmm_job** job)
+{
+    int64_t cells = 0;
+    std::vector<int64_t> bc(blocks.size());
+    for (size_t k = 0; k < blocks.size(); ++k) {
+        int64_t rl = 0, hl = 0;
+        for (int32_t r = 0; r < blocks[k].nr; ++r) rl += std::max(0, src.read_len(blocks[k].r0 + r));
+        for (int32_t h = 0; h < blocks[k].nh; ++h) hl += std::max(0, src.hap_len(blocks[k].h0 + h));
+        bc[k] = rl * hl;
+        cells += bc[k];
+    }
+    const int np = part_count(cells, int(g_devs.size()));
+    if (np > 1) {
+        const int64_t share = (cells + np - 1) / np;
+        std::vector<Block> split;
+        for (size_t k = 0; k < blocks.size(); ++k) {
+            const Block& B = blocks[k];
+            const int pieces = int(std::min<int64_t>(B.nr, (bc[k] + share - 1) / std::max<int64_t>(share, 1)));
+            if (pieces <= 1) {
+                split.push_back(B);
+                continue;
+            }
+            for (int q = 0; q < pieces; ++q) {
+                const int32_t a = int32_t(int64_t(B.nr) * q / pieces), e = int32_t(int64_t(B.nr) * (q + 1) / pieces);
+                if (a == e) continue;
+                split.push_back(Block{B.r0 + a, e - a, B.h0, B.nh, B.out + int64_t(a) * B.ostride, B.ostride});
+            }
+        }
+        blocks.swap(split);
+    }
+    std::vector<int64_t> pre(blocks.size() + 1, 0);
+    for (size_t k = 0; k < blocks.size(); ++k) {
+        int64_t rl = 0, hl = 0;
+        for (int32_t r = 0; r < blocks[k].nr; ++r) rl += std::max(0, src.read_len(blocks[k].r0 + r));
+        for (int32_t h = 0; h < blocks[k].nh; ++h) hl += std::max(0, src.hap_len(blocks[k].h0 + h));
+        pre[k + 1] = pre[k] + rl * hl;
+    }
+    const int nparts = std::max(1, std::min<int>(np, int(blocks.size())));
+    const std::vector<int64_t> cut = equal_cuts(pre, nparts);
+    std::vector<PartSpec> specs;
+    std::vector<double> pc;
+    for (int j = 0; j < nparts; ++j) {
+        if (cut[size_t(j)] == cut[size_t(j) + 1]) continue;
+        PartSpec s;
+        s.flat = false;
+        s.blocks.assign(blocks.begin() + long(cut[size_t(j)]), blocks.begin() + long(cut[size_t(j) + 1]));
+        specs.push_back(std::move(s));
+        pc.push_back(double(pre[size_t(cut[size_t(j) + 1])] - pre[size_t(cut[size_t(j)])]));
+    }
+    if (specs.empty()) {
+        *job = new hc_phmm_job();
+        return HC_PHMM_OK;
+    }
+    return submit(src, specs, pc, Outputs{}, job);
+}
+
+Src flat_src(const int64_t* read_off, const int32_t* R, const int64_t* hap_off, const int32_t* H, const uint8_t* rs,
+             const uint8_t* q, const uint8_t* ins, const uint8_t* del, const uint8_t* gcp, const uint8_t* hap)
+{
+    Src s;
+    s.read_off = read_off;
+    s.R = R;
+    s.hap_off = hap_off;
+    s.H = H;
+    s.rs = rs;
+    s.q = q;
+    s.ins = ins;
+    s.del = del;
+    s.gcp = gcp;
+    s.hap = hap;
+    return s;
+}
+
+bool flat_args_ok(int64_t n, const int64_t* read_off, const int32_t* R, const int64_t* hap_off, const int32_t* H,
+                  const uint8_t* rs, const uint8_t* q, const uint8_t* ins, const uint8_t* del, const uint8_t* gcp,
+                  const uint8_t* hap)
+{
+    return n == 0 || (read_off && R && hap_off && H && rs && q && ins && del && gcp && hap);
+}
+
+// Regions -> one Src over concatenated read / hap structs + one block per region.
+struct RegionSet {
+    std::vector<hc_phmm_read> reads;
+    std::vector<hc_phmm_hap> haps;
+    std::vector<Block> blocks;
+};
+
+int gather_regions(const hc_phmm_region* regions, int32_t n_regions, RegionSet& rs)
+{
+    if (n_regions < 0 || (n_regions > 0 && !regions)) return fail(HC_PHMM_EINVAL, "bad region list");
+    size_t tr = 0, th = 0;
+    for (int k = 0; k < n_regions; ++k) {
+        const hc_phmm_region& g = regions[k];
+        if (g.n_reads < 0 || g.n_haps < 0) return fail(HC_PHMM_EINVAL, "negative count in region");
+        if (g.n_reads == 0 || g.n_haps == 0) continue;
+        if (!g.reads || !g.haps || !g.out) return fail(HC_PHMM_EINVAL, "null pointer in region");
+        tr += size_t(g.n_reads);
+        th += size_t(g.n_haps);
+    }
+    rs.reads.resize(tr);
+    rs.haps.resize(th);
+    size_t r0 = 0, h0 = 0;
+    for (int k = 0; k < n_regions; ++k) {
+        const hc_phmm_region& g = regions[k];
+        if (g.n_reads == 0 || g.n_haps == 0) continue;
+        std::memcpy(rs.reads.data() + r0, g.reads, sizeof(hc_phmm_read) * size_t(g.n_reads));
+        std::memcpy(rs.haps.data() + h0, g.haps, sizeof(hc_phmm_hap) * size_t(g.n_haps));
+        rs.blocks.push_back(Block{int64_t(r0), g.n_reads, int64_t(h0), g.n_haps, g.out, g.n_haps});
+        r0 += size_t(g.n_reads);
+        h0 += size_t(g.n_haps);
     }
     return HC_PHMM_OK;
 }
@@ -901,37 +1471,46 @@ int flat_views(int64_t n, const int64_t* read_off, const int32_t* R, const int64
 // --------------------------------------------------------------------------
 // C ABI
 namespace hcphmm {
-// Shared with sw_engine.cpp: one last-error slot per thread for the library.
 void set_last_error(const std::string& msg) { g_err = msg; }
+int primary_device()
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    return g_devs.empty() ? -1 : g_devs[0]->ordinal;
+}
 }  // namespace hcphmm
 
 extern "C" {
 
-int hc_phmm_version(void) { return 100; }
+int hc_phmm_version(void) { return 200; }
 
 const char* hc_phmm_last_error(void) { return g_err.c_str(); }
 
 int hc_phmm_init(uint32_t /*flags*/, int device)
 {
     std::lock_guard<std::mutex> lk(g_mu);
-    return ensure_init(device);
+    const int32_t d = device;
+    return init_devices_locked(&d, 1, device < 0);
+}
+
+int hc_phmm_init_devices(uint32_t /*flags*/, const int32_t* devices, int32_t n)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    return init_devices_locked(devices, n, false);
+}
+
+int hc_phmm_device_count(void)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    return int(g_devs.size());
 }
 
 int hc_phmm_shutdown(void)
 {
+    hcphmm::sw_release();
+    hcphmm::gt_release();
     std::lock_guard<std::mutex> lk(g_mu);
-    if (!g_eng.ready) return HC_PHMM_OK;
-    (void)hipFree(g_eng.lut_f);
-    (void)hipFree(g_eng.lut_d);
-    (void)hipFree(g_ws.dev);
-    (void)hipHostFree(g_ws.host);
-    free_batch(g_ws.batch);
-    g_ws = Workspace{};
-    (void)hipEventDestroy(g_eng.fork);
-    (void)hipEventDestroy(g_eng.join);
-    (void)hipStreamDestroy(g_eng.side);
-    (void)hipStreamDestroy(g_eng.stream);
-    g_eng = Engine{};
+    for (Device* d : g_devs) release_device(d);
+    g_devs.clear();
     return HC_PHMM_OK;
 }
 
@@ -945,112 +1524,101 @@ int hc_phmm_get_luts(float* pf, double* pd, float* mf, double* md)
     return HC_PHMM_OK;
 }
 
+int hc_phmm_submit_pairs(int64_t n, const int64_t* read_off, const int32_t* R, const int64_t* hap_off,
+                         const int32_t* H, const uint8_t* rs, const uint8_t* q, const uint8_t* ins,
+                         const uint8_t* del, const uint8_t* gcp, const uint8_t* hap, double* loglik,
+                         float* raw_f32, double* raw_f64, uint8_t* rescued, hc_phmm_job** job)
+{
+    if (!job) return fail(HC_PHMM_EINVAL, "null job");
+    *job = nullptr;
+    if (n < 0) return fail(HC_PHMM_EINVAL, "negative pair count");
+    if (!flat_args_ok(n, read_off, R, hap_off, H, rs, q, ins, del, gcp, hap))
+        return fail(HC_PHMM_EINVAL, "null input array");
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (n == 0) {
+        *job = new hc_phmm_job();
+        return HC_PHMM_OK;
+    }
+    Outputs o{loglik, raw_f32, raw_f64, rescued};
+    return submit_flat(flat_src(read_off, R, hap_off, H, rs, q, ins, del, gcp, hap), n, o, job);
+}
+
+int hc_phmm_submit_regions(const hc_phmm_region* regions, int32_t n_regions, hc_phmm_job** job)
+{
+    if (!job) return fail(HC_PHMM_EINVAL, "null job");
+    *job = nullptr;
+    RegionSet rs;
+    int rc = gather_regions(regions, n_regions, rs);
+    if (rc) return rc;
+    rc = ensure_init();
+    if (rc) return rc;
+    Src src;
+    src.reads = rs.reads.data();
+    src.haps = rs.haps.data();
+    return submit_blocks(src, rs.blocks, job);
+}
+
+int hc_phmm_job_ready(hc_phmm_job* job)
+{
+    if (!job) return fail(HC_PHMM_EINVAL, "null job");
+    for (Part* p : job->parts) {
+        (void)hipSetDevice(p->dev->ordinal);
+        const hipError_t e = hipEventQuery(p->done);
+        if (e == hipErrorNotReady) return 0;
+        if (e != hipSuccess) return fail(HC_PHMM_EHIP, std::string("device pass: ") + hipGetErrorString(e));
+    }
+    return 1;
+}
+
+int hc_phmm_collect(hc_phmm_job* job)
+{
+    if (!job) return fail(HC_PHMM_EINVAL, "null job");
+    return collect(job);
+}
+
 int hc_phmm_pairs_flat(int64_t n, const int64_t* read_off, const int32_t* R, const int64_t* hap_off,
                        const int32_t* H, const uint8_t* rs, const uint8_t* q, const uint8_t* ins,
                        const uint8_t* del, const uint8_t* gcp, const uint8_t* hap, double* loglik,
                        float* raw_f32, double* raw_f64, uint8_t* rescued)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
-    int rc = ensure_init(-1);
+    hc_phmm_job* job = nullptr;
+    const int rc = hc_phmm_submit_pairs(n, read_off, R, hap_off, H, rs, q, ins, del, gcp, hap, loglik, raw_f32,
+                                        raw_f64, rescued, &job);
     if (rc) return rc;
-    if (n == 0) return HC_PHMM_OK;
-    std::vector<ReadView> rv;
-    std::vector<HapView> hv;
-    std::vector<int32_t> idx;
-    rc = flat_views(n, read_off, R, hap_off, H, rs, q, ins, del, gcp, hap, rv, hv, idx);
-    if (rc) return rc;
-    hc_phmm_batch* b = nullptr;
-    rc = plan(rv, hv, n, idx.data(), idx.data(), true, &b);
-    if (rc) return rc;
-    rc = run_sync(b, loglik, raw_f32, raw_f64, rescued);
-    free_batch(b);
-    return rc;
+    return collect(job);
 }
 
-int hc_phmm_cross(const hc_phmm_read* reads, int32_t n_reads, const hc_phmm_hap* haps,
-                  int32_t n_haps, double* out)
+int hc_phmm_cross(const hc_phmm_read* reads, int32_t n_reads, const hc_phmm_hap* haps, int32_t n_haps, double* out)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
     if (n_reads < 0 || n_haps < 0) return fail(HC_PHMM_EINVAL, "negative count");
     if (n_reads == 0 || n_haps == 0) return HC_PHMM_OK;
     if (!reads || !haps || !out) return fail(HC_PHMM_EINVAL, "null argument");
-    int rc = ensure_init(-1);
+    hc_phmm_region g{reads, n_reads, haps, n_haps, out};
+    hc_phmm_job* job = nullptr;
+    const int rc = hc_phmm_submit_regions(&g, 1, &job);
     if (rc) return rc;
-    std::vector<ReadView> rv(n_reads);
-    std::vector<HapView> hv(n_haps);
-    for (int r = 0; r < n_reads; ++r)
-        rv[r] = ReadView{reads[r].length, (const uint8_t*)reads[r].bases, (const uint8_t*)reads[r].q,
-                         (const uint8_t*)reads[r].i, (const uint8_t*)reads[r].d, (const uint8_t*)reads[r].c};
-    for (int h = 0; h < n_haps; ++h) hv[h] = HapView{haps[h].length, (const uint8_t*)haps[h].bases};
-    const int64_t np = int64_t(n_reads) * n_haps;
-    std::vector<int32_t> pr(np), ph(np);
-    for (int64_t p = 0; p < np; ++p) {
-        pr[p] = int32_t(p / n_haps);   // read-major, intel_pairhmm.hpp:131-132
-        ph[p] = int32_t(p % n_haps);
-    }
-    hc_phmm_batch* b = nullptr;
-    rc = plan(rv, hv, np, pr.data(), ph.data(), true, &b);
-    if (rc) return rc;
-    rc = run_sync(b, out, nullptr, nullptr, nullptr);
-    free_batch(b);
-    return rc;
+    return collect(job);
 }
 
 int hc_phmm_cross_regions(const hc_phmm_region* regions, int32_t n_regions)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (n_regions < 0 || (n_regions > 0 && !regions)) return fail(HC_PHMM_EINVAL, "bad region list");
-    int rc = ensure_init(-1);
+    hc_phmm_job* job = nullptr;
+    const int rc = hc_phmm_submit_regions(regions, n_regions, &job);
     if (rc) return rc;
-    std::vector<ReadView> rv;
-    std::vector<HapView> hv;
-    std::vector<int32_t> pr, ph;
-    std::vector<int64_t> out_base;   // first pair of each region
-    for (int k = 0; k < n_regions; ++k) {
-        const hc_phmm_region& g = regions[k];
-        if (g.n_reads < 0 || g.n_haps < 0) return fail(HC_PHMM_EINVAL, "negative count in region");
-        out_base.push_back(int64_t(pr.size()));
-        if (g.n_reads == 0 || g.n_haps == 0) continue;
-        if (!g.reads || !g.haps || !g.out) return fail(HC_PHMM_EINVAL, "null pointer in region");
-        const int32_t r0 = int32_t(rv.size()), h0 = int32_t(hv.size());
-        for (int r = 0; r < g.n_reads; ++r)
-            rv.push_back(ReadView{g.reads[r].length, (const uint8_t*)g.reads[r].bases, (const uint8_t*)g.reads[r].q,
-                                  (const uint8_t*)g.reads[r].i, (const uint8_t*)g.reads[r].d,
-                                  (const uint8_t*)g.reads[r].c});
-        for (int h = 0; h < g.n_haps; ++h) hv.push_back(HapView{g.haps[h].length, (const uint8_t*)g.haps[h].bases});
-        for (int r = 0; r < g.n_reads; ++r)
-            for (int h = 0; h < g.n_haps; ++h) {
-                pr.push_back(r0 + r);
-                ph.push_back(h0 + h);
-            }
-    }
-    const int64_t np = int64_t(pr.size());
-    if (np == 0) return HC_PHMM_OK;
-    hc_phmm_batch* b = nullptr;
-    rc = plan(rv, hv, np, pr.data(), ph.data(), true, &b);
-    if (rc) return rc;
-    std::vector<double> all(np);
-    rc = run_sync(b, all.data(), nullptr, nullptr, nullptr);
-    free_batch(b);
-    if (rc) return rc;
-    for (int k = 0; k < n_regions; ++k) {
-        const hc_phmm_region& g = regions[k];
-        if (g.n_reads == 0 || g.n_haps == 0) continue;
-        std::memcpy(g.out, all.data() + out_base[k], sizeof(double) * size_t(g.n_reads) * g.n_haps);
-    }
-    return HC_PHMM_OK;
+    return collect(job);
 }
 
 int hc_phmm_compute_likelihoods(const hc_phmm_read* reads, int32_t n_reads, const hc_phmm_hap* haps,
                                 int32_t n_haps, double* out, uint8_t* keep, int32_t* n_kept)
 {
+    if (n_reads > 0 && (!keep || !n_kept)) return fail(HC_PHMM_EINVAL, "null keep/n_kept");
     int rc = hc_phmm_cross(reads, n_reads, haps, n_haps, out);
     if (rc) return rc;
-    if (n_reads > 0 && (!keep || !n_kept)) return fail(HC_PHMM_EINVAL, "null keep/n_kept");
     int kept = 0;
     // normalize_likelihoods_and_filter_poorly_modeled_reads, intel_pairhmm.hpp:24-46
     for (int r = 0; r < n_reads; ++r) {
-        double* row = out + size_t(r) * n_haps;
+        double* row = out + size_t(r) * size_t(n_haps);
         double best = n_haps ? row[0] : -INFINITY;
         for (int h = 1; h < n_haps; ++h)
             if (best < row[h]) best = row[h];
@@ -1065,94 +1633,155 @@ int hc_phmm_compute_likelihoods(const hc_phmm_read* reads, int32_t n_reads, cons
     return HC_PHMM_OK;
 }
 
+// ---- prepared batches (device-resident, one part per device slot)
+
 int hc_phmm_batch_create(int64_t n, const int64_t* read_off, const int32_t* R, const int64_t* hap_off,
                          const int32_t* H, const uint8_t* rs, const uint8_t* q, const uint8_t* ins,
                          const uint8_t* del, const uint8_t* gcp, const uint8_t* hap, hc_phmm_batch** out)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
     if (!out) return fail(HC_PHMM_EINVAL, "null out");
-    int rc = ensure_init(-1);
+    *out = nullptr;
+    if (n < 0) return fail(HC_PHMM_EINVAL, "negative pair count");
+    if (!flat_args_ok(n, read_off, R, hap_off, H, rs, q, ins, del, gcp, hap))
+        return fail(HC_PHMM_EINVAL, "null input array");
+    int rc = ensure_init();
     if (rc) return rc;
-    std::vector<ReadView> rv;
-    std::vector<HapView> hv;
-    std::vector<int32_t> idx;
-    rc = flat_views(n, read_off, R, hap_off, H, rs, q, ins, del, gcp, hap, rv, hv, idx);
-    if (rc) return rc;
-    return plan(rv, hv, n, idx.data(), idx.data(), false, out);
+    const Src src = flat_src(read_off, R, hap_off, H, rs, q, ins, del, gcp, hap);
+    std::vector<int64_t> pre;
+    prefix_sum(n, pre, [&](int64_t p) { return int64_t(std::max(0, R[p])) * std::max(0, H[p]); });
+    const int G = int(g_devs.size());
+    const std::vector<int64_t> cut = equal_cuts(pre, G);
+    auto* B = new hc_phmm_batch();
+    B->n = n;
+    for (int j = 0; j < G; ++j) {
+        if (j > 0 && cut[size_t(j)] == cut[size_t(j) + 1]) continue;
+        PartSpec s;
+        s.flat = true;
+        s.lo = cut[size_t(j)];
+        s.hi = cut[size_t(j) + 1];
+        Device& d = *g_devs[size_t(j)];
+        Part* p = nullptr;
+        rc = hipSetDevice(d.ordinal) == hipSuccess ? plan_part(d, src, s, nullptr, false, &p)
+                                                   : fail(HC_PHMM_EHIP, "hipSetDevice");
+        if (rc) {
+            for (Part* x : B->parts) free_part(x);
+            delete B;
+            return rc;
+        }
+        B->parts.push_back(p);
+    }
+    *out = B;
+    return HC_PHMM_OK;
 }
 
 int hc_phmm_batch_run(hc_phmm_batch* b, void* stream)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
     if (!b) return fail(HC_PHMM_EINVAL, "null batch");
-    if (!g_eng.ready) return fail(HC_PHMM_ENODEV, "not initialised");
-    return run(b, static_cast<hipStream_t>(stream));
+    if (stream && b->parts.size() > 1)
+        return fail(HC_PHMM_EINVAL, "a caller stream selects one device; this batch spans several");
+    for (Part* p : b->parts) {
+        HIP_TRY(hipSetDevice(p->dev->ordinal));
+        const int rc = run_part(p, stream ? static_cast<hipStream_t>(stream) : p->dev->stream);
+        if (rc) return rc;
+    }
+    return HC_PHMM_OK;
 }
 
-int hc_phmm_batch_results(hc_phmm_batch* b, double* loglik, float* raw_f32, double* raw_f64,
-                          uint8_t* rescued)
+int hc_phmm_batch_results(hc_phmm_batch* b, double* loglik, float* raw_f32, double* raw_f64, uint8_t* rescued)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
     if (!b) return fail(HC_PHMM_EINVAL, "null batch");
-    return results(b, loglik, raw_f32, raw_f64, rescued);
+    const Outputs o{loglik, raw_f32, raw_f64, rescued};
+    for (Part* p : b->parts) {
+        if (!p->ran) return fail(HC_PHMM_EINVAL, "batch has not been run");
+        if (p->n == 0) continue;
+        HIP_TRY(hipSetDevice(p->dev->ordinal));
+        HIP_TRY(hipStreamSynchronize(p->last_stream));
+        std::vector<char> host(p->res_bytes);
+        const size_t n = size_t(p->n);
+        HIP_TRY(hipMemcpy(host.data(), p->d_raw32, sizeof(float) * n, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(host.data() + p->res_o64, p->d_raw64, sizeof(double) * n, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(host.data() + p->res_ofl, p->d_flag, n, hipMemcpyDeviceToHost));
+        finish_part(*p, reinterpret_cast<const float*>(host.data()),
+                    reinterpret_cast<const double*>(host.data() + p->res_o64),
+                    reinterpret_cast<const uint8_t*>(host.data() + p->res_ofl), o);
+    }
+    return HC_PHMM_OK;
 }
 
 int hc_phmm_batch_device_results(hc_phmm_batch* b, void** raw_f32, void** raw_f64, void** rescued)
 {
     if (!b) return fail(HC_PHMM_EINVAL, "null batch");
-    if (raw_f32) *raw_f32 = b->d_raw32;
-    if (raw_f64) *raw_f64 = b->d_raw64;
-    if (rescued) *rescued = b->d_flag;
+    if (b->parts.size() != 1) return fail(HC_PHMM_EINVAL, "device results of a batch split over several devices");
+    Part* p = b->parts[0];
+    if (raw_f32) *raw_f32 = p->d_raw32;
+    if (raw_f64) *raw_f64 = p->d_raw64;
+    if (rescued) *rescued = p->d_flag;
     return HC_PHMM_OK;
 }
 
 int hc_phmm_batch_bind_outputs(hc_phmm_batch* b, void* raw_f32, void* raw_f64, void* rescued)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
     if (!b) return fail(HC_PHMM_EINVAL, "null batch");
-    b->d_raw32 = raw_f32 ? static_cast<float*>(raw_f32) : b->own_raw32;
-    b->d_raw64 = raw_f64 ? static_cast<double*>(raw_f64) : b->own_raw64;
-    b->d_flag = rescued ? static_cast<uint8_t*>(rescued) : b->own_flag;
+    if (b->parts.size() != 1) return fail(HC_PHMM_EINVAL, "bind_outputs on a batch split over several devices");
+    Part* p = b->parts[0];
+    p->d_raw32 = raw_f32 ? static_cast<float*>(raw_f32) : p->own_raw32;
+    p->d_raw64 = raw_f64 ? static_cast<double*>(raw_f64) : p->own_raw64;
+    p->d_flag = rescued ? static_cast<uint8_t*>(rescued) : p->own_flag;
     return HC_PHMM_OK;
 }
 
 int hc_phmm_batch_stats(hc_phmm_batch* b, hc_phmm_stats* st)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
     if (!b || !st) return fail(HC_PHMM_EINVAL, "null argument");
     std::memset(st, 0, sizeof(*st));
     st->n_pairs = b->n;
-    st->cells = b->cells;
-    st->n_launch_waves = b->launch_waves;
-    st->n_lane_pairs = b->n_lane;
-    st->n_seg_waves = b->n_seg_waves;
-    if (b->ran && b->ev_used > 0) {
-        HIP_TRY(hipStreamSynchronize(b->last_stream));
-        double sa = 0, sc = 0;
-        for (size_t k = 0; k < b->ev_used; ++k) {
-            float a = 0, c = 0;
-            HIP_TRY(hipEventSynchronize(b->ev_pool[k][2]));
-            HIP_TRY(hipEventElapsedTime(&a, b->ev_pool[k][0], b->ev_pool[k][1]));
-            HIP_TRY(hipEventElapsedTime(&c, b->ev_pool[k][1], b->ev_pool[k][2]));
-            sa += a;
-            sc += c;
+    st->n_devices = int64_t(b->parts.size());
+    for (Part* p : b->parts) {
+        HIP_TRY(hipSetDevice(p->dev->ordinal));
+        st->cells += p->cells;
+        st->n_launch_waves += p->launch_waves;
+        st->n_lane_pairs += p->n_lane;
+        st->n_seg_waves += p->n_seg_waves;
+        st->upload_bytes += int64_t(p->upload_bytes);
+        if (p->pack_ev[0]) {
+            float pk = 0;
+            HIP_TRY(hipEventSynchronize(p->pack_ev[1]));
+            HIP_TRY(hipEventElapsedTime(&pk, p->pack_ev[0], p->pack_ev[1]));
+            st->pack_ms = std::max(st->pack_ms, double(pk));
         }
-        st->n_runs = int64_t(b->ev_used);
-        st->kernel_ms_f32 = sa / double(b->ev_used);
-        st->kernel_ms_f64 = sc / double(b->ev_used);
-        st->run_ms = st->kernel_ms_f32 + st->kernel_ms_f64;
-        b->ev_used = 0;
-        int cnt = 0;
-        HIP_TRY(hipMemcpy(&cnt, b->d_count + (b->parity ^ 1), sizeof(int), hipMemcpyDeviceToHost));
-        st->n_rescued = cnt;
+        if (p->ran && p->ev_used > 0) {
+            HIP_TRY(hipStreamSynchronize(p->last_stream));
+            double sa = 0, sc = 0;
+            for (size_t k = 0; k < p->ev_used; ++k) {
+                float a = 0, c = 0;
+                HIP_TRY(hipEventSynchronize(p->ev_pool[k][2]));
+                HIP_TRY(hipEventElapsedTime(&a, p->ev_pool[k][0], p->ev_pool[k][1]));
+                HIP_TRY(hipEventElapsedTime(&c, p->ev_pool[k][1], p->ev_pool[k][2]));
+                sa += a;
+                sc += c;
+            }
+            st->n_runs = std::max(st->n_runs, int64_t(p->ev_used));
+            st->kernel_ms_f32 = std::max(st->kernel_ms_f32, sa / double(p->ev_used));
+            st->kernel_ms_f64 = std::max(st->kernel_ms_f64, sc / double(p->ev_used));
+            st->run_ms = std::max(st->run_ms, (sa + sc) / double(p->ev_used));
+            p->ev_used = 0;
+            int cnt = 0;
+            HIP_TRY(hipMemcpy(&cnt, p->d_count + (p->parity ^ 1), sizeof(int), hipMemcpyDeviceToHost));
+            st->n_rescued += cnt;
+        }
     }
     return HC_PHMM_OK;
 }
 
 int hc_phmm_batch_destroy(hc_phmm_batch* b)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
-    free_batch(b);
+    if (!b) return HC_PHMM_OK;
+    for (Part* p : b->parts) {
+        (void)hipSetDevice(p->dev->ordinal);
+        if (p->last_stream) (void)hipStreamSynchronize(p->last_stream);
+        free_part(p);
+    }
+    delete b;
     return HC_PHMM_OK;
 }
 
@@ -1193,7 +1822,7 @@ bool calculate(Batch& batch)
     static_assert(sizeof(Read) == sizeof(hc_phmm_read), "Read layout");
     static_assert(sizeof(Haplotype) == sizeof(hc_phmm_hap), "Haplotype layout");
     if (batch.num_reads < 0 || batch.num_haps < 0 || !batch.results) return false;
-    std::vector<double> out(size_t(batch.num_reads) * size_t(batch.num_haps));
+    std::vector<double> out(static_cast<size_t>(batch.num_reads) * size_t(batch.num_haps));
     const int rc = hc_phmm_cross(reinterpret_cast<const hc_phmm_read*>(batch.reads), batch.num_reads,
                                  reinterpret_cast<const hc_phmm_hap*>(batch.haps), batch.num_haps, out.data());
     if (rc != HC_PHMM_OK) return false;

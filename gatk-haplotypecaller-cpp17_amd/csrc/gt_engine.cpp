@@ -24,6 +24,8 @@
 
 namespace hcphmm {
 void set_last_error(const std::string& msg);
+int primary_device();
+void gt_release();
 }
 
 using namespace hcgt;
@@ -51,11 +53,13 @@ int fail(int code, const std::string& msg)
             return fail(HC_PHMM_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+// Runs on the engine's first device slot, made current on the calling thread.
 int ensure_init()
 {
-    if (g_stream) return HC_PHMM_OK;
     const int rc = hc_phmm_init(0, -1);
     if (rc != HC_PHMM_OK) return rc;
+    HIP_TRY(hipSetDevice(hcphmm::primary_device()));
+    if (g_stream) return HC_PHMM_OK;
     HIP_TRY(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
     HIP_TRY(hipMalloc(&g_jac, sizeof(double) * kJacobianLen));
     static_assert(sizeof(kMathJacobianBits) == sizeof(double) * kJacobianLen, "table length");
@@ -201,4 +205,21 @@ extern "C" int hc_gt_genotype_sites(const hc_gt_site* sites, int32_t n_sites)
     if (rc) return rc;
     if (n_sites == 0) return HC_PHMM_OK;
     return run(sites, n_sites);
+}
+
+// Called by hc_phmm_shutdown.
+void hcphmm::gt_release()
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_stream) return;
+    (void)hipStreamSynchronize(g_stream);
+    if (g_jac) (void)hipFree(g_jac);
+    if (g_dev) (void)hipFree(g_dev);
+    if (g_host) (void)hipHostFree(g_host);
+    (void)hipStreamDestroy(g_stream);
+    g_stream = nullptr;
+    g_jac = nullptr;
+    g_dev = nullptr;
+    g_host = nullptr;
+    g_dev_bytes = g_host_bytes = 0;
 }

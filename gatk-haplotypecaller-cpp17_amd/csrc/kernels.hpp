@@ -5,14 +5,14 @@
 
 namespace hcphmm {
 
-// One row of a read, packed into 32 bits (built on the host, engine.cpp):
+// One row of a read, packed into 32 bits (built on the device, pack_kernels.hip):
 //   bits  0- 6  q  (base quality byte & 127)
 //   bits  7-13  i  (insertion GOP byte & 127)
 //   bits 14-20  d  (deletion GOP byte & 127)
 //   bits 21-27  c  (gap continuation byte & 127)
 //   bits 28-30  read base code, ConvertChar (pairhmm_common.h:26-44): A0 C1 T2 G3 N4
 //   bit  31     first row of a read only: the read's gap qualities are constant
-//               (set on the device by mark_cg_kernel)
+//               (found on the host while staging, set by pack_reads_kernel)
 __host__ __device__ inline uint32_t pack_row(int q, int i, int d, int c, int code)
 {
     return uint32_t(q & 127) | (uint32_t(i & 127) << 7) | (uint32_t(d & 127) << 14) |
@@ -95,6 +95,7 @@ hipError_t launch_lane_f32(int variant, const LaneArgs& a, hipStream_t s);
 hipError_t launch_lane_seg_f32(const LaneArgs& a, hipStream_t s);
 bool seg_width_ok(int bc);
 constexpr int kSegMaxBC = 64;
+constexpr int kSegMinBC = 16;   // narrowest compiled fp32 block width
 
 // fp64 rescue pass in column-segmented form, planned on the device
 // (lane_kernel.hip rescue_plan_kernel). Two width tiers: bc[0] for the whole
@@ -132,13 +133,13 @@ hipError_t launch_diag_f64(int W, const DiagArgs& a, int grid, hipStream_t s);
 size_t diag_lds_bytes(int W, int ring_len, bool f64);
 hipError_t configure_kernels();   // raise the dynamic-LDS limit once
 
-// Device packing (pack_kernels.hip). raw: 5 byte planes (bases, q, i, d, c) of
-// `stride` bytes (multiple of 16, 16-B aligned); haps: {byte offset, H, table
-// word offset, 0}; tab_row0: first table row of each hap (prefix sum).
-hipError_t launch_pack_rows(const uint8_t* raw, long long nrows, long long stride, uint32_t* rows,
-                            hipStream_t s);
-hipError_t launch_mark_cg(uint32_t* rows, const int2* reads, int nreads, hipStream_t s);
-hipError_t launch_hap_tables(const uint8_t* hap_bytes, const int4* haps, int nhaps, const long long* tab_row0,
-                             long long ntab_rows, uint32_t* hapw, hipStream_t s);
+// Device packing (pack_kernels.hip). Reads: `bases` / `quals` one byte per
+// row (row k of read r at rdesc[r].x + k); rdesc {row offset, length, constant
+// gap triple i | d << 7 | c << 14 or -1, offset into the i/d/c planes `gaps`
+// (3 planes of gap_stride bytes) when the read's gap qualities vary}.
+// Haps: {byte offset, H, table word offset, 0}; tables as hap_table_words.
+hipError_t launch_pack_reads(const uint8_t* bases, const uint8_t* quals, const uint8_t* gaps, long long gap_stride,
+                             const int4* rdesc, int nreads, uint32_t* rows, hipStream_t s);
+hipError_t launch_hap_tables(const uint8_t* hap_bytes, const int4* haps, int nhaps, uint32_t* hapw, hipStream_t s);
 
 }  // namespace hcphmm

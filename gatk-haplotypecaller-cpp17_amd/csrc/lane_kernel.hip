@@ -154,7 +154,7 @@ __device__ __forceinline__ LaneCtx pair_ctx(const PairDesc* pairs, const uint32_
     return LaneCtx{rows + pd.x, hapw + pd.z, pd.y, pd.w};
 }
 
-// Constant-gap tag of a read: bit 31 of its first row word (mark_cg_kernel).
+// Constant-gap tag of a read: bit 31 of its first row word (pack_reads_kernel).
 // EQ additionally needs insertion == deletion gap quality.
 __device__ __forceinline__ bool read_cg(uint32_t w1) { return (w1 >> 31) != 0; }
 __device__ __forceinline__ bool read_eq(uint32_t w1) { return read_cg(w1) && row_i(w1) == row_d(w1); }

@@ -26,6 +26,8 @@
 
 namespace hcphmm {
 void set_last_error(const std::string& msg);
+int primary_device();
+void sw_release();
 }
 
 using namespace hcsw;
@@ -58,12 +60,15 @@ int fail(int code, const std::string& msg)
             return fail(HC_SW_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+// The aligner runs on the engine's first device slot (hc_phmm_init /
+// hc_phmm_init_devices); every entry point makes that device current on the
+// calling thread.
 int ensure_init(int device)
 {
-    if (g_stream) return HC_SW_OK;
-    const int rc = hc_phmm_init(0, device);   // device selection + gfx950 check
+    const int rc = hc_phmm_init(0, device);   // device selection + gfx950 check (no-op once initialised)
     if (rc != HC_PHMM_OK) return rc;
-    HIP_TRY(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
+    HIP_TRY(hipSetDevice(hcphmm::primary_device()));
+    if (!g_stream) HIP_TRY(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
     return HC_SW_OK;
 }
 
@@ -91,10 +96,23 @@ bool fast_ok(const hc_sw_params& p, int overhang, int n1max, int n2max)
     return v < (int64_t(1) << 28);
 }
 
+// IntelSWAligner::is_all_match (intel_smithwaterman.hpp:47-58): equal lengths
+// and at most MINIMAL_MISMATCH_TO_TOLERANCE = 2 mismatching bytes.
+bool all_match(const uint8_t* ref, const uint8_t* alt, int n1, int n2)
+{
+    if (n1 != n2) return false;
+    int mm = 0;
+    for (int i = 0; mm <= 2 && i < n1; ++i) mm += ref[i] != alt[i];
+    return mm <= 2;
+}
+
 }  // namespace
 
 struct hc_sw_batch {
-    int64_t n = 0;
+    int64_t n = 0;                  // caller's pairs
+    int64_t nd = 0;                 // pairs on the device (the rest: host all-match shortcut)
+    std::vector<int64_t> dev_ids;   // caller index of device pair d
+    std::vector<std::pair<int64_t, int32_t>> host_sc;   // {caller index, length}: shortcut answered on the host
     int n1max = 0, n2max = 0;
     int64_t cells = 0;
     hc_sw_params params{};
@@ -173,17 +191,27 @@ int create(int64_t n, const int64_t* ref_off, const int32_t* ref_len, const uint
     b->overhang = overhang;
     b->shortcut = shortcut ? 1 : 0;
 
-    std::vector<SwPair> pairs(static_cast<size_t>(n));
+    std::vector<SwPair> pairs;
+    pairs.reserve(static_cast<size_t>(n));
     int64_t ref_ext = 0, alt_ext = 0, bt_total = 0, el_total = 0;
     for (int64_t k = 0; k < n; ++k) {
         const int n1 = ref_len[k], n2 = alt_len[k];
-        if (n1 < 1 || n2 < 1 || n1 > HC_SW_MAX_LEN1 || n2 > HC_SW_MAX_LEN2 || ref_off[k] < 0 || alt_off[k] < 0) {
+        const bool in_range = n1 >= 1 && n2 >= 1 && n1 <= HC_SW_MAX_LEN1 && n2 <= HC_SW_MAX_LEN2;
+        if (n1 >= 1 && n2 >= 1 && ref_off[k] >= 0 && alt_off[k] >= 0 && !in_range && shortcut &&
+            all_match(refs + ref_off[k], alts + alt_off[k], n1, n2)) {
+            // IntelSWAligner::align answers an equal-length pair with <= 2
+            // mismatches before runSWOnePairBT_avx2 sees it (intel_smithwaterman.hpp:
+            // 36-37), so the aligner's length limit does not apply to it.
+            b->host_sc.emplace_back(k, n1);
+            continue;
+        }
+        if (!in_range || ref_off[k] < 0 || alt_off[k] < 0) {
             free_batch(b);
             return fail(HC_SW_EINVAL, "pair " + std::to_string(k) + ": sequence length out of range [1, " +
                                           std::to_string(HC_SW_MAX_LEN1) + "] x [1, " +
                                           std::to_string(HC_SW_MAX_LEN2) + "] or negative offset");
         }
-        SwPair& P = pairs[size_t(k)];
+        SwPair P;
         P.ref_off = ref_off[k];
         P.alt_off = alt_off[k];
         P.n1 = n1;
@@ -197,7 +225,11 @@ int create(int64_t n, const int64_t* ref_off, const int32_t* ref_len, const uint
         b->n1max = std::max(b->n1max, n1);
         b->n2max = std::max(b->n2max, n2);
         b->cells += int64_t(n1) * n2;
+        pairs.push_back(P);
+        b->dev_ids.push_back(k);
     }
+    n = int64_t(pairs.size());
+    b->nd = n;
     // Longest pairs first: the tail of the launch is made of short waves.
     std::vector<int32_t> order(static_cast<size_t>(n));
     std::iota(order.begin(), order.end(), 0);
@@ -283,14 +315,14 @@ int create(int64_t n, const int64_t* ref_off, const int32_t* ref_len, const uint
 
 int run(hc_sw_batch* b, hipStream_t s)
 {
-    if (b->n == 0) {
+    if (b->nd == 0) {
         b->ran = true;
         return HC_SW_OK;
     }
     SwDpArgs d{};
     d.pairs = b->pairs;
     d.order = b->order;
-    d.n = int(b->n);
+    d.n = int(b->nd);
     d.refs = b->refs;
     d.alts = b->alts;
     d.bt = b->bt;
@@ -309,7 +341,7 @@ int run(hc_sw_batch* b, hipStream_t s)
     t.pairs = b->pairs;
     t.res = b->res;
     t.bt = b->bt;
-    t.n = int(b->n);
+    t.n = int(b->nd);
     t.overhang = b->overhang;
     t.elems = b->elems;
     t.slots = b->slots;
@@ -336,62 +368,76 @@ int run(hc_sw_batch* b, hipStream_t s)
 int results(hc_sw_batch* b, int32_t* offsets, char* cigars, int32_t stride, int32_t* scores)
 {
     if (!b->ran) return fail(HC_SW_EINVAL, "batch has not run");
-    const int64_t n = b->n;
-    if (n == 0) return HC_SW_OK;
+    if (b->n == 0) return HC_SW_OK;
     if (!offsets || !cigars || stride < 2) return fail(HC_SW_EINVAL, "null output / stride < 2");
-    // [slots | n_elems | offsets] are contiguous on the device: one D2H.
-    std::vector<char> tail_vec;
-    char* tail = nullptr;
-    if (!b->owns && g_ws.host_bytes >= b->tail_bytes) {
-        tail = g_ws.host;
-    } else {
-        tail_vec.resize(b->tail_bytes);
-        tail = tail_vec.data();
-    }
-    HIP_TRY(hipMemcpy(tail, b->dev + b->tail_off, b->tail_bytes, hipMemcpyDeviceToHost));
-    const uint16_t* slotv = reinterpret_cast<const uint16_t*>(tail);
-    const int32_t* cntv = reinterpret_cast<const int32_t*>(tail + (reinterpret_cast<char*>(b->n_elems) - (b->dev + b->tail_off)));
-    const int32_t* offv = reinterpret_cast<const int32_t*>(tail + (reinterpret_cast<char*>(b->offsets) - (b->dev + b->tail_off)));
-    std::memcpy(offsets, offv, sizeof(int32_t) * size_t(n));
-    std::vector<int32_t> cnt(cntv, cntv + n);
-    // Pairs with more than kSlotElems elements: their whole scratch (rare).
-    std::vector<uint32_t> big;
-    std::vector<size_t> big_at(static_cast<size_t>(n), SIZE_MAX);
-    std::vector<SwPair> P;
-    for (int64_t k = 0; k < n; ++k) {
-        if (cnt[size_t(k)] <= kSlotElems) continue;
-        if (P.empty()) {
-            P.resize(size_t(n));
-            HIP_TRY(hipMemcpy(P.data(), b->pairs, sizeof(SwPair) * size_t(n), hipMemcpyDeviceToHost));
-        }
-        big_at[size_t(k)] = big.size();
-        big.resize(big.size() + size_t(cnt[size_t(k)]));
-        HIP_TRY(hipMemcpy(big.data() + big_at[size_t(k)], b->elems + P[size_t(k)].el_off,
-                          sizeof(uint32_t) * size_t(cnt[size_t(k)]), hipMemcpyDeviceToHost));
-    }
-    if (scores) {
-        std::vector<SwResult> r(static_cast<size_t>(n));
-        HIP_TRY(hipMemcpy(r.data(), b->res, sizeof(SwResult) * size_t(n), hipMemcpyDeviceToHost));
-        for (int64_t k = 0; k < n; ++k) scores[k] = r[size_t(k)].score;
-    }
     bool too_long = false;
-    for (int64_t k = 0; k < n; ++k) {
+    // Over-length pairs the all-match shortcut answered on the host: {0, <n>M}
+    // (intel_smithwaterman.hpp:36-37).
+    for (const auto& [k, len] : b->host_sc) {
         char* o = cigars + size_t(k) * size_t(stride);
-        int pos = 0;
-        // Elements are in traceback order: print them back to front (:388-413).
-        for (int e = cnt[size_t(k)] - 1; e >= 0 && pos >= 0; --e) {
-            const uint32_t v = cnt[size_t(k)] <= kSlotElems ? uint32_t(slotv[size_t(k) * kSlotElems + size_t(e)])
-                                                             : big[big_at[size_t(k)] + size_t(e)];
-            const int op = int(v & 15);
-            const char ch = op == kOpM ? 'M' : op == kOpI ? 'I' : op == kOpD ? 'D' : op == kOpS ? 'S' : 'R';
-            const int w = std::snprintf(o + pos, size_t(stride - pos), "%u%c", v >> 4, ch);
-            pos = (w < 0 || pos + w >= stride) ? -1 : pos + w;
-        }
-        if (pos < 0) {
+        offsets[k] = 0;
+        if (scores) scores[k] = 0;
+        const int w = std::snprintf(o, size_t(stride), "%dM", len);
+        if (w < 0 || w >= stride) {
             too_long = true;
             o[0] = 0;
-        } else if (cnt[size_t(k)] == 0) {
-            o[0] = 0;
+        }
+    }
+    const int64_t n = b->nd;   // device pairs; caller index b->dev_ids[k]
+    if (n > 0) {
+        // [slots | n_elems | offsets] are contiguous on the device: one D2H.
+        std::vector<char> tail_vec;
+        char* tail = nullptr;
+        if (!b->owns && g_ws.host_bytes >= b->tail_bytes) {
+            tail = g_ws.host;
+        } else {
+            tail_vec.resize(b->tail_bytes);
+            tail = tail_vec.data();
+        }
+        HIP_TRY(hipMemcpy(tail, b->dev + b->tail_off, b->tail_bytes, hipMemcpyDeviceToHost));
+        const uint16_t* slotv = reinterpret_cast<const uint16_t*>(tail);
+        const int32_t* cntv = reinterpret_cast<const int32_t*>(tail + (reinterpret_cast<char*>(b->n_elems) - (b->dev + b->tail_off)));
+        const int32_t* offv = reinterpret_cast<const int32_t*>(tail + (reinterpret_cast<char*>(b->offsets) - (b->dev + b->tail_off)));
+        for (int64_t k = 0; k < n; ++k) offsets[b->dev_ids[size_t(k)]] = offv[k];
+        std::vector<int32_t> cnt(cntv, cntv + n);
+        // Pairs with more than kSlotElems elements: their whole scratch (rare).
+        std::vector<uint32_t> big;
+        std::vector<size_t> big_at(static_cast<size_t>(n), SIZE_MAX);
+        std::vector<SwPair> P;
+        for (int64_t k = 0; k < n; ++k) {
+            if (cnt[size_t(k)] <= kSlotElems) continue;
+            if (P.empty()) {
+                P.resize(size_t(n));
+                HIP_TRY(hipMemcpy(P.data(), b->pairs, sizeof(SwPair) * size_t(n), hipMemcpyDeviceToHost));
+            }
+            big_at[size_t(k)] = big.size();
+            big.resize(big.size() + size_t(cnt[size_t(k)]));
+            HIP_TRY(hipMemcpy(big.data() + big_at[size_t(k)], b->elems + P[size_t(k)].el_off,
+                              sizeof(uint32_t) * size_t(cnt[size_t(k)]), hipMemcpyDeviceToHost));
+        }
+        if (scores) {
+            std::vector<SwResult> r(static_cast<size_t>(n));
+            HIP_TRY(hipMemcpy(r.data(), b->res, sizeof(SwResult) * size_t(n), hipMemcpyDeviceToHost));
+            for (int64_t k = 0; k < n; ++k) scores[b->dev_ids[size_t(k)]] = r[size_t(k)].score;
+        }
+        for (int64_t k = 0; k < n; ++k) {
+            char* o = cigars + size_t(b->dev_ids[size_t(k)]) * size_t(stride);
+            int pos = 0;
+            // Elements are in traceback order: print them back to front (:388-413).
+            for (int e = cnt[size_t(k)] - 1; e >= 0 && pos >= 0; --e) {
+                const uint32_t v = cnt[size_t(k)] <= kSlotElems ? uint32_t(slotv[size_t(k) * kSlotElems + size_t(e)])
+                                                                 : big[big_at[size_t(k)] + size_t(e)];
+                const int op = int(v & 15);
+                const char ch = op == kOpM ? 'M' : op == kOpI ? 'I' : op == kOpD ? 'D' : op == kOpS ? 'S' : 'R';
+                const int w = std::snprintf(o + pos, size_t(stride - pos), "%u%c", v >> 4, ch);
+                pos = (w < 0 || pos + w >= stride) ? -1 : pos + w;
+            }
+            if (pos < 0) {
+                too_long = true;
+                o[0] = 0;
+            } else if (cnt[size_t(k)] == 0) {
+                o[0] = 0;
+            }
         }
     }
     if (too_long) return fail(HC_SW_ERANGE, "a CIGAR does not fit in the stride");
@@ -422,6 +468,8 @@ int hc_sw_batch_run(hc_sw_batch* b, void* stream)
 {
     std::lock_guard<std::mutex> lk(g_mu);
     if (!b) return fail(HC_SW_EINVAL, "null batch");
+    const int rc = ensure_init(-1);
+    if (rc) return rc;
     return run(b, stream ? static_cast<hipStream_t>(stream) : g_stream);
 }
 
@@ -429,6 +477,8 @@ int hc_sw_batch_results(hc_sw_batch* b, int32_t* offsets, char* cigars, int32_t 
 {
     std::lock_guard<std::mutex> lk(g_mu);
     if (!b) return fail(HC_SW_EINVAL, "null batch");
+    const int rc = ensure_init(-1);
+    if (rc) return rc;
     return results(b, offsets, cigars, stride, scores);
 }
 
@@ -436,18 +486,21 @@ int hc_sw_batch_stats(hc_sw_batch* b, hc_sw_stats* st)
 {
     std::lock_guard<std::mutex> lk(g_mu);
     if (!b || !st) return fail(HC_SW_EINVAL, "null batch / stats");
+    const int rc = ensure_init(-1);
+    if (rc) return rc;
     st->n_pairs = b->n;
     st->cells = b->cells;
-    st->n_shortcut = 0;
-    if (b->ran && b->n) {
-        std::vector<SwResult> r(size_t(b->n));
-        HIP_TRY(hipMemcpy(r.data(), b->res, sizeof(SwResult) * size_t(b->n), hipMemcpyDeviceToHost));
-        std::vector<SwPair> P(static_cast<size_t>(b->n));
-        HIP_TRY(hipMemcpy(P.data(), b->pairs, sizeof(SwPair) * size_t(b->n), hipMemcpyDeviceToHost));
+    st->n_shortcut = int64_t(b->host_sc.size());
+    if (b->ran && b->nd) {
+        const size_t nd = size_t(b->nd);
+        std::vector<SwResult> r(nd);
+        HIP_TRY(hipMemcpy(r.data(), b->res, sizeof(SwResult) * nd, hipMemcpyDeviceToHost));
+        std::vector<SwPair> P(nd);
+        HIP_TRY(hipMemcpy(P.data(), b->pairs, sizeof(SwPair) * nd, hipMemcpyDeviceToHost));
         st->cells = 0;
-        for (int64_t k = 0; k < b->n; ++k) {
-            if (r[size_t(k)].shortcut) ++st->n_shortcut;
-            else st->cells += int64_t(P[size_t(k)].n1) * P[size_t(k)].n2;
+        for (size_t k = 0; k < nd; ++k) {
+            if (r[k].shortcut) ++st->n_shortcut;
+            else st->cells += int64_t(P[k].n1) * P[k].n2;
         }
     }
     const double k = b->n_runs ? 1.0 / double(b->n_runs) : 0.0;
@@ -484,3 +537,19 @@ int hc_sw_align_flat(int64_t n, const int64_t* ref_off, const int32_t* ref_len, 
 }
 
 }  // extern "C"
+
+// Called by hc_phmm_shutdown: the next call re-creates the stream and workspace
+// on whatever device the engine is then initialised on.
+void hcphmm::sw_release()
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_stream) return;
+    (void)hipStreamSynchronize(g_stream);
+    if (g_ws.dev) (void)hipFree(g_ws.dev);
+    if (g_ws.host) (void)hipHostFree(g_ws.host);
+    for (auto& e : g_ws.ev)
+        if (e) (void)hipEventDestroy(e);
+    g_ws = Workspace{};
+    (void)hipStreamDestroy(g_stream);
+    g_stream = nullptr;
+}

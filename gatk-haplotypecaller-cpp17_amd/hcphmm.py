@@ -13,6 +13,10 @@ Names follow the reference's PairHMM interface
 * :func:`cross` — computeLikelihoodsNative (:115-152) without normalisation.
 * :func:`pairs` — the same per-pair computation over independent pairs.
 * :class:`Batch` — plan (pack + upload) once, run the device pass many times.
+* :func:`submit_pairs` / :func:`submit_regions` + :meth:`Job.collect` — the
+  asynchronous calls: host planning of the next batch overlaps the device pass.
+* :func:`init_devices` — one process, several device slots (each call is
+  split by cells over them).
 """
 from __future__ import annotations
 
@@ -64,7 +68,8 @@ class Stats(C.Structure):
     _fields_ = [("n_pairs", C.c_int64), ("cells", C.c_int64), ("n_rescued", C.c_int64),
                 ("kernel_ms_f32", C.c_double), ("kernel_ms_f64", C.c_double),
                 ("run_ms", C.c_double), ("n_launch_waves", C.c_int64), ("n_runs", C.c_int64),
-                ("n_lane_pairs", C.c_int64), ("n_seg_waves", C.c_int64)]
+                ("n_lane_pairs", C.c_int64), ("n_seg_waves", C.c_int64), ("n_devices", C.c_int64),
+                ("pack_ms", C.c_double), ("upload_bytes", C.c_int64)]
 
 
 def build() -> None:
@@ -83,6 +88,12 @@ def lib():
         raise PairHMMError(ENODEV, f"{LIB_PATH} missing: run `make -C {HERE}` (no fallback path exists)")
     L = C.CDLL(LIB_PATH)
     L.hc_phmm_init.argtypes = [C.c_uint32, C.c_int]
+    L.hc_phmm_init_devices.argtypes = [C.c_uint32, _i32p, C.c_int32]
+    L.hc_phmm_submit_pairs.argtypes = [C.c_int64, _i64p, _i32p, _i64p, _i32p] + [_u8p] * 6 + \
+        [_f64p, _f32p, _f64p, _u8p, C.POINTER(C.c_void_p)]
+    L.hc_phmm_submit_regions.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]
+    L.hc_phmm_job_ready.argtypes = [C.c_void_p]
+    L.hc_phmm_collect.argtypes = [C.c_void_p]
     L.hc_phmm_last_error.restype = C.c_char_p
     flat = [C.c_int64, _i64p, _i32p, _i64p, _i32p] + [_u8p] * 6
     L.hc_phmm_pairs_flat.argtypes = flat + [_f64p, _f32p, _f64p, _u8p]
@@ -119,7 +130,22 @@ def _p(a, t):
 
 
 def init(device: int = -1) -> None:
+    """Select the device (-1: current / whatever the engine already runs on)."""
     _check(lib().hc_phmm_init(0, device))
+
+
+def init_devices(devices=None) -> None:
+    """Configure device slots (HIP ordinals; None = every visible device). An
+    ordinal may repeat: two streams on one GPU."""
+    if devices is None:
+        _check(lib().hc_phmm_init_devices(0, None, 0))
+        return
+    arr = np.ascontiguousarray(devices, np.int32)
+    _check(lib().hc_phmm_init_devices(0, _p(arr, _i32p), len(arr)))
+
+
+def device_count() -> int:
+    return int(lib().hc_phmm_device_count())
 
 
 def shutdown() -> None:
@@ -181,9 +207,7 @@ def cross(reads, haps):
     return out
 
 
-def cross_regions(regions):
-    """Many regions in one device pass: regions = [(reads, haps), ...] as for
-    :func:`cross`; returns one (n_reads, n_haps) array per region."""
+def _region_array(regions):
     keep, outs = [], []
     arr = (Region * max(len(regions), 1))()
     for k, (reads, haps) in enumerate(regions):
@@ -192,8 +216,65 @@ def cross_regions(regions):
         keep.extend([ra, ha, kk])
         outs.append(out)
         arr[k] = Region(ra, len(reads), ha, len(haps), _p(out, _f64p))
+    return arr, outs, keep
+
+
+def cross_regions(regions):
+    """Many regions in one device pass: regions = [(reads, haps), ...] as for
+    :func:`cross`; returns one (n_reads, n_haps) array per region."""
+    arr, outs, _keep = _region_array(regions)
     _check(lib().hc_phmm_cross_regions(arr, len(regions)))
     return outs
+
+
+class Job:
+    """An asynchronous call in flight (hc_phmm_job): :meth:`collect` waits for
+    the device and returns the results; the inputs may be dropped already."""
+
+    def __init__(self, handle, result, keep):
+        self._h, self._result, self._keep = handle, result, keep
+
+    def ready(self) -> bool:
+        rc = lib().hc_phmm_job_ready(self._h)
+        if rc < 0:
+            _check(rc)
+        return rc == 1
+
+    def collect(self):
+        h, self._h = self._h, None
+        if h is None:
+            raise PairHMMError(EINVAL, "job already collected")
+        _check(lib().hc_phmm_collect(h))
+        self._keep = None
+        return self._result
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            try:
+                lib().hc_phmm_collect(self._h)
+            except Exception:
+                pass
+
+
+def submit_pairs(b) -> Job:
+    """Asynchronous :func:`pairs`: returns a :class:`Job` whose collect()
+    gives the same dict."""
+    args, _arrs = _flat_args(b)
+    n = len(_arrs["R"])
+    out = dict(loglik=np.zeros(n, np.float64), raw_f32=np.zeros(n, np.float32),
+               raw_f64=np.zeros(n, np.float64), rescued=np.zeros(n, np.uint8))
+    h = C.c_void_p()
+    _check(lib().hc_phmm_submit_pairs(*args, _p(out["loglik"], _f64p), _p(out["raw_f32"], _f32p),
+                                      _p(out["raw_f64"], _f64p), _p(out["rescued"], _u8p), C.byref(h)))
+    return Job(h, out, None)
+
+
+def submit_regions(regions) -> Job:
+    """Asynchronous :func:`cross_regions`."""
+    arr, outs, keep = _region_array(regions)
+    h = C.c_void_p()
+    _check(lib().hc_phmm_submit_regions(arr, len(regions), C.byref(h)))
+    return Job(h, outs, None)
 
 
 def compute_likelihoods(haps, reads):
@@ -220,7 +301,13 @@ class Batch:
         self._h = h
 
     def run(self, stream=None):
-        """Enqueue the device pass (asynchronous). stream: hipStream_t as int, or None."""
+        """Enqueue the device pass (asynchronous). stream: a hipStream_t handle as
+        int (e.g. torch.cuda.Stream().cuda_stream), or None for the library's own
+        stream. The legacy null stream (0, torch's default stream) cannot be
+        named through the C ABI, where NULL means the library stream: run under a
+        created stream to order the pass with other work."""
+        if stream is not None and int(stream) == 0:
+            raise ValueError("stream 0 (the null stream) is not selectable; pass a created stream or None")
         _check(lib().hc_phmm_batch_run(self._h, C.c_void_p(stream) if stream else None))
 
     def results(self):

@@ -83,7 +83,8 @@ def _p(a, t):
     return a.ctypes.data_as(t)
 
 
-def init(device: int = 0):
+def init(device: int = -1):
+    """Select the device (-1: the one the engine already runs on, else current)."""
     _check(lib().hc_sw_init(device))
 
 

@@ -14,6 +14,16 @@
  *                                list of independent (read, hap) pairs
  *   hc_phmm_batch_*              the same split into plan (pack + H2D) and execute
  *                                (device only) for device-resident batches
+ *   hc_phmm_submit_* / _collect  asynchronous form of the calls above: host
+ *                                planning of the next batch overlaps the device
+ *                                pass of the previous one (the driver's window
+ *                                loop, haplotypecaller.hpp:138-152, keeps
+ *                                assembling while the GPU works)
+ *   hc_phmm_init_devices         one process, several GPUs: every call is split
+ *                                by cells over the configured devices, each with
+ *                                its own stream (the in-call parallelism the
+ *                                reference has as an OpenMP loop,
+ *                                intel_pairhmm.hpp:128-130)
  *   hc_phmm_read / hc_phmm_hap   field-for-field the accelerator hook structs
  *                                shacc_pairhmm::Read / ::Haplotype
  *                                (pairhmm/native/shacc_pairhmm.h:12-24)
@@ -25,11 +35,12 @@
  * the reference kernel: raw fp32 sum, fp64 rescue when raw < 1e-28f, glibc
  * log10f/log10 finish (intel_pairhmm.hpp:131-146).
  *
- * Every pointer is borrowed for the duration of the call; nothing is retained.
- * Calls are synchronous and thread-safe (serialised internally). All entry
- * points return 0 on success or a negative HC_PHMM_E* code; the message of the
- * calling thread's last error is available from hc_phmm_last_error(). There is
- * no CPU fallback: without a usable MI355X the calls fail with HC_PHMM_ENODEV.
+ * Every pointer is borrowed for the duration of the call (for hc_phmm_submit_*:
+ * inputs until submit returns, outputs until hc_phmm_collect returns); nothing
+ * else is retained. Calls are thread-safe. All entry points return 0 on success
+ * or a negative HC_PHMM_E* code; the message of the calling thread's last
+ * error is available from hc_phmm_last_error(). There is no CPU fallback:
+ * without a usable MI355X the calls fail with HC_PHMM_ENODEV.
  */
 #ifndef HC_PAIRHMM_H
 #define HC_PAIRHMM_H
@@ -76,12 +87,24 @@ typedef struct hc_phmm_stats {
     int64_t n_runs;         /* runs since the previous stats() call          */
     int64_t n_lane_pairs;   /* pairs on the lane-per-pair kernel (rest: anti-diagonal) */
     int64_t n_seg_waves;    /* lane waves that split each pair over 2..16 lanes       */
+    int64_t n_devices;      /* device slots the batch is split over                  */
+    double pack_ms;         /* device packing of a new batch (rows + hap tables),
+                               done once at create; max over devices               */
+    int64_t upload_bytes;   /* host -> device bytes of the batch's inputs            */
 } hc_phmm_stats;
 
 /* Select the device (HIP ordinal; -1 = current) and build the device LUTs.
- * flags: reserved, pass 0. Idempotent. (intel_pairhmm.hpp:77-113 initNative) */
+ * flags: reserved, pass 0. (intel_pairhmm.hpp:77-113 initNative.) Calling it
+ * again is a no-op for the same device or for -1; naming a different device
+ * than the engine runs on is HC_PHMM_EINVAL (hc_phmm_shutdown first). */
 int hc_phmm_init(uint32_t flags, int device);
-int hc_phmm_shutdown(void);
+/* Several device slots in one process: devices[k] is a HIP ordinal (-1 =
+ * current); devices == NULL or n == 0 means every visible device. An ordinal
+ * may repeat (two streams on one GPU). Every later call splits its pairs by
+ * cells over the slots, one stream each; results are identical to one device. */
+int hc_phmm_init_devices(uint32_t flags, const int32_t* devices, int32_t n);
+int hc_phmm_device_count(void);   /* configured device slots (0: not initialised) */
+int hc_phmm_shutdown(void);       /* releases every engine (PairHMM, SW, genotyper) */
 const char* hc_phmm_last_error(void);
 int hc_phmm_version(void);   /* major*10000 + minor*100 + patch */
 
@@ -150,6 +173,23 @@ int hc_phmm_batch_device_results(hc_phmm_batch* b, void** raw_f32, void** raw_f6
  * the library's own buffer for that output. */
 int hc_phmm_batch_bind_outputs(hc_phmm_batch* b, void* raw_f32, void* raw_f64, void* rescued);
 int hc_phmm_batch_destroy(hc_phmm_batch* b);
+
+/* Asynchronous calls. submit plans the batch on the host, stages it, enqueues
+ * H2D + device pass + D2H on the device stream(s) and returns; the inputs may
+ * be released as soon as submit returns. collect waits for the device, applies
+ * the log10 finish into the outputs named at submit and frees the job. Jobs may
+ * be collected in any order; several may be in flight (each holds its own
+ * device and pinned workspace until collected). */
+typedef struct hc_phmm_job hc_phmm_job;
+int hc_phmm_submit_pairs(int64_t n, const int64_t* read_off, const int32_t* R,
+                         const int64_t* hap_off, const int32_t* H,
+                         const uint8_t* rs, const uint8_t* q, const uint8_t* ins,
+                         const uint8_t* del, const uint8_t* gcp, const uint8_t* hap,
+                         double* loglik, float* raw_f32, double* raw_f64, uint8_t* rescued,
+                         hc_phmm_job** job);
+int hc_phmm_submit_regions(const hc_phmm_region* regions, int32_t n_regions, hc_phmm_job** job);
+int hc_phmm_job_ready(hc_phmm_job* job);   /* 1: device work done, 0: not yet, < 0: error */
+int hc_phmm_collect(hc_phmm_job* job);
 
 /* LUTs the engine uses (for parity tests against the reference's Context<>):
  * ph2pr_f/d[128], mm_f/d[n_mm] with n_mm = 255*256/2 = 32640. */

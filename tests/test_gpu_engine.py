@@ -1,0 +1,146 @@
+"""GPU: the engine around the kernels — several device slots in one process,
+parts and chunks, the asynchronous submit / collect calls, cross-region
+batching — bit for bit against the oracle and the golden vectors. On the
+1-GPU box a device list [0, 0] gives two slots (two streams, two workspaces)
+on one GPU, which exercises every sharding path the 8-GPU node uses."""
+import numpy as np
+import pytest
+
+import workloads as W
+from test_gpu_parity import assert_same, bits
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def two_slots(engine):
+    """The engine on device slots [0, 0]; restored to [0] afterwards."""
+    engine.shutdown()
+    engine.init_devices([0, 0])
+    try:
+        yield engine
+    finally:
+        engine.shutdown()
+        engine.init(0)
+
+
+@pytest.fixture
+def many_parts(monkeypatch):
+    """Split even small calls into several parts (shards x chunks)."""
+    monkeypatch.setenv("HC_PHMM_SHARD_MIN_CELLS", "0")
+    monkeypatch.setenv("HC_PHMM_CHUNK_CELLS", "20000000")
+
+
+def golden_ref(golden):
+    return dict(raw_f32=golden["raw_f32"], rescued=golden["rescued"],
+                raw_f64=golden["raw_f64_all"], loglik=golden["loglik"])
+
+
+def test_init_rejects_a_different_device(two_slots):
+    assert two_slots.device_count() == 2
+    with pytest.raises(two_slots.PairHMMError) as e:
+        two_slots.init(0)        # engine runs on [0, 0]: naming [0] is a different selection
+    assert e.value.code == two_slots.EINVAL
+    two_slots.init(-1)           # -1: whatever the engine runs on
+    two_slots.init_devices([0, 0])
+
+
+def test_two_slots_golden(two_slots, golden, golden_batch, many_parts):
+    res = two_slots.pairs(golden_batch)
+    assert_same(res, golden_ref(golden), "golden on [0,0]")
+
+
+def test_two_slots_s2_shard_vs_oracle(two_slots, oracle_lib):
+    """A 125k-pair S2 shard (one rank's share of configs[3] at 8 GPUs) split over
+    two device slots by cells: a 3 000-pair sample equals the oracle, and the
+    whole shard equals the single-slot run."""
+    b = W.config("S2", 125_000)
+    res = two_slots.pairs(b)
+    idx = np.random.default_rng(2).choice(125_000, 3000, replace=False)
+    assert_same({k: res[k][idx] for k in res}, oracle_lib.pairs(W.subset(b, idx), nthreads=16), "S2-125k [0,0]")
+    bt = two_slots.Batch(b)
+    st0 = bt.stats()
+    assert st0.n_devices == 2 and st0.pack_ms > 0 and st0.upload_bytes > 0
+    bt.run()
+    r2 = bt.results()
+    st = bt.stats()
+    bt.close()
+    assert st.n_pairs == 125_000 and st.cells == W.cells(b) and st.n_runs == 1
+    for k in res:
+        assert np.array_equal(bits(res[k]), bits(r2[k])), k
+
+
+def test_parts_and_chunks_are_exact(engine, oracle_lib, many_parts):
+    """One call cut into many contiguous parts (chunks on one slot) gives the
+    same bits as the oracle."""
+    b = W.generate(4000, (50, 900), (20, 250), 0.03, seed=21)
+    assert_same(engine.pairs(b), oracle_lib.pairs(b, nthreads=16), "chunked")
+
+
+def test_async_jobs_collected_out_of_order(engine, oracle_lib):
+    batches = [W.generate(1500 + 500 * k, (100, 600), (50, 250), 0.02, seed=30 + k) for k in range(4)]
+    jobs = [engine.submit_pairs(b) for b in batches]
+    for k in (2, 0, 3, 1):
+        assert_same(jobs[k].collect(), oracle_lib.pairs(batches[k], nthreads=16), f"job {k}")
+    with pytest.raises(engine.PairHMMError):
+        jobs[0].collect()
+
+
+def test_async_jobs_overlap_inputs_released(engine, oracle_lib):
+    """Inputs may be dropped as soon as submit returns (they are staged)."""
+    b = W.generate(2000, (100, 500), (50, 250), 0.01, seed=41)
+    ref = oracle_lib.pairs(b, nthreads=16)
+    cp = {k: v.copy() for k, v in b.items()}
+    job = engine.submit_pairs(cp)
+    for v in cp.values():
+        v[...] = 0
+    del cp
+    assert_same(job.collect(), ref, "released inputs")
+
+
+def _regions_ref(oracle_lib, regions):
+    out = []
+    for reads, haps in regions:
+        if not reads or not haps:
+            out.append(np.zeros((len(reads), len(haps))))
+            continue
+        flat = W.region_flat(reads, haps)
+        out.append(oracle_lib.pairs(flat, nthreads=16)["loglik"].reshape(len(reads), len(haps)))
+    return out
+
+
+@pytest.mark.parametrize("split", ["one_part", "many_parts"])
+def test_cross_regions_vs_oracle(engine, oracle_lib, monkeypatch, split):
+    """Cross-region batching against the oracle: regions of
+    different shapes, empty ones, and (many_parts) regions cut into read
+    ranges over several parts."""
+    if split == "many_parts":
+        monkeypatch.setenv("HC_PHMM_SHARD_MIN_CELLS", "0")
+        monkeypatch.setenv("HC_PHMM_CHUNK_CELLS", "30000000")
+    regions = [W.region(n_reads=int(nr), n_haps=int(nh), seed=200 + k)
+               for k, (nr, nh) in enumerate([(50, 2), (120, 8), (0, 3), (415, 32), (7, 1), (300, 5)])]
+    got = engine.cross_regions(regions)
+    for k, (g, e) in enumerate(zip(got, _regions_ref(oracle_lib, regions))):
+        assert g.shape == e.shape
+        assert np.array_equal(bits(g), bits(e)), f"region {k}"
+
+
+def test_submit_regions_two_slots(two_slots, oracle_lib):
+    regions = [W.region(n_reads=200, n_haps=int(nh), seed=300 + k) for k, nh in enumerate([4, 16, 2, 8])]
+    ref = _regions_ref(oracle_lib, regions)
+    jobs = [two_slots.submit_regions(regions[:2]), two_slots.submit_regions(regions[2:])]
+    got = jobs[1].collect() + jobs[0].collect()
+    for g, e in zip(got, ref[2:] + ref[:2]):
+        assert np.array_equal(bits(g), bits(e))
+
+
+def test_per_base_gap_reads_take_the_full_upload(engine, oracle_lib):
+    """Reads whose gap qualities vary are uploaded with their i/d/c planes; mixed
+    with constant-gap reads in one batch."""
+    b = W.generate(3000, (80, 400), (30, 200), 0.02, seed=9)
+    rng = np.random.default_rng(4)
+    rows = np.repeat(np.arange(3000) % 3 == 0, b["R"])
+    n = int(rows.sum())
+    b["ins"][rows] = rng.integers(33 + 5, 33 + 60, n, dtype=np.uint8)
+    b["gcp"][rows] = rng.integers(33 + 5, 33 + 30, n, dtype=np.uint8)
+    assert_same(engine.pairs(b), oracle_lib.pairs(b, nthreads=16), "mixed gaps")
