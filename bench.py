@@ -65,20 +65,52 @@ def cpu_baseline(batch, threads, reps, sample_desc):
                 sample=sample_desc, seconds=round(best, 3)), res
 
 
-def traffic_from_profiles(workload, cells):
-    """HBM bytes per launch of the dominant kernel from the committed PMC summary
-    of this workload (profiles/*pmc*<workload>*.json, tools/pmc_summary.py),
-    scaled by cells when this launch is a shard of the profiled one; else None."""
-    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc*{workload}*.json")))
+def pmc_from_profiles(workload, cells, kernel_ms):
+    """Counters of the dominant kernel from the newest committed PMC summary of
+    this workload (profiles/r*_pmc_<workload>.json, tools/pmc_summary.py),
+    scaled by cells when this launch is a shard of the profiled one: HBM bytes
+    per launch (2*FETCH_SIZE + WRITE_SIZE, gfx950 rule), LDS bank-conflict
+    cycles per launch, VALU lane-instructions per cell, and the measured HBM
+    rate traffic / kernel time."""
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}.json")))
     if not cands:
-        return None, None
+        return {}
     try:
         d = json.load(open(cands[-1]))
-        per_cell = d.get("hbm_bytes_per_cell")
-        t = int(per_cell * cells) if per_cell else d.get("hbm_bytes_per_launch")
-        return t, os.path.relpath(cands[-1], ROOT)
+        k = d["kernels"][d["dominant_kernel"]]
+        prof_cells = d.get("cells") or (d["hbm_bytes_per_launch"] / d["hbm_bytes_per_cell"])
+        scale = cells / prof_cells
+        traffic = int(d["hbm_bytes_per_launch"] * scale)
+        out = dict(traffic=traffic, traffic_source=os.path.relpath(cands[-1], ROOT),
+                   lds_bank_conflict_cycles=int(k.get("SQ_LDS_BANK_CONFLICT", 0) * scale),
+                   valu_lane_instr_per_cell=round(k["SQ_INSTS_VALU"] * 64 / prof_cells, 3))
+        if kernel_ms > 0:
+            out["hbm_measured_GBs"] = round(traffic / (kernel_ms * 1e-3) / 1e9, 2)
+        return out
     except Exception:
-        return None, None
+        return {}
+
+
+def host_cpu():
+    """CPUs this process may use and the CPU model. The share is the cgroup CPU
+    quota when one is set (the GPU box grants 16 CPUs of a 256-CPU machine;
+    affinity and os.cpu_count() show the whole machine), else the affinity set."""
+    cores = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            cores = max(1, min(cores, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    model = "?"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return cores, model
 
 
 SW_OPS_PER_CELL = 22       # MAIN_CODE int32 vector ops per cell (PairWiseSW.h:4-38)
@@ -194,6 +226,128 @@ def gt_secondary(no_cpu: bool):
     return ent
 
 
+FP64_PEAK_TOPS = 39.3   # AMD MI355X FP64 vector 78.6 TFLOPS (FMA = 2) -> 39.3 T non-FMA op/s; the guide has no FP64 row
+
+
+def resident_pass(hcphmm, W, name, npairs):
+    """One BASELINE config as a device-resident batch: 5 timed device passes
+    (HIP events). S4 also prices its fp64 rescue pass (intel_pairhmm.hpp:
+    137-139): 12 f64 ops per rescued cell / fp64 pass time vs the fp64 peak."""
+    b = W.config(name, npairs)
+    bb = hcphmm.Batch(b)
+    for _ in range(2):
+        bb.run()
+    bb.stats()
+    for _ in range(5):
+        bb.run()
+    s2 = bb.stats()
+    cells = W.cells(b)
+    ent = dict(pairs=len(b["R"]), cells=cells, device_pass_ms=round(s2.run_ms, 4),
+               gcups=round(cells / (s2.run_ms * 1e-3) / 1e9, 2),
+               kernel_ms_f32=round(s2.kernel_ms_f32, 4),
+               frac_f32_kernel=round(12 * cells / (s2.kernel_ms_f32 * 1e-3) / 78.6e12, 4)
+               if s2.kernel_ms_f32 > 0 else None,
+               kernel_ms_f64=round(s2.kernel_ms_f64, 4), rescued=int(s2.n_rescued),
+               new_batch_device_ms=round(s2.run_ms + s2.pack_ms, 4))
+    if s2.n_rescued and s2.kernel_ms_f64 > 0:
+        r = bb.results()
+        m = r["rescued"].astype(bool)
+        rc = int(np.dot(b["R"][m].astype(np.int64), b["H"][m].astype(np.int64)))
+        ach = FLOPS_PER_CELL * rc / (s2.kernel_ms_f64 * 1e-3) / 1e12
+        ent["rescued_cells"] = rc
+        ent["fp64_tcups"] = round(rc / (s2.kernel_ms_f64 * 1e-3) / 1e12, 3)
+        ent["roofline_f64"] = dict(bound="valu-f64", achieved=round(ach, 3), peak=FP64_PEAK_TOPS, unit="T op/s",
+                                   frac=round(ach / FP64_PEAK_TOPS, 4),
+                                   note="12 f64 mul/add per rescued cell / fp64 rescue pass (plan + kernels) time; "
+                                        "peak = AMD spec FP64 vector 78.6 TFLOPS with FMA counted as 2")
+    bb.close()
+    return ent
+
+
+def end_to_end(hcphmm, W, batch, total_cells):
+    """The real call path on the S2 batch: host buffers in, log10 likelihoods
+    out (hc_phmm_pairs_flat: host planning + staging + H2D + device packing +
+    kernels + D2H + host log10, the call cut into parts so the planning of part
+    k+1 overlaps the device pass of part k). Median of 3 after a first call
+    that sizes the workspaces."""
+    t0 = time.perf_counter()
+    hcphmm.pairs(batch)
+    first = time.perf_counter() - t0
+    reps = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        hcphmm.pairs(batch)
+        reps.append(time.perf_counter() - t0)
+    e2e = float(np.median(reps))
+    # Two calls in flight: submit the second before collecting the first (after
+    # one such round that sizes the second set of workspaces).
+    for j in [hcphmm.submit_pairs(batch), hcphmm.submit_pairs(batch)]:
+        j.collect()
+    t0 = time.perf_counter()
+    j1 = hcphmm.submit_pairs(batch)
+    j2 = hcphmm.submit_pairs(batch)
+    j1.collect()
+    j2.collect()
+    two = time.perf_counter() - t0
+    return {"end_to_end_gcups": round(total_cells / e2e / 1e9, 2), "end_to_end_ms": round(e2e * 1e3, 2),
+            "end_to_end_first_call_ms": round(first * 1e3, 2),
+            "end_to_end_async_2calls_gcups": round(2 * total_cells / two / 1e9, 2),
+            "end_to_end_note": "hc_phmm_pairs_flat on host buffers (host planning, staging, H2D, device packing, "
+                               "kernels, D2H, host log10), median of 3; async: two submit_pairs in flight"}
+
+
+def region_calls(hcphmm, W, no_cpu):
+    """One active region (415 reads x N haps, hap ~415 bp, read 150 bp), the
+    call shape of IntelPairHMM::compute_likelihoods (haplotypecaller.hpp:103):
+    host buffers in, doubles out. `call_ms` times the C call (argument structs
+    built once, as a C++ caller holds them); `python_call_ms` includes building
+    them from Python bytes each time. Then 64 such regions (415 x 32) in one
+    cross-region call, and the same 64 as a stream of 8 submits of 8 regions."""
+    sec = {}
+    for nh in (32, 128):
+        reads, haps = W.region(415, nh)
+        call = hcphmm.CrossCall(reads, haps)
+        for _ in range(3):
+            call()
+        reps = 20
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            call()
+        dt = (time.perf_counter() - t0) / reps
+        t0 = time.perf_counter()
+        for _ in range(5):
+            hcphmm.cross(reads, haps)
+        dpy = (time.perf_counter() - t0) / 5
+        flat = W.region_flat(reads, haps)
+        ent = dict(reads=len(reads), haps=nh, cells=W.cells(flat), call_ms=round(dt * 1e3, 3),
+                   python_call_ms=round(dpy * 1e3, 3), gcups=round(W.cells(flat) / dt / 1e9, 2))
+        if not no_cpu:
+            c1, _ = cpu_baseline(flat, 1, 1, "same region, 1 thread")
+            ent["cpu_reference_1core_ms"] = round(c1["seconds"] * 1e3, 1)
+        sec[f"region_415x{nh}"] = ent
+    regs = [W.region(415, 32, seed=1000 + k) for k in range(64)]
+    rc = sum(W.cells(W.region_flat(r, h)) for r, h in regs)
+    call = hcphmm.RegionsCall(regs)
+    groups = [hcphmm.RegionsCall(regs[k:k + 8]) for k in range(0, 64, 8)]
+    for _ in range(2):   # size the workspaces (several parts / jobs in flight)
+        call()
+        for j in [g.submit() for g in groups]:
+            j.collect()
+    t0 = time.perf_counter()
+    call()
+    dt = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    jobs = [g.submit() for g in groups]
+    for j in jobs:
+        j.collect()
+    dj = time.perf_counter() - t0
+    sec["regions_64x_415x32_one_call"] = dict(regions=len(regs), cells=rc, call_ms=round(dt * 1e3, 2),
+                                               gcups=round(rc / dt / 1e9, 2),
+                                               stream_8x8_submits_ms=round(dj * 1e3, 2),
+                                               stream_gcups=round(rc / dj / 1e9, 2))
+    return sec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -201,7 +355,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="S2", choices=["S1", "S1w", "S2", "S4"])
     ap.add_argument("--pairs", type=int, default=None, help="override pair count")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core of this process's CPU set")
     ap.add_argument("--cpu-reps", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip end-to-end and secondary configs")
@@ -210,6 +364,7 @@ def main():
     ap.add_argument("--check", type=int, default=0,
                     help="rank 0 re-computes this many random pairs alone and compares them bit for bit "
                          "with the gathered multi-rank results")
+    ap.add_argument("--check-out", default=None, help="with --check: save the reassembled results (npz)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -290,18 +445,21 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     value = total_cells * args.steps / elapsed / 1e9
 
-    # Dominant kernel: fp32 anti-diagonal PairHMM. Algorithmic work 12 ops/cell.
+    # Dominant kernel: the fp32 PairHMM pass. Algorithmic work 12 ops/cell.
     k_ms = st.kernel_ms_f32
     achieved = FLOPS_PER_CELL * my_cells / (k_ms * 1e-3) / 1e12 if k_ms > 0 else 0.0
-    traffic, tsrc = traffic_from_profiles(args.workload, my_cells)
+    pmc = pmc_from_profiles(args.workload, my_cells, k_ms)
     roofline = dict(bound="valu", achieved=round(achieved, 3), peak=VALU_PEAK_TOPS, unit="TFLOP/s",
-                    frac=round(achieved / VALU_PEAK_TOPS, 4), traffic=traffic,
+                    frac=round(achieved / VALU_PEAK_TOPS, 4), traffic=pmc.get("traffic"),
                     kernel=(("phmm_seg_kernel" if st.n_seg_waves > 0 else "phmm_lane_kernel")
                             if st.n_lane_pairs == st.n_pairs else "phmm_diag_kernel<float,16>"),
                     kernel_ms=round(k_ms, 4),
                     flops_per_cell=FLOPS_PER_CELL, cells_per_launch=my_cells,
                     hbm_algorithmic_GBs=round(algorithmic_bytes(sub) / (k_ms * 1e-3) / 1e9, 2) if k_ms > 0 else None,
-                    hbm_peak_GBs=HBM_PEAK_GBS, traffic_source=tsrc)
+                    hbm_measured_GBs=pmc.get("hbm_measured_GBs"), hbm_peak_GBs=HBM_PEAK_GBS,
+                    lds_bank_conflict_cycles=pmc.get("lds_bank_conflict_cycles"),
+                    valu_lane_instr_per_cell=pmc.get("valu_lane_instr_per_cell"),
+                    traffic_source=pmc.get("traffic_source"))
 
     out = {
         "metric": "PairHMM GCUPS (cell updates/s), fp32 pass + fp64 rescue",
@@ -316,18 +474,26 @@ def main():
         "roofline": roofline,
         "kernel_ms_f64": round(st.kernel_ms_f64, 4),
         "device_pass_ms": round(st.run_ms, 4),
+        # A batch seen for the first time also packs its rows and hap tables on
+        # the device (once per batch, outside the resident-batch step above).
+        "new_batch_device_ms": round(st.run_ms + st.pack_ms, 4),
+        "pack_ms": round(st.pack_ms, 4),
+        "upload_bytes": int(st.upload_bytes),
     }
 
     cpu_res = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        thr = min(args.cpu_threads, os.cpu_count() or 1)
+        cores, model = host_cpu()
+        thr = args.cpu_threads or cores
         cb, cpu_res = cpu_baseline(batch, thr, args.cpu_reps,
-                                   f"the full {args.workload} batch ({n_total} pairs), {thr} OpenMP threads, "
-                                   f"best of {args.cpu_reps}")
+                                   f"the full {args.workload} batch ({n_total} pairs), {thr} OpenMP threads "
+                                   f"(every CPU of this process's share), best of {args.cpu_reps}")
+        cb.update(nproc=cores, cpu_model=model, machine_cpus=os.cpu_count())
         out["cpu_baseline"] = cb
         if not args.no_extra:
             s1 = W.subset(batch, np.arange(min(n_total, 20_000)))
-            c1, _ = cpu_baseline(s1, 1, 1, f"first {len(s1['R'])} pairs of {args.workload}, 1 thread")
+            c1, _ = cpu_baseline(s1, 1, 1, f"first {len(s1['R'])} pairs of {args.workload}, 1 thread "
+                                           "(the reference as built: OpenMP compiled out)")
             out["cpu_baseline_1core"] = c1
 
     if rank == 0 and world == 1:
@@ -339,75 +505,33 @@ def main():
                        for k in ("raw_f32", "rescued", "loglik"))
             out["parity_vs_cpu_reference"] = "bit-exact" if same else "MISMATCH"
     if rank == 0 and world == 1 and not args.no_extra:
-        # First call grows the library's device/pinned workspace; later calls reuse it.
-        t0 = time.perf_counter()
-        hcphmm.pairs(batch)
-        e2e_first = time.perf_counter() - t0
-        e2e_reps = []
-        for _ in range(3):
-            t0 = time.perf_counter()
-            hcphmm.pairs(batch)
-            e2e_reps.append(time.perf_counter() - t0)
-        e2e = float(np.median(e2e_reps))
-        out["end_to_end_gcups"] = round(total_cells / e2e / 1e9, 2)
-        out["end_to_end_ms"] = round(e2e * 1e3, 2)
-        out["end_to_end_first_call_ms"] = round(e2e_first * 1e3, 2)
-        out["end_to_end_note"] = ("host plan + pack + H2D + kernels + D2H + host log10, one call of "
-                                  "hc_phmm_pairs_flat on host buffers (median of 3 after a first call "
-                                  "that sizes the workspace)")
+        out.update(end_to_end(hcphmm, W, batch, total_cells))
         sec = {}
         # S1w1M: the north star's 101x250 shape at a size that fills the chip
         # (S1/S1w are 10k-pair, latency-bound passes of < 0.15 ms).
         for name, npairs in (("S1", None), ("S1w", None), ("S1w1M", 1_000_000), ("S4", None)):
-            b2 = W.config(name.replace("1M", ""), npairs)
-            bb = hcphmm.Batch(b2)
-            for _ in range(2):
-                bb.run()
-            bb.stats()
-            for _ in range(5):
-                bb.run()
-            s2 = bb.stats()
-            sec[name] = dict(pairs=len(b2["R"]), cells=W.cells(b2), device_pass_ms=round(s2.run_ms, 4),
-                             gcups=round(W.cells(b2) / (s2.run_ms * 1e-3) / 1e9, 2),
-                             kernel_ms_f32=round(s2.kernel_ms_f32, 4),
-                             frac_f32_kernel=round(12 * W.cells(b2) / (s2.kernel_ms_f32 * 1e-3) / 78.6e12, 4)
-                             if s2.kernel_ms_f32 > 0 else None,
-                             rescued=int(s2.n_rescued))
-            bb.close()
-        # One active region, the real call shape of IntelPairHMM::compute_likelihoods:
-        # 415 reads x n haps, hap ~415 bp, read 150 bp; host buffers in, doubles out.
-        for nh in (32, 128):
-            reads, haps = W.region(415, nh)
-            hcphmm.cross(reads, haps)
-            t0 = time.perf_counter()
-            reps = 5
-            for _ in range(reps):
-                hcphmm.cross(reads, haps)
-            dt = (time.perf_counter() - t0) / reps
-            flat = W.region_flat(reads, haps)
-            ent = dict(reads=len(reads), haps=nh, cells=W.cells(flat), call_ms=round(dt * 1e3, 3),
-                       gcups=round(W.cells(flat) / dt / 1e9, 2))
-            if not args.no_cpu:
-                c1, _ = cpu_baseline(flat, 1, 1, "same region, 1 thread")
-                ent["cpu_reference_1core_ms"] = round(c1["seconds"] * 1e3, 1)
-            sec[f"region_415x{nh}"] = ent
-        # Cross-region batching: 64 such regions (415 x 32) in one call.
-        regs = [W.region(415, 32, seed=1000 + k) for k in range(64)]
-        hcphmm.cross_regions(regs)
-        t0 = time.perf_counter()
-        hcphmm.cross_regions(regs)
-        dt = time.perf_counter() - t0
-        rc = sum(W.cells(W.region_flat(r, h)) for r, h in regs[:1]) * len(regs)
-        sec["regions_64x_415x32_one_call"] = dict(regions=len(regs), cells_approx=rc, call_ms=round(dt * 1e3, 2),
-                                                   gcups=round(rc / dt / 1e9, 2))
+            sec[name] = resident_pass(hcphmm, W, name.replace("1M", ""), npairs)
+        sec.update(region_calls(hcphmm, W, args.no_cpu))
         sec["smith_waterman"] = sw_secondary(args.no_cpu)
         sec["genotyper"] = gt_secondary(args.no_cpu)
         out["secondary"] = sec
     if world > 1:
         out["gather"] = f"dist.gather ({'gloo, rehearsal' if gloo else 'RCCL'}) of raw_f32 + raw_f64 per step"
+    if args.check and world > 1:
+        # One more step into outputs poisoned with NaN on every rank (and in rank
+        # 0's gather buffers): what is gathered must come from this very run.
+        with torch.cuda.stream(stream):
+            raw32.fill_(float("nan"))
+            raw64.fill_(float("nan"))
+            for g in (g32 or []) + (g64 or []):
+                g.fill_(float("nan"))
+        torch.cuda.synchronize()
+        dist.barrier()
+        step()
+        torch.cuda.synchronize()
     if args.check and world > 1 and rank == 0:
-        # Reassemble batch order from the last step's gathered shards and compare a
-        # random sample with a single-process run of the same pairs.
+        # Reassemble batch order from the gathered shards and compare a random
+        # sample with a single-process run of the same pairs.
         full32 = np.zeros(n_total, np.float32)
         full64 = np.zeros(n_total, np.float64)
         for r, sh in enumerate(shards):
@@ -417,7 +541,10 @@ def main():
         ref = hcphmm.pairs(W.subset(batch, idx))
         ok = (np.array_equal(full32[idx].view(np.uint32), ref["raw_f32"].view(np.uint32)) and
               np.array_equal(full64[idx].view(np.uint64), ref["raw_f64"].view(np.uint64)))
+        ok = ok and not np.isnan(full32).any() and not np.isnan(full64).any()
         out["multi_rank_check"] = f"{len(idx)} pairs {'bit-exact' if ok else 'MISMATCH'}"
+        if args.check_out:
+            np.savez(args.check_out, raw_f32=full32, raw_f64=full64)
     bt.close()
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -318,6 +318,10 @@ struct PhaseTimer {
     }
 };
 
+// Host-only planning (no device calls): hcx_plan_* below time the host side
+// of plan_part in a container without a GPU.
+bool g_dry = false;
+
 int64_t env_i64(const char* name, int64_t dflt)
 {
     const char* e = std::getenv(name);
@@ -455,13 +459,13 @@ void sort_desc(std::vector<int>& idx, const std::vector<uint32_t>& key)
 
 // Stable parallel counting sort of `idx` by bucket(p) DESCENDING, buckets < nb.
 template <typename B>
-void counting_sort_desc(std::vector<int>& idx, int nb, B bucket)
+void counting_sort_desc(std::vector<int>& idx, std::vector<int>& out, std::vector<int64_t>& hist, int nb, B bucket)
 {
     const int64_t n = int64_t(idx.size());
     if (n < 2) return;
     const int T = int(std::min<int64_t>(64, std::max<int64_t>(1, n / 8192)));
     const int64_t chunk = (n + T - 1) / T;
-    std::vector<int64_t> hist(static_cast<size_t>(T) * nb, 0);
+    hist.assign(size_t(T) * nb, 0);
     WorkerPool::get().run(T, [&](int t) {
         int64_t* h = hist.data() + size_t(t) * nb;
         for (int64_t k = t * chunk, e = std::min(n, k + chunk); k < e; ++k) ++h[bucket(idx[k])];
@@ -474,7 +478,7 @@ void counting_sort_desc(std::vector<int>& idx, int nb, B bucket)
             h = run;
             run += c;
         }
-    std::vector<int> out(static_cast<size_t>(n));
+    out.resize(size_t(n));
     WorkerPool::get().run(T, [&](int t) {
         int64_t* h = hist.data() + size_t(t) * nb;
         for (int64_t k = t * chunk, e = std::min(n, k + chunk); k < e; ++k) out[h[bucket(idx[k])]++] = idx[k];
@@ -517,6 +521,23 @@ struct Layout {
     }
 };
 
+// Whether a read's (i, d, c) gap qualities are the same on every row (then
+// they travel once, in its descriptor). Blocks of 64 rows without early exit
+// inside a block, so the compiler vectorises the compare.
+bool constant_gaps(const ReadView& v)
+{
+    const uint8_t i0 = v.i[0], d0 = v.d[0], c0 = v.c[0];
+    int k = 0;
+    for (; k + 64 <= v.len; k += 64) {
+        uint8_t a = 0;
+        for (int j = 0; j < 64; ++j) a |= uint8_t((v.i[k + j] ^ i0) | (v.d[k + j] ^ d0) | (v.c[k + j] ^ c0));
+        if (a) return false;
+    }
+    uint8_t a = 0;
+    for (; k < v.len; ++k) a |= uint8_t((v.i[k] ^ i0) | (v.d[k] ^ d0) | (v.c[k] ^ c0));
+    return a == 0;
+}
+
 // The part's reads / haps in part-local order, and the (read, hap) of each
 // part-local pair.
 struct Local {
@@ -546,6 +567,12 @@ struct Local {
         if (spec->flat) return spec->lo + lr;
         const size_t b = size_t(std::upper_bound(blk_r.begin(), blk_r.end(), lr) - blk_r.begin()) - 1;
         return spec->blocks[b].r0 + (lr - blk_r[b]);
+    }
+    int64_t hap_mult(int64_t lh) const   // reads paired with local hap lh
+    {
+        if (spec->flat) return 1;
+        const size_t b = size_t(std::upper_bound(blk_h.begin(), blk_h.end(), lh) - blk_h.begin()) - 1;
+        return spec->blocks[b].nr;
     }
     int64_t hap_id(int64_t lh) const
     {
@@ -580,6 +607,26 @@ struct Local {
     }
 };
 
+// Grow-only per-thread scratch of the planner: fresh large vectors would be
+// fresh mmap'd pages, zero-filled by the kernel on first touch, every call.
+struct PlanScratch {
+    std::vector<int32_t> rlen, gapw, hlen;
+    std::vector<int64_t> row_off, gap_off, hap_w, hap_b;
+    std::vector<uint8_t> hcls, cls, seg_bc, seg_nb, used, in_tail;
+    std::vector<uint32_t> hcand, key, id;
+    std::vector<int> seg_in, one_ord, ord2[2], seg_ord, sort_tmp;
+    std::vector<LaneWave> lw, ordered;
+    std::vector<std::vector<LaneWave>> part_w;
+    std::vector<int64_t> hist;
+};
+thread_local PlanScratch t_scr;
+
+template <typename T>
+void grow(std::vector<T>& v, size_t n)
+{
+    if (v.size() < n) v.resize(n);
+}
+
 // Plan one part on device d: host binning + staging, then the H2D, device
 // packing and (with_run) the device pass and the D2H of the results, all
 // enqueued on d's stream. slot == nullptr: the part owns its memory (batches).
@@ -593,41 +640,47 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const int64_t nr = loc.nr, nh = loc.nh, npairs = loc.np;
     if (npairs > (int64_t(1) << 31) - 1) return fail(HC_PHMM_EINVAL, "too many pairs for one batch");
 
-    // Reads: validate, lengths -> row offsets, gap-quality constancy.
-    std::vector<int64_t> row_off, gap_off;
-    std::vector<int32_t> gapw(static_cast<size_t>(nr));
+    // Reads: validate, lengths, gap-quality constancy; haps: validate, lengths.
+    PlanScratch& S = t_scr;
+    grow(S.rlen, size_t(nr));
+    grow(S.gapw, size_t(nr));
+    grow(S.hlen, size_t(nh));
+    int32_t* rlen = S.rlen.data();
+    int32_t* gapw = S.gapw.data();
+    int32_t* hlen = S.hlen.data();
     std::atomic<int> bad_read{0}, bad_hap{0};
-    prefix_sum(nr, row_off, [&](int64_t r) -> int64_t {
-        const ReadView v = src.read(loc.read_id(r));
-        if (v.len <= 0 || v.len > HC_PHMM_MAX_READ_LEN || !v.bases || !v.q || !v.i || !v.d || !v.c) {
-            bad_read.store(1);
-            gapw[size_t(r)] = 0;
-            return 0;
+    parallel_for(nr, [&](int64_t lo, int64_t hi) {
+        for (int64_t r = lo; r < hi; ++r) {
+            const ReadView v = src.read(loc.read_id(r));
+            if (v.len <= 0 || v.len > HC_PHMM_MAX_READ_LEN || !v.bases || !v.q || !v.i || !v.d || !v.c) {
+                bad_read.store(1);
+                rlen[size_t(r)] = 0;
+                gapw[size_t(r)] = 0;
+                continue;
+            }
+            rlen[size_t(r)] = v.len;
+            gapw[size_t(r)] = constant_gaps(v) ? int32_t((v.i[0] & 127) | ((v.d[0] & 127) << 7) | ((v.c[0] & 127) << 14))
+                                               : -1;
         }
-        // constant gap qualities: every row's (i, d, c) equals the first row's
-        const uint8_t i0 = v.i[0], d0 = v.d[0], c0 = v.c[0];
-        bool cg = true;
-        for (int k = 1; k < v.len && cg; ++k) cg = (v.i[k] == i0) & (v.d[k] == d0) & (v.c[k] == c0);
-        gapw[size_t(r)] = cg ? int32_t((i0 & 127) | ((d0 & 127) << 7) | ((c0 & 127) << 14)) : -1;
-        return v.len;
-    });
+    }, 2048);
     if (bad_read.load()) return fail(HC_PHMM_EINVAL, "read with invalid length or null array");
-    prefix_sum(nr, gap_off, [&](int64_t r) -> int64_t {
-        return gapw[size_t(r)] < 0 ? int64_t(row_off[size_t(r) + 1] - row_off[size_t(r)]) : 0;
-    });
-    std::vector<int64_t> hap_w, hap_b;   // table words / byte offsets
-    prefix_sum(nh, hap_w, [&](int64_t h) -> int64_t {
-        const HapView v = src.hapv(loc.hap_id(h));
-        if (v.len <= 0 || v.len > HC_PHMM_MAX_HAP_LEN || !v.bases) {
-            bad_hap.store(1);
-            return 0;
+    parallel_for(nh, [&](int64_t lo, int64_t hi) {
+        for (int64_t h = lo; h < hi; ++h) {
+            const HapView v = src.hapv(loc.hap_id(h));
+            const bool ok = v.len > 0 && v.len <= HC_PHMM_MAX_HAP_LEN && v.bases;
+            if (!ok) bad_hap.store(1);
+            hlen[size_t(h)] = ok ? v.len : 0;
         }
-        return hap_table_words(v.len);
-    });
+    }, 8192);
     if (bad_hap.load())
         return fail(HC_PHMM_EINVAL, "haplotype with invalid length (1.." + std::to_string(HC_PHMM_MAX_HAP_LEN) +
                                         ") or null bases");
-    prefix_sum(nh, hap_b, [&](int64_t h) -> int64_t { return src.hap_len(loc.hap_id(h)); });
+    // rows / irregular gap rows / table words / hap bytes
+    std::vector<int64_t>&row_off = S.row_off, &gap_off = S.gap_off, &hap_w = S.hap_w, &hap_b = S.hap_b;
+    prefix_sum(nr, row_off, [&](int64_t r) -> int64_t { return rlen[size_t(r)]; });
+    prefix_sum(nr, gap_off, [&](int64_t r) -> int64_t { return gapw[size_t(r)] < 0 ? rlen[size_t(r)] : 0; });
+    prefix_sum(nh, hap_w, [&](int64_t h) -> int64_t { return hap_table_words(hlen[size_t(h)]); });
+    prefix_sum(nh, hap_b, [&](int64_t h) -> int64_t { return hlen[size_t(h)]; });
     const int64_t nrows = row_off[size_t(nr)], ngap = gap_off[size_t(nr)];
     if (nrows > INT32_MAX || hap_w[size_t(nh)] > INT32_MAX || hap_b[size_t(nh)] > INT32_MAX || ngap > INT32_MAX)
         return fail(HC_PHMM_EINVAL, "batch too large (row or hap pool exceeds 2^31)");
@@ -656,9 +709,12 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const size_t host_upload_cap = o_lw + waves_max;
     const size_t host_res_off = (host_upload_cap + 255) & ~size_t(255);
     char* host = nullptr;
-    std::vector<char> dummy;
     bool own_host = false;
-    if (slot) {
+    static std::vector<char> dry_host;   // g_dry: plain memory, one planner at a time
+    if (g_dry) {
+        if (dry_host.size() < host_res_off + res_bytes) dry_host.resize(host_res_off + res_bytes);
+        host = dry_host.data();
+    } else if (slot) {
         const int rc = slot_reserve(*slot, 0, host_res_off + res_bytes);
         if (rc) return rc;
         host = slot->host;
@@ -677,50 +733,43 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     } hguard{host, own_host};
     tm.mark("staging alloc");
 
-    // Pair descriptors straight into the staging image; classification.
+    // Per hap: kernel class, lanes at each width cap (times the reads it pairs
+    // with), then the pass's cap and the hap's two (BC, nb) candidates.
     PairDesc* pd = reinterpret_cast<PairDesc*>(host + o_pairs);
     const int pol = kernel_policy();
     const bool use_lane = pol != 2;
     const int seg_max_h = lane_seg_policy() == 0 ? 0 : 64 * kSegMaxBC;
-    // class: 0 seg, 1 one-lane, 2 diag W16, 3 diag W64
-    std::vector<uint8_t> cls(static_cast<size_t>(npairs));
-    std::atomic<int64_t> cells_a{0}, wide_a{0};
-    std::atomic<int> hmax_a{0};
     constexpr int kCaps[5] = {64, 48, 32, 24, 16};
+    // class: 0 seg, 1 one-lane, 2 diag W16, 3 diag W64
+    grow(S.hcls, size_t(nh));
+    uint8_t* hcls = S.hcls.data();
     std::array<std::atomic<int64_t>, 5> lanes_at{};
-    std::array<std::atomic<int64_t>, 4> cls_n{};
     for (auto& x : lanes_at) x = 0;
-    for (auto& x : cls_n) x = 0;
-    parallel_for(npairs, [&](int64_t lo, int64_t hi) {
-        int64_t c = 0, w = 0, lanes[5] = {}, cn[4] = {};
+    std::atomic<int64_t> wide_a{0};
+    std::atomic<int> hmax_a{0};
+    parallel_for(nh, [&](int64_t lo, int64_t hi) {
+        int64_t lanes[5] = {}, w = 0;
         int hm = 0;
-        loc.pairs(lo, hi, [&](int64_t k, int64_t r, int64_t h) {
-            const int R = int(row_off[size_t(r) + 1] - row_off[size_t(r)]);
-            const int H = int(hap_b[size_t(h) + 1] - hap_b[size_t(h)]);
-            pd[k] = PairDesc{int(row_off[size_t(r)]), R, int(hap_w[size_t(h)]), H};
-            c += int64_t(R) * H;
-            hm = std::max(hm, H);
-            w += H > 64 * 32;
+        for (int64_t h = lo; h < hi; ++h) {
+            const int H = hlen[size_t(h)];
+            const int64_t m = loc.hap_mult(h);
             int cl;
             if (use_lane && (pol == 1 || H <= kLaneMaxH))
                 cl = H > seg_max_h ? 1 : 0;
             else
                 cl = H > kW64Threshold ? 3 : 2;
-            cls[size_t(k)] = uint8_t(cl);
-            ++cn[cl];
+            hcls[size_t(h)] = uint8_t(cl);
             if (cl == 0)
-                for (int q = 0; q < 5; ++q) lanes[q] += std::min(64, (H + kCaps[q] - 1) / kCaps[q]);
-        });
-        cells_a += c;
+                for (int q = 0; q < 5; ++q) lanes[q] += m * std::min(64, (H + kCaps[q] - 1) / kCaps[q]);
+            hm = std::max(hm, H);
+            w += H > 64 * 32 ? m : 0;
+        }
+        for (int q = 0; q < 5; ++q) lanes_at[q] += lanes[q];
         wide_a += w;
         int cur = hmax_a.load();
         while (hm > cur && !hmax_a.compare_exchange_weak(cur, hm)) {
         }
-        for (int q = 0; q < 5; ++q) lanes_at[q] += lanes[q];
-        for (int q = 0; q < 4; ++q) cls_n[q] += cn[q];
     }, 1 << 14);
-    tm.mark("descriptors");
-
     // Column-segmented waves (lane_kernel.hip run_seg): a pair gets nb lanes of
     // BC columns, BC from the compiled widths, choosing between nb0 =
     // ceil(H/cap) and nb0 + 1 lanes by modelled cost nb*BC*(R + nb - 1). The
@@ -742,59 +791,125 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             }
         }
     }
-    std::vector<int> seg_in(static_cast<size_t>(cls_n[0].load())), one_ord, ord2[2];
-    one_ord.reserve(size_t(cls_n[1].load()));
-    ord2[0].reserve(size_t(cls_n[2].load()));
-    ord2[1].reserve(size_t(cls_n[3].load()));
-    {
-        size_t ns = 0;
-        for (int64_t k = 0; k < npairs; ++k) {
-            switch (cls[size_t(k)]) {
-            case 0: seg_in[ns++] = int(k); break;
-            case 1: one_ord.push_back(int(k)); break;
-            case 2: ord2[0].push_back(int(k)); break;
-            default: ord2[1].push_back(int(k)); break;
-            }
-        }
-    }
-    std::vector<uint8_t> seg_bc(static_cast<size_t>(npairs), 0), seg_nb(static_cast<size_t>(npairs), 0);
-    std::atomic<int> rmin_a{INT32_MAX}, rmax_a{0};
-    parallel_for(int64_t(seg_in.size()), [&](int64_t lo, int64_t hi) {
-        int rlo = INT32_MAX, rhi = 0;
-        for (int64_t q = lo; q < hi; ++q) {
-            const int p = seg_in[size_t(q)];
-            const int H = pd[p].w, R = pd[p].y;
+    struct Cand {
+        uint8_t bc[2], nb[2];
+    };
+    static_assert(sizeof(Cand) == sizeof(uint32_t), "Cand packs into a word");
+    grow(S.hcand, size_t(nh));
+    Cand* hcand = reinterpret_cast<Cand*>(S.hcand.data());
+    parallel_for(nh, [&](int64_t lo, int64_t hi) {
+        for (int64_t h = lo; h < hi; ++h) {
+            if (hcls[size_t(h)] != 0) continue;
+            const int H = hlen[size_t(h)];
             const int nb0 = std::min(64, (H + cap - 1) / cap);
-            int64_t best = INT64_MAX;
-            for (int nb = nb0; nb <= std::min(nb0 + 1, 64); ++nb) {
+            Cand c{};
+            for (int q = 0; q < 2; ++q) {
+                const int nb = std::min(nb0 + q, 64);
                 int bc = std::max(kSegMinBC, ((H + nb - 1) / nb + 3) / 4 * 4);
                 while (!seg_width_ok(bc)) bc += 4;
-                const int nbb = (H + bc - 1) / bc;
-                const int64_t cost = int64_t(nbb) * bc * (R + nbb - 1);
-                if (cost < best) {
-                    best = cost;
-                    seg_bc[size_t(p)] = uint8_t(bc);
-                    seg_nb[size_t(p)] = uint8_t(nbb);
-                }
+                c.bc[q] = uint8_t(bc);
+                c.nb[q] = uint8_t((H + bc - 1) / bc);
             }
-            rlo = std::min(rlo, R);
-            rhi = std::max(rhi, R);
+            hcand[size_t(h)] = c;
         }
+    }, 1 << 14);
+    tm.mark("hap classes");
+
+    // Per pair: descriptor straight into the staging image, class, and for
+    // segmented pairs the cheaper candidate for its R.
+    grow(S.cls, size_t(npairs));
+    grow(S.seg_bc, size_t(npairs));
+    grow(S.seg_nb, size_t(npairs));
+    uint8_t *cls = S.cls.data(), *seg_bc = S.seg_bc.data(), *seg_nb = S.seg_nb.data();
+    std::atomic<int64_t> cells_a{0};
+    std::atomic<int> rmin_a{INT32_MAX}, rmax_a{0};
+    const int T = int(std::min<int64_t>(64, std::max<int64_t>(1, npairs / 8192)));
+    const int64_t pchunk = (npairs + T - 1) / T;
+    std::vector<std::array<int64_t, 4>> tcnt(size_t(T) + 1);
+    WorkerPool::get().run(T, [&](int t) {
+        const int64_t lo = t * pchunk, hi = std::min(npairs, lo + pchunk);
+        // Plain restrict locals: the uint8_t stores below may alias anything,
+        // so anything reached through a capture would be reloaded per pair.
+        const int32_t* __restrict rl = rlen;
+        const int32_t* __restrict hl = hlen;
+        const int64_t* __restrict ro = row_off.data();
+        const int64_t* __restrict hw = hap_w.data();
+        const uint8_t* __restrict hc = hcls;
+        const Cand* __restrict cand = hcand;
+        PairDesc* __restrict pdo = pd;
+        uint8_t* __restrict clo = cls;
+        uint8_t* __restrict bco = seg_bc;
+        uint8_t* __restrict nbo = seg_nb;
+        int64_t c = 0, cn0 = 0, cn1 = 0, cn2 = 0, cn3 = 0;
+        int rlo = INT32_MAX, rhi = 0;
+        auto one = [=, &c, &cn0, &cn1, &cn2, &cn3, &rlo, &rhi](int64_t k, int64_t r, int64_t h) {
+            const int R = rl[r], H = hl[h];
+            pdo[k] = PairDesc{int(ro[r]), R, int(hw[h]), H};
+            c += int64_t(R) * H;
+            const int cl = hc[h];
+            clo[k] = uint8_t(cl);
+            if (cl == 0) {
+                ++cn0;
+                const Cand cd = cand[h];
+                const int c0 = int(cd.nb[0]) * cd.bc[0] * (R + cd.nb[0] - 1);
+                const int c1 = int(cd.nb[1]) * cd.bc[1] * (R + cd.nb[1] - 1);
+                const int q = c1 < c0 ? 1 : 0;
+                bco[k] = cd.bc[q];
+                nbo[k] = cd.nb[q];
+                rlo = R < rlo ? R : rlo;
+                rhi = R > rhi ? R : rhi;
+            } else {
+                cn1 += cl == 1;
+                cn2 += cl == 2;
+                cn3 += cl == 3;
+            }
+        };
+        if (spec.flat) {
+            for (int64_t k = lo; k < hi; ++k) one(k, k, k);
+        } else {
+            loc.pairs(lo, hi, one);
+        }
+        cells_a += c;
+        tcnt[size_t(t) + 1] = {cn0, cn1, cn2, cn3};
         int cur = rmin_a.load();
         while (rlo < cur && !rmin_a.compare_exchange_weak(cur, rlo)) {
         }
         cur = rmax_a.load();
         while (rhi > cur && !rmax_a.compare_exchange_weak(cur, rhi)) {
         }
-    }, 1 << 14);
-    tm.mark("seg choose");
+    });
+    // Stable split of the pairs by class (per-task offsets, parallel scatter).
+    std::array<int64_t, 4> cls_tot{};
+    for (int t = 1; t <= T; ++t)
+        for (int q = 0; q < 4; ++q) {
+            const int64_t v = tcnt[size_t(t)][size_t(q)];
+            tcnt[size_t(t)][size_t(q)] = cls_tot[size_t(q)];
+            cls_tot[size_t(q)] += v;
+        }
+    std::vector<int>&seg_in = S.seg_in, &one_ord = S.one_ord, (&ord2)[2] = S.ord2;
+    seg_in.resize(size_t(cls_tot[0]));
+    one_ord.resize(size_t(cls_tot[1]));
+    ord2[0].resize(size_t(cls_tot[2]));
+    ord2[1].resize(size_t(cls_tot[3]));
+    WorkerPool::get().run(T, [&](int t) {
+        int* dst[4] = {seg_in.data(), one_ord.data(), ord2[0].data(), ord2[1].data()};
+        int64_t pos[4];
+        for (int q = 0; q < 4; ++q) pos[q] = tcnt[size_t(t) + 1][size_t(q)];
+        for (int64_t k = t * pchunk, e = std::min(npairs, k + pchunk); k < e; ++k) {
+            const int q = cls[size_t(k)];
+            dst[q][pos[q]++] = int(k);
+        }
+    });
+    tm.mark("pairs");
     if (!seg_in.empty()) {
         const int rlo = rmin_a.load(), rspan = rmax_a.load() - rlo + 1;
         const int nbk = (kSegMaxBC / 4 + 1) * rspan;
         if (nbk <= (1 << 18)) {
-            counting_sort_desc(seg_in, nbk, [&](int p) { return (seg_bc[size_t(p)] / 4) * rspan + (pd[p].y - rlo); });
+            counting_sort_desc(seg_in, S.sort_tmp, S.hist, nbk,
+                               [&](int p) { return (seg_bc[size_t(p)] / 4) * rspan + (pd[p].y - rlo); });
         } else {
-            std::vector<uint32_t> key(static_cast<size_t>(npairs));
+            std::vector<uint32_t>& key = S.key;
+            grow(key, size_t(npairs));
             for (int p : seg_in) key[size_t(p)] = (uint32_t(seg_bc[size_t(p)]) << 16) | uint32_t(std::min(pd[p].y, 65535));
             sort_desc(seg_in, key);
         }
@@ -803,41 +918,58 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     // Greedy packing in independent segments of the sorted list (one per task;
     // a segment boundary costs at most one partly filled wave).
     const int64_t ns = int64_t(seg_in.size());
-    std::vector<int> seg_ord(static_cast<size_t>(ns));
-    std::vector<LaneWave> lw;
+    std::vector<int>& seg_ord = S.seg_ord;
+    seg_ord.resize(size_t(ns));
+    std::vector<LaneWave>& lw = S.lw;
+    lw.clear();
     {
         const int T = int(std::min<int64_t>(64, std::max<int64_t>(1, ns / 16384)));
         const int64_t chunk = (ns + T - 1) / T;
-        std::vector<std::vector<LaneWave>> part_w(static_cast<size_t>(T));
+        std::vector<std::vector<LaneWave>>& part_w = S.part_w;
+        if (part_w.size() < size_t(T)) part_w.resize(size_t(T));
+        for (auto& W : part_w) W.clear();
+        S.used.assign(size_t(ns), 0);
         WorkerPool::get().run(T, [&](int t) {
             const int64_t b = t * chunk, e = std::min(ns, b + chunk);
             if (b >= e) return;
             const int64_t m = e - b;
-            std::vector<uint8_t> used(static_cast<size_t>(m), 0);
+            const int* __restrict in = seg_in.data() + b;
+            const uint8_t* __restrict bcs = seg_bc;
+            const uint8_t* __restrict nbs = seg_nb;
+            const PairDesc* __restrict pdi = pd;
+            int* __restrict ordo = seg_ord.data();
+            uint8_t* __restrict used = S.used.data() + b;
             auto& W = part_w[size_t(t)];
             int64_t slot_n = b;
             constexpr int64_t kLook = 64;
             for (int64_t i = 0; i < m; ++i) {
-                if (used[size_t(i)]) continue;
-                const int bc = seg_bc[size_t(seg_in[size_t(b + i)])];
+                if (used[i]) continue;
+                const int bc = bcs[in[i]];
                 LaneWave w{};
                 w.slot0 = int(slot_n);
                 w.ncols = bc;
-                w.rmin = INT32_MAX;
+                int rmin = INT32_MAX, rmax = 0, nst = 0, np = 0;
                 int free = 64;
-                for (int64_t j = i; j < m && j < i + kLook && free > 0; ++j) {
-                    if (used[size_t(j)]) continue;
-                    const int p = seg_in[size_t(b + j)];
-                    if (seg_bc[size_t(p)] != bc) break;
-                    if (seg_nb[size_t(p)] > free) continue;
-                    used[size_t(j)] = 1;
-                    free -= seg_nb[size_t(p)];
-                    seg_ord[size_t(slot_n++)] = p;
-                    ++w.npairs;
-                    w.rmax = std::max(w.rmax, pd[p].y);
-                    w.rmin = std::min(w.rmin, pd[p].y);
-                    w.nsteps = std::max(w.nsteps, pd[p].y + seg_nb[size_t(p)] - 1);
+                const int64_t jend = std::min(m, i + kLook);
+                for (int64_t j = i; j < jend && free > 0; ++j) {
+                    if (used[j]) continue;
+                    const int p = in[j];
+                    if (bcs[p] != bc) break;
+                    const int nb = nbs[p];
+                    if (nb > free) continue;
+                    used[j] = 1;
+                    free -= nb;
+                    ordo[slot_n++] = p;
+                    ++np;
+                    const int R = pdi[p].y;
+                    rmax = R > rmax ? R : rmax;
+                    rmin = R < rmin ? R : rmin;
+                    nst = R + nb - 1 > nst ? R + nb - 1 : nst;
                 }
+                w.npairs = np;
+                w.rmax = rmax;
+                w.rmin = rmin;
+                w.nsteps = nst;
                 W.push_back(w);
             }
         });
@@ -856,14 +988,17 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         const size_t K = std::min(nw, size_t(tail_rounds) * 4 * size_t(dv.n_cu) * kSegWavesPerSimd);
         auto cost = [&](size_t k) { return int64_t(lw[k].ncols) * lw[k].nsteps; };
         if (K > 0 && K < nw) {
-            std::vector<uint32_t> id(nw);
+            std::vector<uint32_t>& id = S.id;
+            id.resize(nw);
             std::iota(id.begin(), id.end(), 0u);
             std::nth_element(id.begin(), id.begin() + long(K), id.end(), [&](uint32_t x, uint32_t y) {
                 return cost(x) != cost(y) ? cost(x) < cost(y) : x < y;
             });
-            std::vector<uint8_t> in_tail(nw, 0);
+            std::vector<uint8_t>& in_tail = S.in_tail;
+            in_tail.assign(nw, 0);
             for (size_t k = 0; k < K; ++k) in_tail[id[k]] = 1;
-            std::vector<LaneWave> ordered;
+            std::vector<LaneWave>& ordered = S.ordered;
+            ordered.clear();
             ordered.reserve(nw);
             for (size_t k = 0; k < nw; ++k)
                 if (!in_tail[k]) ordered.push_back(lw[k]);
@@ -885,7 +1020,8 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const LaneVariant& LV = lane_variant(lane_var);
     int64_t carry_rows = 0;
     {
-        std::vector<uint32_t> key(static_cast<size_t>(npairs));
+        std::vector<uint32_t>& key = S.key;
+        grow(key, size_t(npairs));
         auto cols16 = [&](int p) { return (pd[p].w + 15) / 16 * 16; };
         for (int p : one_ord) key[size_t(p)] = (uint32_t(cols16(p)) << 16) | uint32_t(std::min(pd[p].y, 65535));
         sort_desc(one_ord, key);
@@ -955,6 +1091,10 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         }
     }, 256);
     tm.mark("staging fill");
+    if (g_dry) {
+        *out = nullptr;
+        return HC_PHMM_OK;
+    }
 
     // Device region: the upload image, then packed rows / tables, outputs, scratch.
     Layout L;
@@ -1303,6 +1443,7 @@ int submit(const Src& src, const std::vector<PartSpec>& specs, const std::vector
 int collect(hc_phmm_job* J)
 {
     int rc = HC_PHMM_OK;
+    PhaseTimer tm;
     for (size_t j = 0; j < J->parts.size(); ++j) {
         Part* p = J->parts[j];
         if (rc == HC_PHMM_OK) {
@@ -1311,9 +1452,19 @@ int collect(hc_phmm_job* J)
             if (e != hipSuccess) {
                 rc = fail(HC_PHMM_EHIP, std::string("device pass: ") + hipGetErrorString(e));
             } else {
+                tm.mark("collect: wait");
+                if (tm.on) {
+                    float a = 0, f32 = 0, f64 = 0;
+                    (void)hipEventElapsedTime(&a, p->pack_ev[0], p->pack_ev[1]);
+                    (void)hipEventElapsedTime(&f32, p->ev[0], p->ev[1]);
+                    (void)hipEventElapsedTime(&f64, p->ev[1], p->ev[2]);
+                    std::fprintf(stderr, "[hc_phmm]   device: pack %.3f ms, fp32 %.3f ms, fp64 %.3f ms (%lld pairs)\n", a,
+                                 f32, f64, (long long)p->n);
+                }
                 const char* h = p->host_res;
                 finish_part(*p, reinterpret_cast<const float*>(h), reinterpret_cast<const double*>(h + p->res_o64),
                             reinterpret_cast<const uint8_t*>(h + p->res_ofl), J->out);
+                tm.mark("collect: finish");
             }
         } else {
             (void)hipSetDevice(p->dev->ordinal);
@@ -1785,7 +1936,60 @@ int hc_phmm_batch_destroy(hc_phmm_batch* b)
     return HC_PHMM_OK;
 }
 
+// ---- host-planning timing hooks (not part of the ABI: tools/plan_bench.py)
+// Plan a call's parts on the host only, as submit would on `n_dev` slots of
+// `n_cu` compute units, `reps` times; HC_PHMM_TRACE=1 prints the phases.
+// Returns the mean milliseconds per call.
+double hcx_plan_pairs(int64_t n, const int64_t* read_off, const int32_t* R, const int64_t* hap_off, const int32_t* H,
+                      const uint8_t* rs, const uint8_t* q, const uint8_t* ins, const uint8_t* del, const uint8_t* gcp,
+                      const uint8_t* hap, int n_cu, int n_dev, int reps)
+{
+    const Src src = flat_src(read_off, R, hap_off, H, rs, q, ins, del, gcp, hap);
+    Device fake;
+    fake.n_cu = n_cu;
+    g_dry = true;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0; k < reps; ++k) {
+        std::vector<int64_t> pre;
+        prefix_sum(n, pre, [&](int64_t p) { return int64_t(std::max(0, R[p])) * std::max(0, H[p]); });
+        const int np = part_count(pre.back(), n_dev);
+        const std::vector<int64_t> cut = equal_cuts(pre, np);
+        for (int j = 0; j < np; ++j) {
+            PartSpec s;
+            s.lo = cut[size_t(j)];
+            s.hi = cut[size_t(j) + 1];
+            Part* p = nullptr;
+            (void)plan_part(fake, src, s, nullptr, false, &p);
+        }
+    }
+    g_dry = false;
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / reps;
+}
+
+double hcx_plan_regions(const hc_phmm_region* regions, int32_t n_regions, int n_cu, int reps)
+{
+    RegionSet rs;
+    if (gather_regions(regions, n_regions, rs)) return -1;
+    Src src;
+    src.reads = rs.reads.data();
+    src.haps = rs.haps.data();
+    Device fake;
+    fake.n_cu = n_cu;
+    PartSpec s;
+    s.flat = false;
+    s.blocks = rs.blocks;
+    g_dry = true;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0; k < reps; ++k) {
+        Part* p = nullptr;
+        (void)plan_part(fake, src, s, nullptr, false, &p);
+    }
+    g_dry = false;
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / reps;
+}
+
 }  // extern "C"
+
 
 // --------------------------------------------------------------------------
 // The reference's own accelerator slot: a strong definition of the weak

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstdint>
 #include <functional>
 #include <mutex>
@@ -71,7 +72,10 @@ private:
 
     WorkerPool()
     {
-        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        // HC_PHMM_THREADS caps the pool (default: the hardware threads, at most 16).
+        unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        if (const char* e = std::getenv("HC_PHMM_THREADS"))
+            if (std::atoi(e) > 0) hw = unsigned(std::atoi(e));
         const int nw = int(std::min(hw, 16u)) - 1;
         for (int k = 0; k < nw; ++k) workers_.emplace_back([this] { loop(); });
     }

@@ -207,6 +207,40 @@ def cross(reads, haps):
     return out
 
 
+class CrossCall:
+    """hc_phmm_cross on one fixed region with its argument structs built once,
+    as a C++ caller holds them (IntelPairHMM::compute_likelihoods' inputs,
+    intel_pairhmm.hpp:48-56): calling it times the library, not ctypes."""
+
+    def __init__(self, reads, haps):
+        self.ra, self.ha, self._keep = _structs(reads, haps)
+        self.nr, self.nh = len(reads), len(haps)
+        self.out = np.zeros((self.nr, self.nh), np.float64)
+        self._outp = _p(self.out, _f64p)
+
+    def __call__(self):
+        _check(lib().hc_phmm_cross(self.ra, self.nr, self.ha, self.nh, self._outp))
+        return self.out
+
+
+class RegionsCall:
+    """hc_phmm_cross_regions / hc_phmm_submit_regions on fixed regions with the
+    argument structs built once (as a C++ caller holds them)."""
+
+    def __init__(self, regions):
+        self.arr, self.outs, self._keep = _region_array(regions)
+        self.n = len(regions)
+
+    def __call__(self):
+        _check(lib().hc_phmm_cross_regions(self.arr, self.n))
+        return self.outs
+
+    def submit(self) -> "Job":
+        h = C.c_void_p()
+        _check(lib().hc_phmm_submit_regions(self.arr, self.n, C.byref(h)))
+        return Job(h, self.outs, None)
+
+
 def _region_array(regions):
     keep, outs = [], []
     arr = (Region * max(len(regions), 1))()
