@@ -1,5 +1,7 @@
-# GPU session: the whole -m gpu suite, then the default bench line.
+# GPU session: the whole -m gpu suite, smoke, then the default bench line.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_r2b.log 2>&1 || { echo "pytest failed"; exit 1; }
-timeout -k 10 600 python -u bench.py > gpurun_out/bench_r2b.json 2> gpurun_out/bench_r2b.err
+TAG=${1:-r02}
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_$TAG.log 2>&1 || { echo "pytest failed"; exit 1; }
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { echo "smoke failed"; exit 1; }
+timeout -k 10 600 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
