@@ -401,7 +401,6 @@ namespace {
 constexpr int kW64Threshold = 768;     // anti-diagonal kernel: H above this -> one pair per wave
 constexpr int kLaneMaxH = 4096;        // longer haps stay on the anti-diagonal kernel (policy "auto")
 constexpr int kSegWavesPerSimd = 3;    // resident seg waves per SIMD (phmm_seg_kernel occupancy)
-constexpr int kSegMinWavesPerSimd = 2; // small batches: narrower seg blocks until this many waves
 
 int lane_variant_id() { return int(env_i64("HC_PHMM_LANE_VARIANT", 0)); }
 
@@ -739,16 +738,23 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const int pol = kernel_policy();
     const bool use_lane = pol != 2;
     const int seg_max_h = lane_seg_policy() == 0 ? 0 : 64 * kSegMaxBC;
-    constexpr int kCaps[5] = {64, 48, 32, 24, 16};
+    constexpr int kNCaps = 7;
+    constexpr int kCaps[kNCaps] = {64, 48, 32, 24, 16, 12, 8};
     // class: 0 seg, 1 one-lane, 2 diag W16, 3 diag W64
     grow(S.hcls, size_t(nh));
     uint8_t* hcls = S.hcls.data();
-    std::array<std::atomic<int64_t>, 5> lanes_at{};
+    std::array<std::atomic<int64_t>, kNCaps> lanes_at{};
     for (auto& x : lanes_at) x = 0;
     std::atomic<int64_t> wide_a{0};
     std::atomic<int> hmax_a{0};
+    // Modelled wave instructions at each cap (13 per column + ~30 per step,
+    // R + nb - 1 steps at the batch's mean read length), for the cap choice.
+    const double ravg = double(nrows) / double(std::max<int64_t>(nr, 1));
+    std::mutex work_mu;
+    std::array<double, kNCaps> work_at{};
     parallel_for(nh, [&](int64_t lo, int64_t hi) {
-        int64_t lanes[5] = {}, w = 0;
+        int64_t lanes[kNCaps] = {}, w = 0;
+        double work[kNCaps] = {};
         int hm = 0;
         for (int64_t h = lo; h < hi; ++h) {
             const int H = hlen[size_t(h)];
@@ -760,11 +766,21 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
                 cl = H > kW64Threshold ? 3 : 2;
             hcls[size_t(h)] = uint8_t(cl);
             if (cl == 0)
-                for (int q = 0; q < 5; ++q) lanes[q] += m * std::min(64, (H + kCaps[q] - 1) / kCaps[q]);
+                for (int q = 0; q < kNCaps; ++q) {
+                    const int bc = seg_width_ceil((H + std::min(64, (H + kCaps[q] - 1) / kCaps[q]) - 1) /
+                                                  std::min(64, (H + kCaps[q] - 1) / kCaps[q]));
+                    const int nb = (H + bc - 1) / bc;
+                    lanes[q] += m * nb;
+                    work[q] += double(m) * nb * (ravg + nb - 1) * (13.0 * bc + 30.0);
+                }
             hm = std::max(hm, H);
             w += H > 64 * 32 ? m : 0;
         }
-        for (int q = 0; q < 5; ++q) lanes_at[q] += lanes[q];
+        for (int q = 0; q < kNCaps; ++q) lanes_at[q] += lanes[q];
+        {
+            std::lock_guard<std::mutex> lk(work_mu);
+            for (int q = 0; q < kNCaps; ++q) work_at[size_t(q)] += work[q];
+        }
         wide_a += w;
         int cur = hmax_a.load();
         while (hm > cur && !hmax_a.compare_exchange_weak(cur, hm)) {
@@ -773,21 +789,27 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     // Column-segmented waves (lane_kernel.hip run_seg): a pair gets nb lanes of
     // BC columns, BC from the compiled widths, choosing between nb0 =
     // ceil(H/cap) and nb0 + 1 lanes by modelled cost nb*BC*(R + nb - 1). The
-    // width cap is 64 unless the batch is too small to give every SIMD
-    // kSegMinWavesPerSimd waves at that width (a lone wave issues at half
-    // rate): then the widest cap that does, down to 16. Pairs are binned by
-    // (BC, R) descending and packed greedily into waves of up to 64 lanes (a
-    // short look-ahead fills a wave's last lanes).
+    // width cap minimises the modelled pass time: the waves one SIMD runs
+    // (at least 2: a lone wave issues at half rate) times a wave's modelled
+    // instructions (R + nb - 1 steps of 13 per column + ~30). Large batches get the widest cap (least
+    // per-step overhead); a batch that gives each SIMD only a few waves gets
+    // the width that balances waves per SIMD against steps per wave (measured
+    // on MI355X: S1 10k x 101x150 best at 16, S1w 10k x 101x250 at 24).
     int cap = kSegMaxBC;
     {
-        const int64_t want = int64_t(kSegMinWavesPerSimd) * 4 * dv.n_cu * 64;   // lanes
         const int64_t forced = env_i64("HC_PHMM_SEG_CAP", 0);
         if (forced > 0) {
-            cap = int(std::max<int64_t>(16, std::min<int64_t>(kSegMaxBC, forced)));
-        } else {
-            for (int c = 0; c < 5; ++c) {
-                cap = kCaps[c];
-                if (lanes_at[c].load() >= want) break;
+            cap = int(std::max<int64_t>(kSegMinBC, std::min<int64_t>(kSegMaxBC, forced)));
+        } else if (lanes_at[0].load() > 0) {
+            const double simds = 4.0 * dv.n_cu;
+            double best = 0;
+            for (int c = 0; c < kNCaps; ++c) {
+                const double waves = double(lanes_at[c].load()) / 60.0;   // ~60 of 64 lanes filled
+                const double est = std::max(2.0, std::ceil(waves / simds)) * work_at[size_t(c)] / 60.0 / waves;
+                if (c == 0 || est < best * 0.98) {
+                    best = est;
+                    cap = kCaps[c];
+                }
             }
         }
     }
@@ -805,8 +827,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             Cand c{};
             for (int q = 0; q < 2; ++q) {
                 const int nb = std::min(nb0 + q, 64);
-                int bc = std::max(kSegMinBC, ((H + nb - 1) / nb + 3) / 4 * 4);
-                while (!seg_width_ok(bc)) bc += 4;
+                const int bc = seg_width_ceil((H + nb - 1) / nb);
                 c.bc[q] = uint8_t(bc);
                 c.nb[q] = uint8_t((H + bc - 1) / bc);
             }
@@ -903,10 +924,10 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     tm.mark("pairs");
     if (!seg_in.empty()) {
         const int rlo = rmin_a.load(), rspan = rmax_a.load() - rlo + 1;
-        const int nbk = (kSegMaxBC / 4 + 1) * rspan;
+        const int nbk = (kSegMaxBC / 2 + 1) * rspan;
         if (nbk <= (1 << 18)) {
             counting_sort_desc(seg_in, S.sort_tmp, S.hist, nbk,
-                               [&](int p) { return (seg_bc[size_t(p)] / 4) * rspan + (pd[p].y - rlo); });
+                               [&](int p) { return (seg_bc[size_t(p)] / 2) * rspan + (pd[p].y - rlo); });
         } else {
             std::vector<uint32_t>& key = S.key;
             grow(key, size_t(npairs));

@@ -94,8 +94,9 @@ hipError_t launch_lane_f32(int variant, const LaneArgs& a, hipStream_t s);
 // takes ceil(H / BC) lanes; BC per wave, one of the compiled block widths.
 hipError_t launch_lane_seg_f32(const LaneArgs& a, hipStream_t s);
 bool seg_width_ok(int bc);
+int seg_width_ceil(int bc);   // narrowest compiled width >= bc (-1: none)
 constexpr int kSegMaxBC = 64;
-constexpr int kSegMinBC = 16;   // narrowest compiled fp32 block width
+constexpr int kSegMinBC = 8;    // narrowest compiled fp32 block width
 
 // fp64 rescue pass in column-segmented form, planned on the device
 // (lane_kernel.hip rescue_plan_kernel). Two width tiers: bc[0] for the whole

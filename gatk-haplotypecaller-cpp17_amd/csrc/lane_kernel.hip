@@ -282,10 +282,36 @@ struct SegSteps {
 //     column by column left to right exactly as the reference does.
 // Lanes outside 1 <= i <= rmax (pipeline fill / drain) are masked off; columns
 // past H compute values that only flow right and are never summed.
-template <typename T, int BC, bool CG, bool EQ>
-__device__ __forceinline__ void run_seg(const T* __restrict__ lut, const SegSteps& st, int lane, int s,
-                                        const LaneCtx& cx, T T0, T& sumM, T& sumX, uint2* __restrict__ mt)
+// Rows of read words a lane keeps in flight (loaded PD steps before use). A
+// lone step of a narrow block is too short to cover a global load, so narrow
+// blocks prefetch deeper; the step loop is unrolled by PD so every word lands
+// in its own register and is not touched (no wait) until its step.
+#ifndef HC_SEG_DEEP
+#define HC_SEG_DEEP 1   // 0: one-step prefetch everywhere, prior tables read from global memory (A/B builds)
+#endif
+template <typename T, int BC>
+constexpr int seg_prefetch()
 {
+    if (!HC_SEG_DEEP) return 1;
+    return sizeof(T) == 8 ? (BC >= 16 ? 1 : 2) : (BC >= 32 ? 1 : (BC >= 16 ? 2 : 4));
+}
+
+// Call f(integral_constant<P>) for P = 0 .. N-1 (compile-time phases).
+template <int P, int N, typename F>
+__device__ __forceinline__ void for_phases(F&& f)
+{
+    if constexpr (P < N) {
+        f(std::integral_constant<int, P>{});
+        for_phases<P + 1, N>(f);
+    }
+}
+
+template <typename T, int BC, bool CG, bool EQ>
+__device__ __forceinline__ void run_seg(const T* __restrict__ lut, const T* __restrict__ slut, const SegSteps& st,
+                                        int lane, int s, const LaneCtx& cx, T T0, T& sumM, T& sumX,
+                                        uint2* __restrict__ mt)
+{
+    constexpr int PD = seg_prefetch<T, BC>();
     const int c0 = s * BC;
     const int R = cx.R;
     {   // this lane's BC-column window of the match table, fixed for the sweep:
@@ -306,16 +332,41 @@ __device__ __forceinline__ void run_seg(const T* __restrict__ lut, const SegStep
         Tt[j] = T0;   // row 0
         X[j] = T(0);
     }
-    uint32_t wc = cx.rrow[0], wn = cx.rrow[min(2, R) - 1];
+    // wq[P]: the word of row i+1 (clamped to 1..R) at the steps of phase
+    // P = (k-1) mod PD, for every lane at every step; the loads are issued
+    // unconditionally so that each path has the same outstanding loads and
+    // the wait for a word is the one PD steps after its load.
+    uint32_t wc = cx.rrow[0];
+    uint32_t wq[PD];
+#pragma unroll
+    for (int P = 0; P < PD; ++P) wq[P] = cx.rrow[min(max(P + 2 - s, 1), R) - 1];
     RowConst<T> k;
-    row_const<T>(lut, wc, wn, k);
+    row_const<T>(lut, wc, cx.rrow[min(2, R) - 1], k);
     uint2 mrow = mt[k.rc * 64 + lane];
     T y_out = T(0), t_out = T(0);   // handed to lane s+1: Y past column c0+BC, T[BC-1] of the last row
     T t_hold = T(0);                // lane s-1's right-edge T of the previous row
     const int lim0 = cx.H - c0;     // columns of this block inside the hap (<= 0: none)
-    auto step = [&](int kk, auto sum_tag) {
+    auto step = [&](int kk, auto sum_tag, auto ph_tag) {
         constexpr bool SUM = decltype(sum_tag)::value;
+        constexpr int P = decltype(ph_tag)::value;
         const int i = kk - s;
+        const uint32_t wn = wq[P];   // row i+1, loaded PD steps ago
+        T pm_n = T(0), px_n = T(0);
+        uint2 m_n = mrow;
+        int ridx = min(max(i + PD + 1, 1), R) - 1;   // the word needed PD steps from now
+        if constexpr (CG) {   // next row's prior constants (LDS) and match words
+            const int qo = row_q(wn), mo = row_rc(wn) * 64 + lane;
+            // Order the load after the last use of wn, so the word can land in
+            // wn's register (no register move, hence no wait, at the loop back edge).
+            asm volatile("" : "+v"(ridx) : "v"(qo), "v"(mo));
+            const T* __restrict__ pl = HC_SEG_DEEP ? slut : lut;
+            pm_n = pl[kOffPm + qo];
+            px_n = pl[kOffPx + qo];
+            m_n = mt[mo];
+        } else {
+            asm volatile("" : "+v"(ridx) : "v"(wn));
+        }
+        wq[P] = cx.rrow[ridx];
         const T y_in = from_left(y_out);
         const T t_in = from_left(t_out);
         T sM_in = T(0), sX_in = T(0);
@@ -333,14 +384,6 @@ __device__ __forceinline__ void run_seg(const T* __restrict__ lut, const SegStep
                 row_const<T>(lut, wc, wn, k);
                 mrow = mt[k.rc * 64 + lane];
             }
-            const uint32_t wnn = cx.rrow[min(i + 2, R) - 1];
-            T pm_n = T(0), px_n = T(0);
-            uint2 m_n = mrow;
-            if constexpr (CG) {
-                pm_n = lut[kOffPm + row_q(wn)];
-                px_n = lut[kOffPx + row_q(wn)];
-                m_n = mt[row_rc(wn) * 64 + lane];
-            }
             const bool last = SUM && i == R;
             const int lim = last ? lim0 : 0;
             if (last) {
@@ -357,31 +400,48 @@ __device__ __forceinline__ void run_seg(const T* __restrict__ lut, const SegStep
                 k.px = px_n;
                 mrow = m_n;
             }
-            wc = wn;
-            wn = wnn;
         }
+        wc = wn;
     };
+    // Everything the prologue loaded is in registers before the sweep: the
+    // wait-count pass then sees only the sweep's own prefetches in flight and
+    // waits on each word exactly PD steps after its load (s_waitcnt vmcnt(0)).
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    // Groups of PD steps (phases 0..PD-1); the sum variant from the group that
+    // holds step rmin on (extra steps past nsteps find every lane inactive).
     int kk = 1;
-    for (; kk < st.rmin; ++kk) step(kk, std::false_type{});
-    for (; kk <= st.nsteps; ++kk) step(kk, std::true_type{});
+    for (; kk + PD - 1 < st.rmin; kk += PD)
+        for_phases<0, PD>([&](auto ph) { step(kk + decltype(ph)::value, std::false_type{}, ph); });
+    for (; kk <= st.nsteps; kk += PD)
+        for_phases<0, PD>([&](auto ph) { step(kk + decltype(ph)::value, std::true_type{}, ph); });
 }
 
 // Two compiled paths per width: EQ (the reference's constant 'I'/'I'/'+' gap
 // qualities) and the generic per-row path (any gap qualities).
 template <typename T, int BC>
-__device__ __forceinline__ void run_seg_bc(const T* __restrict__ lut, const SegSteps& st, int lane, int s,
-                                           const LaneCtx& cx, T T0, T& sumM, T& sumX, uint2* __restrict__ mt,
-                                           bool wave_eq)
+__device__ __forceinline__ void run_seg_bc(const T* __restrict__ lut, const T* __restrict__ slut, const SegSteps& st,
+                                           int lane, int s, const LaneCtx& cx, T T0, T& sumM, T& sumX,
+                                           uint2* __restrict__ mt, bool wave_eq)
 {
     if (wave_eq)
-        run_seg<T, BC, true, true>(lut, st, lane, s, cx, T0, sumM, sumX, mt);
+        run_seg<T, BC, true, true>(lut, slut, st, lane, s, cx, T0, sumM, sumX, mt);
     else
-        run_seg<T, BC, false, false>(lut, st, lane, s, cx, T0, sumM, sumX, mt);
+        run_seg<T, BC, false, false>(lut, slut, st, lane, s, cx, T0, sumM, sumX, mt);
+}
+
+// The prior tables [ph2pr | pm | px | gapm] (luts.hpp) in LDS: the per-row
+// prior lookups of the segmented kernels read them there.
+constexpr int kSlutLen = kOffMM;
+template <typename T>
+__device__ __forceinline__ void load_slut(T* __restrict__ slut, const T* __restrict__ lut)
+{
+    for (int t = threadIdx.x; t < kSlutLen; t += blockDim.x) slut[t] = lut[t];
+    __syncthreads();
 }
 
 // Block widths of fp32 column-segmented waves (LaneWave.ncols of a seg wave).
 #define HC_SEG_WIDTHS(X) \
-    X(16) X(20) X(24) X(28) X(32) X(36) X(40) X(44) X(48) X(52) X(56) X(60) X(64)
+    X(8) X(10) X(12) X(14) X(16) X(20) X(24) X(28) X(32) X(36) X(40) X(44) X(48) X(52) X(56) X(60) X(64)
 
 // Wave metadata is wave-uniform: pin it to SGPRs so loops and switches are
 // scalar branches.
@@ -446,6 +506,8 @@ __global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
 template <int OCC>
 __global__ __launch_bounds__(256, OCC) void phmm_seg_kernel(LaneArgs a)
 {
+    __shared__ float slut[kSlutLen];
+    load_slut(slut, a.lut);
     const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (wid >= a.n_waves) return;
     const int lane = threadIdx.x & 63;
@@ -489,7 +551,7 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg_kernel(LaneArgs a)
     float sumM = 0.f, sumX = 0.f;
     switch (bc) {
 #define HC_SEG_CASE(W) \
-    case W: run_seg_bc<float, W>(a.lut, st, lane, s, cx, T0, sumM, sumX, mt, wave_eq); break;
+    case W: run_seg_bc<float, W>(a.lut, slut, st, lane, s, cx, T0, sumM, sumX, mt, wave_eq); break;
         HC_SEG_WIDTHS(HC_SEG_CASE)
 #undef HC_SEG_CASE
     default: break;
@@ -593,6 +655,8 @@ template <int OCC>
 __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
 {
     __shared__ uint2 mtab[4][5 * 64];
+    __shared__ double slut[kSlutLen];
+    load_slut(slut, a.lut);
     uint2* mt = mtab[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     const Seg64Plan* __restrict__ p = a.plan;
@@ -620,9 +684,9 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
         const bool wave_eq = __builtin_amdgcn_ballot_w64(!read_eq(w1)) == 0;
         double sumM = 0.0, sumX = 0.0;
         switch (bc) {
-        case 8: run_seg_bc<double, 8>(a.lut, st, lane, s, cx, T0, sumM, sumX, mt, wave_eq); break;
-        case 16: run_seg_bc<double, 16>(a.lut, st, lane, s, cx, T0, sumM, sumX, mt, wave_eq); break;
-        default: run_seg_bc<double, 32>(a.lut, st, lane, s, cx, T0, sumM, sumX, mt, wave_eq); break;
+        case 8: run_seg_bc<double, 8>(a.lut, slut, st, lane, s, cx, T0, sumM, sumX, mt, wave_eq); break;
+        case 16: run_seg_bc<double, 16>(a.lut, slut, st, lane, s, cx, T0, sumM, sumX, mt, wave_eq); break;
+        default: run_seg_bc<double, 32>(a.lut, slut, st, lane, s, cx, T0, sumM, sumX, mt, wave_eq); break;
         }
         if (owner) a.raw_out[pid] = sumM + sumX;
         __builtin_amdgcn_wave_barrier();   // the next wave's match table reuses mt
@@ -670,6 +734,13 @@ bool seg_width_ok(int bc)
         return true;
     default: return false;
     }
+}
+
+int seg_width_ceil(int bc)
+{
+    for (int w = bc < kSegMinBC ? kSegMinBC : bc; w <= kSegMaxBC; ++w)
+        if (seg_width_ok(w)) return w;
+    return -1;
 }
 
 hipError_t launch_lane_seg_f32(const LaneArgs& a, hipStream_t s)

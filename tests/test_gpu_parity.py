@@ -243,6 +243,23 @@ def test_seg_widths_and_gap_modes(engine, oracle_lib, monkeypatch, gaps, seg):
     assert_same(res, oracle_lib.pairs(b, nthreads=16), f"seg={seg}/{gaps}")
 
 
+@pytest.mark.parametrize("gaps", ["eq", "per_base"])
+@pytest.mark.parametrize("cap", [8, 10, 12, 14])
+def test_narrow_seg_widths(engine, oracle_lib, monkeypatch, gaps, cap):
+    """The narrow block widths small batches use (BC 8-14: up to 64 lanes per
+    pair, R + 63 steps) forced through the width cap, bit-exact against the
+    oracle on both cell paths."""
+    monkeypatch.setenv("HC_PHMM_SEG_CAP", str(cap))
+    b = W.generate(3000, (10, 900), (5, 250), 0.02, seed=12 + cap)
+    if gaps == "per_base":
+        rng = np.random.default_rng(cap)
+        n = len(b["ins"])
+        b["ins"][:] = rng.integers(33 + 5, 33 + 60, n, dtype=np.uint8)
+        b["dels"][:] = rng.integers(33 + 5, 33 + 60, n, dtype=np.uint8)
+        b["gcp"][:] = rng.integers(33 + 5, 33 + 30, n, dtype=np.uint8)
+    assert_same(engine.pairs(b), oracle_lib.pairs(b, nthreads=16), f"cap={cap}/{gaps}")
+
+
 def test_repeated_runs_reuse_rescue_counters(engine, oracle_lib):
     """A prepared batch run many times: the fp32 pass appends to one of two
     rescue counters by run parity and the rescue pass zeroes the other for the
