@@ -370,6 +370,7 @@ struct Part {
     Seg64Plan* d_plan = nullptr;
     int64_t n_wide = 0;
     int* d_count = nullptr;
+    int inker_limit = 0;   // in-wave rescues allowed in the last run
     int parity = 0;
     char* dev_base = nullptr;
     Slot* slot = nullptr;         // borrowed workspace (jobs), else dev_base is owned
@@ -1124,7 +1125,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const size_t o_hapw = L.take(sizeof(uint32_t) * (size_t(hap_w[size_t(nh)]) + 1));
     const size_t o_res = L.take(res_bytes);
     const size_t o_list = L.take(sizeof(int) * n1);
-    const size_t o_count = L.take(2 * sizeof(int));
+    const size_t o_count = L.take(4 * sizeof(int));   // rescue list counters, in-wave rescue counters (by run parity)
     const size_t o_sorted = L.take(sizeof(int) * n1);
     const size_t o_big = L.take(sizeof(int) * n1);
     const size_t o_bigc = L.take(sizeof(int));
@@ -1194,7 +1195,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     auto enqueue = [&]() -> int {
         for (auto& e : b->pack_ev) HIP_TRY(hipEventCreate(&e));
         HIP_TRY(hipMemcpyAsync(dev, host, upload, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemsetAsync(b->d_count, 0, 2 * sizeof(int), s));
+        HIP_TRY(hipMemsetAsync(b->d_count, 0, 4 * sizeof(int), s));
         HIP_TRY(hipEventRecord(b->pack_ev[0], s));
         HIP_TRY(launch_pack_reads(reinterpret_cast<const uint8_t*>(dev + o_bases),
                                   reinterpret_cast<const uint8_t*>(dev + o_quals),
@@ -1258,6 +1259,12 @@ int run_part(Part* b, hipStream_t s)
         a.rescue_list = b->d_list;
         a.rescue_count = count;
         a.raw64_zero = b->d_raw64;
+        a.lut64 = dv.lut_d;
+        if (env_i64("HC_PHMM_RESCUE_IN_WAVE", 1) != 0) {
+            a.inker_count = b->d_count + 2 + par;
+            a.inker_limit = int(std::max<int64_t>(0, env_i64("HC_PHMM_RESCUE_IN_WAVE_MAX", int64_t(4) * 4 * dv.n_cu)));
+        }
+        b->inker_limit = a.inker_limit;
         b->launch_waves += b->lane_waves;
         const int n_one = b->lane_waves - b->n_seg_waves;
         const bool fork = b->n_seg_waves > 0 && n_one > 0;
@@ -1315,6 +1322,7 @@ int run_part(Part* b, hipStream_t s)
         r.list = b->d_list;
         r.count = count;
         r.count_reset = b->d_count + (par ^ 1);
+        r.inker_reset = b->d_count + 2 + (par ^ 1);
         r.sorted = b->d_sorted;
         r.big = b->d_big;
         r.big_count = b->d_big_count;
@@ -1937,9 +1945,10 @@ int hc_phmm_batch_stats(hc_phmm_batch* b, hc_phmm_stats* st)
             st->kernel_ms_f64 = std::max(st->kernel_ms_f64, sc / double(p->ev_used));
             st->run_ms = std::max(st->run_ms, (sa + sc) / double(p->ev_used));
             p->ev_used = 0;
-            int cnt = 0;
-            HIP_TRY(hipMemcpy(&cnt, p->d_count + (p->parity ^ 1), sizeof(int), hipMemcpyDeviceToHost));
-            st->n_rescued += cnt;
+            int cnt[4] = {};
+            HIP_TRY(hipMemcpy(cnt, p->d_count, sizeof(cnt), hipMemcpyDeviceToHost));
+            // in-wave attempts past the limit were appended to the list instead
+            st->n_rescued += cnt[p->parity ^ 1] + std::min(cnt[2 + (p->parity ^ 1)], p->inker_limit);
         }
     }
     return HC_PHMM_OK;

@@ -81,7 +81,16 @@ struct LaneArgs {
     int* rescue_list;
     int* rescue_count;
     double* raw64_zero;       // as DiagArgs::raw64_zero
+    // Rescue inside the fp32 pass (column-segmented waves): a wave with at most
+    // two rescued pairs of H <= kInWaveRescueMaxH recomputes them in fp64 itself
+    // (all 64 lanes on one pair) while the rest of the pass runs, instead of
+    // appending them to rescue_list; at most inker_limit per run (counter
+    // inker_count, null = off).
+    const double* lut64;
+    int* inker_count;
+    int inker_limit;
 };
+constexpr int kInWaveRescueMaxH = 512;   // one pair over 64 lanes of 8 columns
 // Variants of the one-lane kernel (lane_kernel.hip kVariants): pairs per lane
 // P (1), register block width in columns, and the waves per SIMD the register
 // allocation targets. Variant 0 is the default.
@@ -119,6 +128,7 @@ struct Seg64Args {
     const int* list;          // rescue list (fp32 pass, arbitrary order)
     const int* count;         // its length
     int* count_reset;         // the other run parity's counter, zeroed for the next run
+    int* inker_reset;         // the other run parity's in-wave rescue counter, likewise
     int* sorted;              // list in class order (n entries)
     int* big;                 // class 7 pairs
     int* big_count;

@@ -500,6 +500,47 @@ __global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
     if (active) emit(a, pid, sumM + sumX);
 }
 
+// The fp64 rescue (intel_pairhmm.hpp:137-139) of the pairs this wave's fp32
+// pass flagged (`todo`: their owner lanes). A wave with at most two, each with
+// H <= kInWaveRescueMaxH, recomputes them itself while the rest of the pass
+// runs — one pair at a time over the whole wave (8 columns per lane, the
+// same run_seg in double) — so a batch with a few rescues (S2: ~2e-5 of
+// the pairs) needs no separate latency-bound pass after the fp32 kernel. The
+// others are appended to the rescue list for that pass.
+__device__ __forceinline__ void rescue_in_wave(const LaneArgs& a, uint64_t todo, int pid, int lane,
+                                            uint2* __restrict__ mt)
+{
+    const bool few = a.inker_count != nullptr && __popcll(todo) <= 2;
+    while (todo) {
+        const int l = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        const int rp = __builtin_amdgcn_readlane(pid, l);
+        const PairDesc pd = a.pairs[rp];
+        const int R = __builtin_amdgcn_readfirstlane(pd.y), H = __builtin_amdgcn_readfirstlane(pd.w);
+        bool here = few && H <= kInWaveRescueMaxH;
+        if (here) {
+            int c = 0;
+            if (lane == 0) c = atomicAdd(a.inker_count, 1);
+            here = __builtin_amdgcn_readfirstlane(c) < a.inker_limit;
+        }
+        if (!here) {
+            if (lane == l) a.rescue_list[atomicAdd(a.rescue_count, 1)] = rp;
+            continue;
+        }
+        const LaneCtx cx{a.rows + __builtin_amdgcn_readfirstlane(pd.x), a.hapw + __builtin_amdgcn_readfirstlane(pd.z),
+                         R, H};
+        const int nb = (H + 7) / 8;
+        const SegSteps st{R, R, R + nb - 1};
+        const uint32_t w1 = cx.rrow[0];
+        const double T0 = row0_t<double>(a.lut64, w1, H);
+        const bool eq = read_eq(w1);
+        double sM = 0.0, sX = 0.0;
+        run_seg_bc<double, 8>(a.lut64, a.lut64, st, lane, lane, cx, T0, sM, sX, mt, eq);
+        if (lane == nb - 1) a.raw64_zero[rp] = sM + sX;
+        __builtin_amdgcn_wave_barrier();   // the next pair rewrites mt
+    }
+}
+
 // Column-segmented fp32 waves (host-planned). The wave's npairs pairs are the
 // slots slot0 .. slot0+npairs-1; pair g takes nb_g = ceil(H_g / BC) consecutive
 // lanes in slot order. Lanes past the last group idle (s = 0, no output).
@@ -556,7 +597,17 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg_kernel(LaneArgs a)
 #undef HC_SEG_CASE
     default: break;
     }
-    if (owner) emit(a, pid, sumM + sumX);
+    // fp32 result and rescue decision (intel_pairhmm.hpp:133-139).
+    bool resc = false;
+    if (owner) {
+        const float raw = sumM + sumX;
+        resc = raw < 1e-28f;   // MIN_ACCEPTED, pairhmm_common.h:16
+        a.raw_out[pid] = raw;
+        a.rescue_flag[pid] = resc;
+        if (!resc) a.raw64_zero[pid] = 0.0;
+    }
+    const uint64_t todo = __builtin_amdgcn_ballot_w64(resc);
+    if (todo) rescue_in_wave(a, todo, pid, lane, mt);
 }
 
 // ---------------------------------------------------------------------------
@@ -594,6 +645,7 @@ __global__ __launch_bounds__(1024) void rescue_plan_kernel(Seg64Args a)
     if (t == 0) {
         lanes_sh = 0;
         *a.count_reset = 0;
+        *a.inker_reset = 0;
     }
     __syncthreads();
     // Width: 32 unless the lanes at width 32 give fewer than min_lanes

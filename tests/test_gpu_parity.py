@@ -274,12 +274,16 @@ def test_repeated_runs_reuse_rescue_counters(engine, oracle_lib):
     bt.close()
 
 
+@pytest.mark.parametrize("in_wave", ["on", "off"])
 @pytest.mark.parametrize("shape", ["short_list", "mid_list", "long_list", "wide_haps"])
-def test_fp64_rescue_tiers(engine, oracle_lib, shape):
+def test_fp64_rescue_tiers(engine, oracle_lib, monkeypatch, shape, in_wave):
     """The fp64 rescue pass is planned on the device: block width 8 / 16 / 32
     by rescue-list size (a short list is latency-bound), pairs binned into
     2^k-lane classes, haps too wide for 64 blocks of 32 on the anti-diagonal
-    fp64 kernel. High substitution rates force most pairs into rescue."""
+    fp64 kernel. High substitution rates force most pairs into rescue. With
+    in_wave on, fp32 waves holding one or two rescued pairs (H <= 1024)
+    recompute them themselves (short_list is mostly that path)."""
+    monkeypatch.setenv("HC_PHMM_RESCUE_IN_WAVE", "1" if in_wave == "on" else "0")
     n, h, r = {"short_list": (40, (300, 900), (100, 250)),
                "mid_list": (1500, (600, 1100), (150, 250)),
                "long_list": (4500, (1000, 1200), (150, 250)),
@@ -289,3 +293,29 @@ def test_fp64_rescue_tiers(engine, oracle_lib, shape):
     assert ref["rescued"].sum() > n // 2
     res = engine.pairs(b)
     assert_same(res, ref, shape)
+
+
+def test_in_wave_rescue_on_s2_shard(engine, oracle_lib):
+    """S2's rare rescues (a 125k-pair shard: about two) are recomputed inside
+    the fp32 pass by the waves that flag them: every rescued pair, plus a
+    sample, equals the oracle; the in-wave cap forces the rest to the list."""
+    b = W.config("S2", 125_000)
+    res = engine.pairs(b)
+    resc = np.flatnonzero(res["rescued"])
+    assert len(resc) > 0
+    idx = np.union1d(resc, np.random.default_rng(3).choice(125_000, 500, replace=False))
+    assert_same({k: res[k][idx] for k in res}, oracle_lib.pairs(W.subset(b, idx), nthreads=16), "S2 in-wave")
+
+
+def test_in_wave_rescue_cap(engine, oracle_lib, monkeypatch):
+    """With the per-run cap at 1 only the first flagged pair is recomputed in
+    its wave; the others go through the rescue list. Same bits either way,
+    and the rescue count is exact."""
+    monkeypatch.setenv("HC_PHMM_RESCUE_IN_WAVE_MAX", "1")
+    b = W.generate(200, (200, 700), (100, 250), 0.08, seed=23)
+    ref = oracle_lib.pairs(b, nthreads=16)
+    bt = engine.Batch(b)
+    bt.run()
+    assert_same(bt.results(), ref, "cap 1")
+    assert bt.stats().n_rescued == int(ref["rescued"].sum()) > 2
+    bt.close()
