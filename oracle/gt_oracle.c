@@ -47,6 +47,12 @@ double hco_approx_log10_sum_log10(double a, double b)
 void hco_gt_site(const double* L, int n_haps, const int32_t* keep, int n_keep, const int32_t* hap_allele,
                  int n_alleles, double* gl, int32_t* gt_index, int32_t* gq)
 {
+    hco_gt_site_with(L, n_haps, keep, n_keep, hap_allele, n_alleles, gl, gt_index, gq, hco_approx_log10_sum_log10);
+}
+
+void hco_gt_site_with(const double* L, int n_haps, const int32_t* keep, int n_keep, const int32_t* hap_allele,
+                      int n_alleles, double* gl, int32_t* gt_index, int32_t* gq, double (*approx)(double, double))
+{
     const double log10_2 = log10(2.0);   /* std::log10(2), genotyper.hpp:280,321 */
     double* al = (double*)malloc(sizeof(double) * (size_t)(n_keep > 0 ? n_keep : 1) * (size_t)n_alleles);
     /* marginal_likelihoods (:245-264): max over the haplotypes of each allele,
@@ -68,7 +74,7 @@ void hco_gt_site(const double* L, int n_haps, const int32_t* keep, int n_keep, c
             double acc = 0.0;
             for (int r = 0; r < n_keep; ++r) {
                 const double* x = &al[(size_t)r * n_alleles];
-                acc += a1 == a2 ? x[a1] + log10_2 : hco_approx_log10_sum_log10(x[a1], x[a2]);
+                acc += a1 == a2 ? x[a1] + log10_2 : approx(x[a1], x[a2]);
             }
             gl[g] = acc - (double)n_keep * log10_2;
         }

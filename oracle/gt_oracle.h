@@ -33,6 +33,10 @@ double hco_approx_log10_sum_log10(double a, double b);
  * genotype and its quality (capped at 99). */
 void hco_gt_site(const double* L, int n_haps, const int32_t* keep, int n_keep, const int32_t* hap_allele,
                  int n_alleles, double* gl, int32_t* gt_index, int32_t* gq);
+/* The same with the approximate_log10_sum_log10 implementation passed in (e.g.
+ * the reference's own, compiled in oracle/_ref/libref_math.so). */
+void hco_gt_site_with(const double* L, int n_haps, const int32_t* keep, int n_keep, const int32_t* hap_allele,
+                      int n_alleles, double* gl, int32_t* gt_index, int32_t* gq, double (*approx)(double, double));
 
 #ifdef __cplusplus
 }
