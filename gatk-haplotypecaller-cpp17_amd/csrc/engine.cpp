@@ -789,7 +789,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     }, 1 << 14);
     // Column-segmented waves (lane_kernel.hip run_seg): a pair gets nb lanes of
     // BC columns, BC from the compiled widths, choosing between nb0 =
-    // ceil(H/cap) and nb0 + 1 lanes by modelled cost nb*BC*(R + nb - 1). The
+    // ceil(H/cap) and nb0 + 1 lanes by modelled instructions (below). The
     // width cap minimises the modelled pass time: the waves one SIMD runs
     // (at least 2: a lone wave issues at half rate) times a wave's modelled
     // instructions (R + nb - 1 steps of 13 per column + ~30). Large batches get the widest cap (least
@@ -797,6 +797,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     // the width that balances waves per SIMD against steps per wave (measured
     // on MI355X: S1 10k x 101x150 best at 16, S1w 10k x 101x250 at 24).
     int cap = kSegMaxBC;
+    bool few_waves = false;   // the pass gives each SIMD at most ~3 waves: latency-bound, prefer more lanes
     {
         const int64_t forced = env_i64("HC_PHMM_SEG_CAP", 0);
         if (forced > 0) {
@@ -810,6 +811,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
                 if (c == 0 || est < best * 0.98) {
                     best = est;
                     cap = kCaps[c];
+                    few_waves = waves <= 3.0 * simds;
                 }
             }
         }
@@ -817,6 +819,20 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     struct Cand {
         uint8_t bc[2], nb[2];
     };
+    static const std::array<float, 65> kHalfWaste = [] {
+        std::array<float, 65> f{};
+        for (int nb = 1; nb <= 64; ++nb) f[size_t(nb)] = std::sqrt(64.f / float((64 / nb) * nb));
+        return f;
+    }();
+    // A pass with few waves per SIMD is latency-bound: its time is one wave's,
+    // so the candidate with the shorter wave wins there (S1: 11 lanes of 14
+    // columns beat 10 of 16; S1w: 12 of 22 beat 11 of 24).
+    static const std::array<float, 65> kPerLane = [] {
+        std::array<float, 65> f{};
+        for (int nb = 1; nb <= 64; ++nb) f[size_t(nb)] = 1.f / float(nb);
+        return f;
+    }();
+    const float* waste = few_waves ? kPerLane.data() : kHalfWaste.data();
     static_assert(sizeof(Cand) == sizeof(uint32_t), "Cand packs into a word");
     grow(S.hcand, size_t(nh));
     Cand* hcand = reinterpret_cast<Cand*>(S.hcand.data());
@@ -873,9 +889,16 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             if (cl == 0) {
                 ++cn0;
                 const Cand cd = cand[h];
-                const int c0 = int(cd.nb[0]) * cd.bc[0] * (R + cd.nb[0] - 1);
-                const int c1 = int(cd.nb[1]) * cd.bc[1] * (R + cd.nb[1] - 1);
-                const int q = c1 < c0 ? 1 : 0;
+                // modelled wave instructions: nb lanes x (13 per column + 26 per
+                // step) x (R + nb - 1) steps, times half the lane waste of a
+                // wave of such pairs alone (floor(64 / nb) groups): uniform
+                // batches pack like that, mixed ones fill the gaps with others;
+                // with few waves, the wave's own time (per lane)
+                auto cost = [&](int q) {
+                    const int nb = cd.nb[q];
+                    return float(nb * (13 * cd.bc[q] + 26) * (R + nb - 1)) * waste[nb];
+                };
+                const int q = cost(1) < cost(0) ? 1 : 0;
                 bco[k] = cd.bc[q];
                 nbo[k] = cd.nb[q];
                 rlo = R < rlo ? R : rlo;

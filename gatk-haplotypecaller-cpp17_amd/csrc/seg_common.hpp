@@ -1,0 +1,411 @@
+// Device building blocks shared by the column-segmented PairHMM kernels
+// (lane_kernel.hip: phmm_seg_kernel, phmm_seg64_kernel, the one-lane kernel;
+// chain_kernel.hip: phmm_chain_kernel): the cell update in the reference's
+// operation order, the per-row constants, DPP hand-offs, prefetch depth.
+// Same semantics as compute_full_prob_avx{s,d} (avx-pairhmm-template.h:210-346).
+#pragma once
+#include <type_traits>
+
+#include "device_common.hpp"
+#include "kernels.hpp"
+#include "luts.hpp"
+
+namespace hcphmm {
+namespace seg {
+
+template <typename T> __device__ __forceinline__ T initial_value();
+template <> __device__ __forceinline__ float initial_value<float>() { return 0x1p120f; }    // Context.h:149
+template <> __device__ __forceinline__ double initial_value<double>() { return 0x1p1020; }  // Context.h:109
+
+template <typename T>
+struct RowConst {
+    T pm, px;        // prior: 1 - ph2pr[q], ph2pr[q] / 3          (this row)
+    T my, yy;        // Y transitions: ph2pr[d], ph2pr[c]           (this row)
+    T mm, g, mx, xx; // transitions into the NEXT row: mm, 1 - ph2pr[c], ph2pr[i], ph2pr[c]
+    int rc;          // read base code of this row
+};
+
+// initializeVectors / stripeINITIALIZATION (avx-pairhmm-template.h:83-177):
+// wc = this row's packed word, wn = the next row's.
+template <typename T>
+__device__ __forceinline__ void row_const(const T* __restrict__ lut, uint32_t wc, uint32_t wn, RowConst<T>& k)
+{
+    const T* __restrict__ ph2pr = lut + kOffPh2pr;
+    k.pm = lut[kOffPm + row_q(wc)];
+    k.px = lut[kOffPx + row_q(wc)];
+    k.my = ph2pr[row_d(wc)];
+    k.yy = ph2pr[row_c(wc)];
+    k.mm = lut[kOffMM + mm_idx(row_i(wn), row_d(wn))];
+    k.g = lut[kOffGapm + row_c(wn)];
+    k.mx = ph2pr[row_i(wn)];
+    k.xx = ph2pr[row_c(wn)];
+    k.rc = row_rc(wc);
+}
+
+// Prior of column bit `B` (MSB-first) of a match word: v_bfe_i32 (bit -> 0 /
+// -1) and one bit-select per 32-bit half (v_bitop3). The asm keeps the
+// compiler from turning it into and + cmp + cndmask.
+template <int B>
+__device__ __forceinline__ float prior_of(uint32_t w, float pm, float px)
+{
+    int t;
+    asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(t) : "v"(w), "i"(B));
+    return __int_as_float((t & __float_as_int(pm)) | (~t & __float_as_int(px)));
+}
+template <int B>
+__device__ __forceinline__ double prior_of(uint32_t w, double pm, double px)
+{
+    int t;
+    asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(t) : "v"(w), "i"(B));
+    const long long a = __double_as_longlong(pm), b = __double_as_longlong(px);
+    const unsigned lo = unsigned((t & int(a)) | (~t & int(b)));
+    const unsigned hi = unsigned((t & int(a >> 32)) | (~t & int(b >> 32)));
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// Column J of one row of one block; recursion unrolls the row at compile time.
+// M enters as M[i][c0+J+1] (= T_old[J-1] * prior). Before T[J] is overwritten,
+// its old value (the next column's diagonal) is consumed into the next M, so
+// the new T[J] can take the old one's register: no copies between rows.
+// mw0/mw1: the row's match words for block columns 1-32 / 33-64.
+// EQ: mx == my bitwise (insertion and deletion gap qualities equal on every
+// row: the reference's SAMRecord passes 'I' for both, sam.hpp:30-32), so the
+// product M*mx that feeds X[J] is also the M*my term of the next column's Y:
+// one multiply fewer per cell, the same rounded values. Ml then carries that
+// product instead of M.
+template <typename T, int BC, int J, int NC, bool SUM, bool EQ>
+__device__ __forceinline__ void cell(T (&Tt)[BC], T (&X)[BC], T M, T& Ml, T& Yl, uint32_t mw0, uint32_t mw1,
+                                     T pm, T px, const RowConst<T>& k, int lim, T& sumM, T& sumX)
+{
+    if constexpr (J < NC) {
+        T Mn = M;
+        if constexpr (J + 1 < NC)
+            Mn = Tt[J] * prior_of<31 - ((J + 1) & 31)>(((J + 1) >> 5) ? mw1 : mw0, pm, px);
+        const T Xc = X[J];
+        T Y;
+        if constexpr (EQ) {
+            const T Mx = M * k.mx;
+            Y = (J == 0) ? Yl : (Ml + Yl * k.yy);
+            Tt[J] = (M * k.mm + Xc * k.g) + Y * k.g;
+            X[J] = Mx + Xc * k.xx;
+            Ml = Mx;
+        } else {
+            Y = (J == 0) ? Yl : (Ml * k.my + Yl * k.yy);
+            Tt[J] = (M * k.mm + Xc * k.g) + Y * k.g;
+            X[J] = M * k.mx + Xc * k.xx;
+            Ml = M;
+        }
+        if constexpr (SUM) {
+            const bool c = J < lim;   // column c0+J+1 <= H on the pair's last row
+            sumM = sumM + (c ? M : T(0));
+            sumX = sumX + (c ? Xc : T(0));
+        }
+        Yl = Y;
+        cell<T, BC, J + 1, NC, SUM, EQ>(Tt, X, Mn, Ml, Yl, mw0, mw1, pm, px, k, lim, sumM, sumX);
+    }
+}
+
+// Y entering the column after the last one of a row segment: Ml*my + Yl*yy
+// (EQ: Ml already holds M*mx = M*my).
+template <bool EQ, typename T>
+__device__ __forceinline__ T y_next(T Ml, T Yl, T my, T yy)
+{
+    if constexpr (EQ)
+        return Ml + Yl * yy;
+    else
+        return Ml * my + Yl * yy;
+}
+
+struct LaneCtx {
+    const uint32_t* rrow;   // the read's packed rows
+    const uint32_t* hw;     // the hap's match table
+    int R, H;
+};
+
+// Row-0 diagonal T0 = (0*mm + 0*gapm) + (INITIAL/H)*gapm with row 1's
+// constants (avx-pairhmm-template.h:160-166: Y[0][j] = INITIAL / H).
+template <typename T>
+__device__ __forceinline__ T row0_t(const T* __restrict__ lut, uint32_t w1, int H)
+{
+    const T mm1 = lut[kOffMM + mm_idx(row_i(w1), row_d(w1))];
+    const T g1 = lut[kOffGapm + row_c(w1)];
+    const T initY = initial_value<T>() / T(H);
+    return (T(0) * mm1 + T(0) * g1) + initY * g1;
+}
+
+__device__ __forceinline__ LaneCtx pair_ctx(const PairDesc* pairs, const uint32_t* rows, const uint32_t* hapw,
+                                            int pid)
+{
+    const PairDesc pd = pairs[pid];
+    return LaneCtx{rows + pd.x, hapw + pd.z, pd.y, pd.w};
+}
+
+// Constant-gap tag of a read: bit 31 of its first row word (pack_reads_kernel).
+// EQ additionally needs insertion == deletion gap quality.
+__device__ __forceinline__ bool read_cg(uint32_t w1) { return (w1 >> 31) != 0; }
+__device__ __forceinline__ bool read_eq(uint32_t w1) { return read_cg(w1) && row_i(w1) == row_d(w1); }
+
+__device__ __forceinline__ float from_left(float v)
+{
+    // DPP wave_shr:1: lane l receives lane l-1's v (lane 0 receives 0).
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ double from_left(double v)
+{
+    const long long x = __double_as_longlong(v);
+    const unsigned lo = unsigned(__builtin_amdgcn_update_dpp(0, int(x), 0x138, 0xf, 0xf, false));
+    const unsigned hi = unsigned(__builtin_amdgcn_update_dpp(0, int(x >> 32), 0x138, 0xf, 0xf, false));
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// Step bounds of a column-segmented wave (wave-uniform).
+struct SegSteps {
+    int rmax;     // rows swept by every lane
+    int rmin;     // first step that may need the row sums
+    int nsteps;   // max over the wave's pairs of R + nb - 1
+};
+
+// Rows of read words a lane keeps in flight (loaded PD steps before use). A
+// lone step of a narrow block is too short to cover a global load, so narrow
+// blocks prefetch deeper; the step loop is unrolled by PD so every word lands
+// in its own register and is not touched (no wait) until its step.
+#ifndef HC_SEG_DEEP
+#define HC_SEG_DEEP 1   // 0: one-step prefetch everywhere, prior tables read from global memory (A/B builds)
+#endif
+template <typename T, int BC>
+constexpr int seg_prefetch()
+{
+    if (!HC_SEG_DEEP) return 1;
+    return sizeof(T) == 8 ? (BC >= 16 ? 1 : 2) : (BC >= 32 ? 1 : (BC >= 16 ? 2 : 4));
+}
+
+// Call f(integral_constant<P>) for P = 0 .. N-1 (compile-time phases).
+template <int P, int N, typename F>
+__device__ __forceinline__ void for_phases(F&& f)
+{
+    if constexpr (P < N) {
+        f(std::integral_constant<int, P>{});
+        for_phases<P + 1, N>(f);
+    }
+}
+
+// The prior tables [ph2pr | pm | px | gapm] (luts.hpp) in LDS: the per-row
+// prior lookups of the segmented kernels read them there.
+constexpr int kSlutLen = kOffMM;
+template <typename T>
+__device__ __forceinline__ void load_slut(T* __restrict__ slut, const T* __restrict__ lut)
+{
+    for (int t = threadIdx.x; t < kSlutLen; t += blockDim.x) slut[t] = lut[t];
+    __syncthreads();
+}
+
+// Block widths of fp32 column-segmented waves (LaneWave.ncols of a seg wave).
+#ifndef HC_SEG_WIDTH_STEP2
+#define HC_SEG_WIDTH_STEP2 1   // 0: widths 16..64 in steps of 4 only (A/B builds)
+#endif
+#if HC_SEG_WIDTH_STEP2
+#define HC_SEG_WIDTHS(X)                                                                                       \
+    X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(22) X(24) X(26) X(28) X(30) X(32) X(34) X(36) X(38) X(40) X(42) \
+    X(44) X(46) X(48) X(50) X(52) X(54) X(56) X(58) X(60) X(62) X(64)
+#else
+#define HC_SEG_WIDTHS(X) \
+    X(8) X(10) X(12) X(14) X(16) X(20) X(24) X(28) X(32) X(36) X(40) X(44) X(48) X(52) X(56) X(60) X(64)
+#endif
+
+// A pair's nb column blocks of BC columns sit on nb consecutive lanes (a
+// "group"), lane s of the group owning columns s*BC+1 .. s*BC+BC on every row,
+// and lane s sweeps row i = k - s in step k — a one-row skew per block — so the
+// pair finishes in R + nb - 1 steps, with no carry buffer. Each step lane s
+// takes from lane s-1 (DPP wave_shr:1; ignored on a group's first lane):
+//   - the Y entering its first column on row i (lane s-1's row i, last step),
+//   - the right-edge T of row i-1, its first diagonal (two steps back: held
+//     one step in a register),
+//   - on row R, the running sums ΣM, ΣX, so the final sums are accumulated
+//     column by column left to right exactly as the reference does.
+// Lanes outside 1 <= i <= rmax (pipeline fill / drain) are masked off; columns
+// past H compute values that only flow right and are never summed.
+// A lane's match window: columns c0+1 .. c0+64 of the hap's match table
+// (rows of 32 bits, MSB first, kHapLead zero rows before), for each of the 5
+// read codes, into its LDS slots mt[code * 64 + lane].
+__device__ __forceinline__ void fill_window(uint2* __restrict__ mt, int lane, const uint32_t* __restrict__ hw, int H,
+                                            int c0)
+{
+    const int nwpad = (H + 31) / 32 + kHapLead;   // the trailing zero row
+    const int w0 = c0 / 32 + kHapLead, r = c0 & 31;
+    const int i0 = min(w0, nwpad), i1 = min(w0 + 1, nwpad), i2 = min(w0 + 2, nwpad);
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+        const uint64_t x01 = (uint64_t(hw[i0 * 5 + c]) << 32) | hw[i1 * 5 + c];
+        const uint64_t x12 = (uint64_t(hw[i1 * 5 + c]) << 32) | hw[i2 * 5 + c];
+        mt[c * 64 + lane] = make_uint2(uint32_t((x01 << r) >> 32), uint32_t((x12 << r) >> 32));
+    }
+}
+
+template <typename T, int BC, bool CG, bool EQ>
+__device__ __forceinline__ void run_seg(const T* __restrict__ lut, const T* __restrict__ slut, const SegSteps& st,
+                                        int lane, int s, const LaneCtx& cx, T T0, T& sumM, T& sumX,
+                                        uint2* __restrict__ mt)
+{
+    constexpr int PD = seg_prefetch<T, BC>();
+    const int c0 = s * BC;
+    const int R = cx.R;
+    fill_window(mt, lane, cx.hw, cx.H, c0);
+    T Tt[BC], X[BC];
+#pragma unroll
+    for (int j = 0; j < BC; ++j) {
+        Tt[j] = T0;   // row 0
+        X[j] = T(0);
+    }
+    // wq[P]: the word of row i+1 (clamped to 1..R) at the steps of phase
+    // P = (k-1) mod PD, for every lane at every step; the loads are issued
+    // unconditionally so that each path has the same outstanding loads and
+    // the wait for a word is the one PD steps after its load.
+    uint32_t wc = cx.rrow[0];
+    uint32_t wq[PD];
+#pragma unroll
+    for (int P = 0; P < PD; ++P) wq[P] = cx.rrow[min(max(P + 2 - s, 1), R) - 1];
+    RowConst<T> k;
+    row_const<T>(lut, wc, cx.rrow[min(2, R) - 1], k);
+    uint2 mrow = mt[k.rc * 64 + lane];
+    T y_out = T(0), t_out = T(0);   // handed to lane s+1: Y past column c0+BC, T[BC-1] of the last row
+    T t_hold = T(0);                // lane s-1's right-edge T of the previous row
+    const int lim0 = cx.H - c0;     // columns of this block inside the hap (<= 0: none)
+    auto step = [&](int kk, auto sum_tag, auto ph_tag) {
+        constexpr bool SUM = decltype(sum_tag)::value;
+        constexpr int P = decltype(ph_tag)::value;
+        const int i = kk - s;
+        const uint32_t wn = wq[P];   // row i+1, loaded PD steps ago
+        T pm_n = T(0), px_n = T(0);
+        uint2 m_n = mrow;
+        int ridx = min(max(i + PD + 1, 1), R) - 1;   // the word needed PD steps from now
+        if constexpr (CG) {   // next row's prior constants (LDS) and match words
+            const int qo = row_q(wn), mo = row_rc(wn) * 64 + lane;
+            // Order the load after the last use of wn, so the word can land in
+            // wn's register (no register move, hence no wait, at the loop back edge).
+            asm volatile("" : "+v"(ridx) : "v"(qo), "v"(mo));
+            const T* __restrict__ pl = HC_SEG_DEEP ? slut : lut;
+            pm_n = pl[kOffPm + qo];
+            px_n = pl[kOffPx + qo];
+            m_n = mt[mo];
+        } else {
+            asm volatile("" : "+v"(ridx) : "v"(wn));
+        }
+        wq[P] = cx.rrow[ridx];
+        const T y_in = from_left(y_out);
+        const T t_in = from_left(t_out);
+        T sM_in = T(0), sX_in = T(0);
+        if constexpr (SUM) {
+            sM_in = from_left(sumM);
+            sX_in = from_left(sumX);
+        }
+        // Row 1's diagonal is row 0's T at every column; below that, lane
+        // s-1's right edge (column 0 for block 0: T[i][0] = 0 for i >= 1).
+        const T Tdiag = i == 1 ? T0 : (s ? t_hold : T(0));
+        const T Yl0 = s ? y_in : T(0);   // block 0: Y[i][1] = 0*my + 0*yy = 0
+        t_hold = t_in;
+        if (unsigned(i - 1) < unsigned(st.rmax)) {
+            if constexpr (!CG) {
+                row_const<T>(lut, wc, wn, k);
+                mrow = mt[k.rc * 64 + lane];
+            }
+            const bool last = SUM && i == R;
+            const int lim = last ? lim0 : 0;
+            if (last) {
+                sumM = s ? sM_in : T(0);
+                sumX = s ? sX_in : T(0);
+            }
+            T Ml = T(0), Yl = Yl0;
+            const T M0 = Tdiag * prior_of<31>(mrow.x, k.pm, k.px);
+            cell<T, BC, 0, BC, SUM, EQ>(Tt, X, M0, Ml, Yl, mrow.x, mrow.y, k.pm, k.px, k, lim, sumM, sumX);
+            y_out = y_next<EQ>(Ml, Yl, k.my, k.yy);
+            t_out = Tt[BC - 1];
+            if constexpr (CG) {
+                k.pm = pm_n;
+                k.px = px_n;
+                mrow = m_n;
+            }
+        }
+        wc = wn;
+    };
+    // Everything the prologue loaded is in registers before the sweep: the
+    // wait-count pass then sees only the sweep's own prefetches in flight and
+    // waits on each word exactly PD steps after its load (s_waitcnt vmcnt(0)).
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    // Groups of PD steps (phases 0..PD-1); the sum variant from the group that
+    // holds step rmin on (extra steps past nsteps find every lane inactive).
+    int kk = 1;
+    for (; kk + PD - 1 < st.rmin; kk += PD)
+        for_phases<0, PD>([&](auto ph) { step(kk + decltype(ph)::value, std::false_type{}, ph); });
+    for (; kk <= st.nsteps; kk += PD)
+        for_phases<0, PD>([&](auto ph) { step(kk + decltype(ph)::value, std::true_type{}, ph); });
+}
+
+// Two compiled paths per width: EQ (the reference's constant 'I'/'I'/'+' gap
+// qualities) and the generic per-row path (any gap qualities).
+template <typename T, int BC>
+__device__ __forceinline__ void run_seg_bc(const T* __restrict__ lut, const T* __restrict__ slut, const SegSteps& st,
+                                           int lane, int s, const LaneCtx& cx, T T0, T& sumM, T& sumX,
+                                           uint2* __restrict__ mt, bool wave_eq)
+{
+    if (wave_eq)
+        run_seg<T, BC, true, true>(lut, slut, st, lane, s, cx, T0, sumM, sumX, mt);
+    else
+        run_seg<T, BC, false, false>(lut, slut, st, lane, s, cx, T0, sumM, sumX, mt);
+}
+
+// The fp64 rescue (intel_pairhmm.hpp:137-139) of the pairs this wave's fp32
+// pass flagged (`todo`: their owner lanes). A wave with at most two, each with
+// H <= kInWaveRescueMaxH, recomputes them itself while the rest of the pass
+// runs — one pair at a time over the whole wave (8 columns per lane, the
+// same run_seg in double) — so a batch with a few rescues (S2: ~2e-5 of
+// the pairs) needs no separate latency-bound pass after the fp32 kernel. The
+// others are appended to the rescue list for that pass.
+// fp64 recompute of pair rp by the whole wave (H <= kInWaveRescueMaxH: 64
+// lanes of 8 columns), raw f64 sum to raw64_zero[rp].
+__device__ __forceinline__ void rescue_one(const LaneArgs& a, int rp, int lane, uint2* __restrict__ mt)
+{
+    const PairDesc pd = a.pairs[rp];
+    const int R = __builtin_amdgcn_readfirstlane(pd.y), H = __builtin_amdgcn_readfirstlane(pd.w);
+    const LaneCtx cx{a.rows + __builtin_amdgcn_readfirstlane(pd.x), a.hapw + __builtin_amdgcn_readfirstlane(pd.z), R,
+                     H};
+    const int nb = (H + 7) / 8;
+    const SegSteps st{R, R, R + nb - 1};
+    const uint32_t w1 = cx.rrow[0];
+    const double T0 = row0_t<double>(a.lut64, w1, H);
+    const bool eq = read_eq(w1);
+    double sM = 0.0, sX = 0.0;
+    run_seg_bc<double, 8>(a.lut64, a.lut64, st, lane, lane, cx, T0, sM, sX, mt, eq);
+    if (lane == nb - 1) a.raw64_zero[rp] = sM + sX;
+    __builtin_amdgcn_wave_barrier();   // the next pair rewrites mt
+}
+
+// Rescue pair rp in this wave if it qualifies and the run's in-wave budget
+// allows (wave-uniform), else append it to the rescue list (lane `owner_lane`).
+__device__ __forceinline__ void rescue_or_defer(const LaneArgs& a, bool few, int rp, int lane, int owner_lane,
+                                                uint2* __restrict__ mt)
+{
+    bool here = few && __builtin_amdgcn_readfirstlane(a.pairs[rp].w) <= kInWaveRescueMaxH;
+    if (here) {
+        int c = 0;
+        if (lane == 0) c = atomicAdd(a.inker_count, 1);
+        here = __builtin_amdgcn_readfirstlane(c) < a.inker_limit;
+    }
+    if (here)
+        rescue_one(a, rp, lane, mt);
+    else if (lane == owner_lane)
+        a.rescue_list[atomicAdd(a.rescue_count, 1)] = rp;
+}
+
+__device__ __forceinline__ void rescue_in_wave(const LaneArgs& a, uint64_t todo, int pid, int lane,
+                                               uint2* __restrict__ mt)
+{
+    const bool few = a.inker_count != nullptr && __popcll(todo) <= 2;
+    while (todo) {
+        const int l = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        rescue_or_defer(a, few, __builtin_amdgcn_readlane(pid, l), lane, l, mt);
+    }
+}
+
+}  // namespace seg
+}  // namespace hcphmm
