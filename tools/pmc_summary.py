@@ -71,6 +71,11 @@ def main():
     if dominant:
         summary["dominant_kernel"] = dominant
         summary["hbm_bytes_per_launch"] = summary["kernels"][dominant].get("hbm_bytes_per_launch")
+        if cells:
+            summary["cells"] = cells
+            k = summary["kernels"][dominant]
+            if "SQ_INSTS_VALU" in k:
+                summary["valu_lane_instr_per_cell"] = round(k["SQ_INSTS_VALU"] * 64 / cells, 3)
         if cells and summary["hbm_bytes_per_launch"]:
             summary["hbm_bytes_per_cell"] = summary["hbm_bytes_per_launch"] / cells
     with open(out, "w") as fh:
