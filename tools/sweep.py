@@ -40,7 +40,11 @@ def main():
     hcphmm.init(0)
     for wl in a.workloads:
         name, _, n = wl.partition(":")
-        b = W.config(name, int(n) if n else None)
+        if name == "region":   # region:NREADS:NHAPS, one cross product as flat pairs
+            nr, nh = (int(x) for x in n.split(":"))
+            b = W.region_flat(*W.region(n_reads=nr, n_haps=nh))
+        else:
+            b = W.config(name, int(n) if n else None)
         cells = W.cells(b)
         ref = None
         for st in settings:
