@@ -1145,7 +1145,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     Layout L;
     L.off = (upload + 255) & ~size_t(255);
     const size_t o_rows = L.take(sizeof(uint32_t) * (size_t(nrows) + 16));
-    const size_t o_hapw = L.take(sizeof(uint32_t) * (size_t(hap_w[size_t(nh)]) + 1));
+    const size_t o_hapw = L.take(sizeof(uint32_t) * (size_t(hap_w[size_t(nh)]) + 16));
     const size_t o_res = L.take(res_bytes);
     const size_t o_list = L.take(sizeof(int) * n1);
     const size_t o_count = L.take(4 * sizeof(int));   // rescue list counters, in-wave rescue counters (by run parity)

@@ -89,29 +89,8 @@ struct LaneArgs {
     const double* lut64;
     int* inker_count;
     int inker_limit;
-    // Chained waves (chain_kernel.hip): waves[] is unused, cwaves[n_waves] instead.
-    const struct ChainWave* cwaves;
-    const int* cpids;           // per wave, round-major: round t, group g at pid0 + t*G + g (-1: none)
-    const uint32_t* crounds;    // per wave and round: Rmax | Rmin << 16
 };
 
-// Chained column-segmented waves: a wave's lanes form G groups of nb lanes
-// (G = 64 / nb); group g runs T pairs back to back (rounds), lane s of a
-// group starting its next pair's row 1 the step after it finished the last
-// row of the previous one, so a pair's pipeline fill / drain (nb - 1 steps) is
-// paid once per wave instead of once per pair. The pairs of one round have
-// nearly equal R (the planner sorts by R): every lane switches pairs at the
-// same step of its own skewed timeline.
-constexpr int kChainMaxEntries = 256;   // T * G per wave
-constexpr int kChainMaxRounds = 64;
-constexpr int kChainRescueSlots = 4;    // rescued pairs a wave keeps for its own fp64 pass
-struct ChainWave {
-    int pid0;     // first entry of the wave in cpids
-    int r0;       // first entry of the wave in crounds
-    int shape;    // bc | nb << 8 | G << 16 | T << 24, bit 31: every read EQ (constant 'I'/'I'/'+'-like gaps)
-    int nsteps;   // sum over rounds of Rmax, + nb - 1
-};
-hipError_t launch_chain_f32(const LaneArgs& a, hipStream_t s);
 constexpr int kInWaveRescueMaxH = 512;   // one pair over 64 lanes of 8 columns
 // Variants of the one-lane kernel (lane_kernel.hip kVariants): pairs per lane
 // P (1), register block width in columns, and the waves per SIMD the register
