@@ -85,8 +85,8 @@ typedef struct hc_phmm_stats {
     double run_ms;          /* whole device pass, mean over n_runs           */
     int64_t n_launch_waves; /* waves launched by the fp32 pass               */
     int64_t n_runs;         /* runs since the previous stats() call          */
-    int64_t n_lane_pairs;   /* pairs on the lane kernels: chained, segmented or one lane per pair (rest: anti-diagonal) */
-    int64_t n_seg_waves;    /* column-segmented waves (chained and unchained): a pair over nb lanes */
+    int64_t n_lane_pairs;   /* pairs on the lane kernels: segmented or one lane per pair (rest: anti-diagonal) */
+    int64_t n_seg_waves;    /* column-segmented waves: a pair over nb lanes of BC columns */
     int64_t n_devices;      /* device slots the batch is split over                  */
     double pack_ms;         /* device packing of a new batch (rows + hap tables),
                                done once at create; max over devices               */
