@@ -748,6 +748,12 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     for (auto& x : lanes_at) x = 0;
     std::atomic<int64_t> wide_a{0};
     std::atomic<int> hmax_a{0};
+    // seg_width_ceil as a table (the planner calls it per hap and cap).
+    static const std::array<int8_t, kSegMaxBC + 1> kWidthCeil = [] {
+        std::array<int8_t, kSegMaxBC + 1> t{};
+        for (int x = 0; x <= kSegMaxBC; ++x) t[size_t(x)] = int8_t(seg_width_ceil(x));
+        return t;
+    }();
     // Modelled wave instructions at each cap (13 per column + ~30 per step,
     // R + nb - 1 steps at the batch's mean read length), for the cap choice.
     const double ravg = double(nrows) / double(std::max<int64_t>(nr, 1));
@@ -768,8 +774,8 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             hcls[size_t(h)] = uint8_t(cl);
             if (cl == 0)
                 for (int q = 0; q < kNCaps; ++q) {
-                    const int bc = seg_width_ceil((H + std::min(64, (H + kCaps[q] - 1) / kCaps[q]) - 1) /
-                                                  std::min(64, (H + kCaps[q] - 1) / kCaps[q]));
+                    const int nbq = std::min(64, (H + kCaps[q] - 1) / kCaps[q]);
+                    const int bc = kWidthCeil[size_t(std::min(kSegMaxBC, (H + nbq - 1) / nbq))];
                     const int nb = (H + bc - 1) / bc;
                     lanes[q] += m * nb;
                     work[q] += double(m) * nb * (ravg + nb - 1) * (13.0 * bc + 30.0);
@@ -844,7 +850,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             Cand c{};
             for (int q = 0; q < 2; ++q) {
                 const int nb = std::min(nb0 + q, 64);
-                const int bc = seg_width_ceil((H + nb - 1) / nb);
+                const int bc = kWidthCeil[size_t(std::min(kSegMaxBC, (H + nb - 1) / nb))];
                 c.bc[q] = uint8_t(bc);
                 c.nb[q] = uint8_t((H + bc - 1) / bc);
             }

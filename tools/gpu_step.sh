@@ -1,7 +1,8 @@
 set -o pipefail
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-for c in on off; do
-HC_PHMM_CHAIN=$c timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_WAIT_ANY --output-format csv -d gpurun_out/pmc_chain_$c -o run -- python3 tools/sweep.py S1w:1000000 --runs 2 > gpurun_out/pmc_chain_$c.log 2>&1 || exit 1
+for r in 1 2; do
+for lib in new old; do
+  if [ $lib = old ]; then export HC_PHMM_LIB=build_ab/libold.so; else unset HC_PHMM_LIB; fi
+  echo -n "$lib "; timeout -k 10 300 python -u tools/e2e_ab.py 2>> gpurun_out/e2e_ab.err || exit 1
 done
-echo ok
+done
