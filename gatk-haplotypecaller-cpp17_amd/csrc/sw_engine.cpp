@@ -118,6 +118,7 @@ struct hc_sw_batch {
     hc_sw_params params{};
     int overhang = 9, shortcut = 1;
     int fast = 0;
+    int profile = 0;
     char* dev = nullptr;
     SwPair* pairs = nullptr;
     int32_t* order = nullptr;
@@ -240,6 +241,15 @@ int create(int64_t n, const int64_t* ref_off, const int32_t* ref_len, const uint
     b->fast = fast_ok(params, overhang, b->n1max, b->n2max) ? 1 : 0;
     if (const char* e = std::getenv("HC_SW_GENERIC"))   // parity tests of the generic variant
         if (e[0] == '1') b->fast = 0;
+    // The fast path's optional substitution profile (HC_SW_PROFILE=1) holds
+    // score - open as int16. It saves the compare + select of every cell but
+    // its LDS rows halve the waves per CU; on W2/W3 the compare form is faster
+    // (8.7 vs 10.8 ms, 3.6 vs 3.9 ms on MI355X), so it is off by default.
+    const int64_t pm = int64_t(params.match) - params.open, pmm = int64_t(params.mismatch) - params.open;
+    b->profile = 0;
+    if (const char* e = std::getenv("HC_SW_PROFILE"))
+        if (e[0] == '1')
+            b->profile = b->fast && pm >= INT16_MIN && pm <= INT16_MAX && pmm >= INT16_MIN && pmm <= INT16_MAX;
 
     // One device allocation: descriptors, inputs, outputs, scratch.
     size_t off = 0;
@@ -337,6 +347,7 @@ int run(hc_sw_batch* b, hipStream_t s)
     d.n1max = b->n1max;
     d.n2max = b->n2max;
     d.fast = b->fast;
+    d.profile = b->profile;
     SwTraceArgs t{};
     t.pairs = b->pairs;
     t.res = b->res;

@@ -17,6 +17,20 @@
 // point among the last-row (LDS row buffer) and last-column (LDS) candidates
 // with the reference's tie-breaks, in the reference's anti-diagonal order.
 //
+// Fast path (the default when the host proves the cutoff inert): the same
+// cells and bits from fewer VALU issue slots. gfx950 issues v_add/v_sub at
+// full rate but v_max, DPP moves, v_alignbit, compares and any VALU op with an
+// SGPR operand at half rate (tools/ubench/op_rate.hip), so a lane keeps
+// E + extend, F + extend and H(i-1, j-1) + open (the previous step's vertical
+// open score), hands the lane below H + open rather than H (the vertical open
+// score arrives ready by DPP, the diagonal needs no add of its own), and keeps
+// the gap scores in VGPRs: 9 full-rate + 11 half-rate instructions per cell
+// (the first form: 11 + 11 plus 5 SGPR-operand adds). The match/mismatch
+// choice is a compare of the haplotype byte with the lane's seq1 byte, or, on
+// request (HC_SW_PROFILE=1), an int16 load from an LDS profile of
+// (score - open) per distinct seq1 byte and column; the profile's LDS halves
+// the waves per CU and loses on W2/W3.
+//
 // sw_trace_kernel: one wave per pair walks the backtrack from the end point
 // (getCIGAR's state machine), 64 cells per step along the current direction,
 // and writes run-length CIGAR elements.
@@ -162,6 +176,170 @@ __device__ __forceinline__ void stripe(Lane& L, int lane, int n2, int rb, bool r
     }
 }
 
+// ---- profile path ------------------------------------------------------
+struct PLane {
+    int h;    // H(i, j-1): this lane's last cell
+    int ex;   // E(i, j-1) + extend
+    int fx;   // F(i, j-1) + extend (read by the lane below by DPP)
+    int dg;   // H(i-1, j-1) + open: the previous step's vertical open score
+    uint32_t acc;
+};
+
+// One cell of MAIN_CODE (PairWiseSW.h:4-38) per lane, FAST semantics (see
+// step): hn0 = H(i-1,j-1) + score = dg + (score - open).
+template <int MODE, bool LASTW>
+__device__ __forceinline__ void pstep(PLane& L, int t, int lane, int n2, bool row_ok, int ho, int fxo, int sc,
+                                      int open, int extend, int* rowHo, int* rowF)
+{
+    const int eo = L.h + open;        // open_score_h: H(i, j-1) + open
+    const int fo = shr1(ho, eo);      // open_score_v: H(i-1, j) + open (lane 0: row buffer)
+    const int fe = shr1(fxo, L.fx);   // ext_score_v:  F(i-1, j) + extend
+    const int fn = max(fe, fo);
+    const int en = max(eo, L.ex);
+    const int hn0 = L.dg + sc;
+    const int hn1 = max(hn0, en);
+    const int hn = max(hn1, fn);
+    L.acc = __builtin_amdgcn_alignbit(L.acc, uint32_t(L.ex - eo), 31);
+    L.acc = __builtin_amdgcn_alignbit(L.acc, uint32_t(fe - fo), 31);
+    L.acc = __builtin_amdgcn_alignbit(L.acc, uint32_t(hn0 - en), 31);
+    L.acc = __builtin_amdgcn_alignbit(L.acc, uint32_t(hn1 - fn), 31);
+    L.dg = fo;
+    L.fx = fn + extend;
+    const int exn = en + extend;
+    if (MODE == kBulk) {
+        L.h = hn;
+        L.ex = exn;
+    } else if (MODE == kFill) {
+        const bool act = t >= lane;
+        L.h = act ? hn : L.h;
+        L.ex = act ? exn : L.ex;
+    } else if (MODE == kDrain) {
+        L.h = (t - lane < n2) ? hn : L.h;
+        L.ex = exn;
+    } else {
+        const bool act = unsigned(t - lane) < unsigned(n2);
+        L.h = act ? hn : L.h;
+        L.ex = act ? exn : L.ex;
+    }
+    // H(i, j-1) + open for column j - 1 = t - lane, F(i, j) + extend for column
+    // j: the last writer of each slot is the stripe's last row.
+    if (!LASTW || row_ok) {
+        rowHo[63 + t - lane] = eo;
+        rowF[64 + t - lane] = L.fx;
+    }
+}
+
+struct PGroupIn {
+    int ho[kGroup];    // lane 0's H(64s, j) + open
+    int fxo[kGroup];   // lane 0's F(64s, j) + extend
+    int sc[kGroup];    // score(j) - open for this lane's row
+};
+
+// Where a lane's score(j) - open comes from: the LDS profile row of its seq1
+// byte (PROF), or a compare of the haplotype byte with its seq1 byte.
+struct Scorer {
+    const int16_t* prow;   // PROF: prow[t] = score of the column computed at step t
+    const uint8_t* arow;   // compare: arow[t] = haplotype byte of that column
+    int rb;                // compare: this lane's seq1 byte (-1: no row)
+    int mp, mmp;           // compare: match - open, mismatch - open (VGPRs)
+};
+
+typedef const volatile __attribute__((address_space(3))) int LdsInt;
+typedef const volatile __attribute__((address_space(3))) int16_t LdsI16;
+typedef const volatile __attribute__((address_space(3))) uint8_t LdsU8;
+
+// Separate 32-bit loads (volatile: not merged into 64/128-bit tuples, whose
+// elements the register allocator will not reuse as the DPP destinations) and
+// one ds_read_i16 / ds_read_u8 per score (no SDWA extract, which issues at
+// half rate).
+template <bool PROF>
+__device__ __forceinline__ void pload(PGroupIn& g, int t0, LdsInt* rowHo, LdsInt* rowF, const Scorer& sr)
+{
+#pragma unroll
+    for (int k = 0; k < kGroup; ++k) {
+        g.ho[k] = rowHo[64 + t0 + k];
+        g.fxo[k] = rowF[64 + t0 + k];
+        if (PROF) {
+            g.sc[k] = ((LdsI16*)sr.prow)[t0 + k];
+        } else {
+            const int ab = ((LdsU8*)sr.arow)[t0 + k];
+            g.sc[k] = ab == sr.rb ? sr.mp : sr.mmp;
+        }
+    }
+}
+
+// A uniform value in a VGPR: a VALU operand read from an SGPR halves the issue
+// rate of v_add_u32 on gfx950 (tools/ubench/op_rate.hip).
+__device__ __forceinline__ int in_vgpr(int x)
+{
+    int v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(x));
+    return v;
+}
+
+template <int MODE, bool LASTW, bool PROF>
+__device__ __forceinline__ void pgroup(PLane& L, int t0, int lane, int n2, bool row_ok, int open, int extend,
+                                       int* rowHo, int* rowF, const Scorer& sr)
+{
+    PGroupIn g;
+    pload<PROF>(g, t0, (LdsInt*)rowHo, (LdsInt*)rowF, sr);
+#pragma unroll
+    for (int k = 0; k < kGroup; ++k)
+        pstep<MODE, LASTW>(L, t0 + k, lane, n2, row_ok, g.ho[k], g.fxo[k], g.sc[k], open, extend, rowHo, rowF);
+}
+
+template <bool LASTW, bool PROF>
+__device__ __forceinline__ void pstripe(PLane& L, int lane, int n2, bool row_ok, int T, uint32_t* btw, int open,
+                                        int extend, int* rowHo, int* rowF, const Scorer& sr)
+{
+    for (int t0 = 0; t0 < T; t0 += kGroup) {
+        const bool fill = t0 < kStripe, drain = t0 + kGroup > n2;
+        if (!fill && !drain)
+            pgroup<kBulk, LASTW, PROF>(L, t0, lane, n2, row_ok, open, extend, rowHo, rowF, sr);
+        else if (fill && drain)
+            pgroup<kBoth, LASTW, PROF>(L, t0, lane, n2, row_ok, open, extend, rowHo, rowF, sr);
+        else if (fill)
+            pgroup<kFill, LASTW, PROF>(L, t0, lane, n2, row_ok, open, extend, rowHo, rowF, sr);
+        else
+            pgroup<kDrain, LASTW, PROF>(L, t0, lane, n2, row_ok, open, extend, rowHo, rowF, sr);
+        btw[(t0 / kGroup) * kStripe + lane] = L.acc;
+    }
+}
+
+// Rank the distinct bytes of seq1 (the row bases): codeOf[b] = rank, alpha[rank]
+// = b. Returns the number of distinct bytes (wave-uniform).
+__device__ int build_alphabet(const uint8_t* s1, int n1, int lane, uint8_t* codeOf, uint8_t* alpha)
+{
+    reinterpret_cast<int*>(codeOf)[lane] = 0;
+    __syncthreads();
+    for (int x = lane; x < n1; x += 64) codeOf[s1[x]] = 1;
+    __syncthreads();
+    const uint32_t w = reinterpret_cast<const uint32_t*>(codeOf)[lane];
+    const int c0 = (w & 0xff) != 0, c1 = (w & 0xff00) != 0, c2 = (w & 0xff0000) != 0, c3 = (w >> 24) != 0;
+    const int cnt = c0 + c1 + c2 + c3;
+    int incl = cnt;   // inclusive prefix over lanes
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    const int K = __shfl(incl, 63);
+    int r = incl - cnt;
+    __syncthreads();
+    uint32_t out = 0;
+    const int cs[4] = {c0, c1, c2, c3};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (cs[q]) {
+            if (r < kProfCodes) alpha[r] = uint8_t(4 * lane + q);
+            out |= uint32_t(r & 0xff) << (8 * q);
+            ++r;
+        }
+    }
+    reinterpret_cast<uint32_t*>(codeOf)[lane] = out;
+    __syncthreads();
+    return K;
+}
+
 template <bool FAST>
 __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
 {
@@ -188,7 +366,12 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
     const int slots = row_slots(a.n2max);
     int* rowH = lds;
     int* rowF = rowH + slots;
-    uint8_t* altB = reinterpret_cast<uint8_t*>(rowF + fslots(a.n1max, a.n2max));   // 64 pads, columns, pads
+    uint8_t* tail = reinterpret_cast<uint8_t*>(rowF + fslots(a.n1max, a.n2max));
+    uint8_t* altB = tail;   // 64 pads, columns, pads (compare paths)
+    int16_t* prof = reinterpret_cast<int16_t*>(tail);   // profile path
+    const int PS = prof_slots(a.n2max);
+    uint8_t* codeOf = tail + dp_tail_bytes(a.n2max);
+    uint8_t* alpha = codeOf + 256;
     // H(i, n2) of every row goes to this pair's CIGAR-element scratch in HBM
     // (the trace kernel reuses it later); after the last stripe it is copied
     // into rowF, free by then, for the end-point scan.
@@ -196,7 +379,68 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
     const int open = a.open, extend = a.extend, ovh = a.overhang;
     const Scores sc{a.match, a.mismatch, open, extend};
     const int T = stripe_steps(n2);
+    const int nstripes = (n1 + kStripe - 1) / kStripe;
+    uint32_t* bt = a.bt + P.bt_off;
+    const int nw = T / kGroup;
+    int hofs = 0;   // the row buffer holds H + hofs
 
+    const int K = (FAST && a.profile) ? build_alphabet(s1, n1, lane, codeOf, alpha) : 0;
+    const bool use_prof = FAST && a.profile && K <= kProfCodes;
+    if (FAST) {
+        hofs = open;
+        // Row 0 in this path's form: H(0, j) + open, F(0, j) + extend.
+        for (int j = lane; j < kStripe + T + 2 * kGroup; j += 64) {
+            rowH[j] = (j >= 64 ? boundary(ovh, open, extend, j - 63) : 0) + open;
+            rowF[j] = kLow + extend;
+        }
+        if (use_prof) {
+            for (int c = 0; c < K; ++c) {
+                const int b = alpha[c];
+                for (int v = lane; v < PS; v += 64) {
+                    const int j = v - 63;
+                    const int x = (j >= 1 && j <= n2) ? ((s2[j - 1] == b ? a.match : a.mismatch) - open) : 0;
+                    prof[c * PS + v] = int16_t(x);
+                }
+            }
+        } else {
+            for (int c = lane; c < kStripe + T + kGroup; c += 64)
+                altB[c] = (c >= kStripe && c < kStripe + n2) ? s2[c - kStripe] : 0;
+        }
+        __syncthreads();
+        const int open_v = in_vgpr(open), extend_v = in_vgpr(extend);
+        Scorer sr;
+        sr.mp = in_vgpr(a.match - open);
+        sr.mmp = in_vgpr(a.mismatch - open);
+        for (int s = 0; s < nstripes; ++s) {
+            const int i = s * kStripe + lane + 1;
+            const bool row_ok = i <= n1;
+            PLane L;
+            L.h = boundary(ovh, open, extend, i);   // H(i, 0)
+            L.ex = kLow + extend;                    // E(i, 0) + extend (:199)
+            L.fx = kLow + extend;
+            L.dg = rowH[63];                         // lane 0: H(64s, 0) + open
+            L.acc = 0;
+            uint32_t* btw = bt + int64_t(s) * nw * kStripe;
+            const bool lastw = s == nstripes - 1 && (n1 % kStripe) != 0;
+            if (use_prof) {
+                const int code = row_ok ? int(codeOf[s1[i - 1]]) : 0;
+                sr.prow = prof + code * PS + 64 - lane;
+                if (lastw)
+                    pstripe<true, true>(L, lane, n2, row_ok, T, btw, open_v, extend_v, rowH, rowF, sr);
+                else
+                    pstripe<false, true>(L, lane, n2, row_ok, T, btw, open_v, extend_v, rowH, rowF, sr);
+            } else {
+                sr.rb = row_ok ? int(s1[i - 1]) : -1;   // never equals a byte
+                sr.arow = altB + 64 - lane;
+                if (lastw)
+                    pstripe<true, false>(L, lane, n2, row_ok, T, btw, open_v, extend_v, rowH, rowF, sr);
+                else
+                    pstripe<false, false>(L, lane, n2, row_ok, T, btw, open_v, extend_v, rowH, rowF, sr);
+            }
+            if (row_ok) colG[i] = L.h;   // H(i, n2): frozen since the lane left column n2
+            __syncthreads();
+        }
+    } else {
     // Row 0: H(0, j) = boundary, F(0, j) = LOW (PairWiseSW.h:72-75,198).
     for (int j = lane; j < kStripe + T; j += 64) {
         rowH[j] = j >= 64 ? boundary(ovh, open, extend, j - 63) : 0;
@@ -205,9 +449,6 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
     for (int c = lane; c < kStripe + T + kGroup; c += 64) altB[c] = (c >= kStripe && c < kStripe + n2) ? s2[c - kStripe] : 0;
     __syncthreads();
 
-    const int nstripes = (n1 + kStripe - 1) / kStripe;
-    uint32_t* bt = a.bt + P.bt_off;
-    const int nw = T / kGroup;
     for (int s = 0; s < nstripes; ++s) {
         const int i = s * kStripe + lane + 1;
         const bool row_ok = i <= n1;
@@ -225,6 +466,7 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
             stripe<false, FAST>(L, lane, n2, rb, row_ok, T, btw, sc, rowH, rowF, altB);
         if (row_ok) colG[i] = L.h;   // H(i, n2): frozen since the lane left column n2
         __syncthreads();
+    }
     }
 
     __threadfence_block();   // this wave's colG stores complete before its lanes read them back
@@ -244,7 +486,7 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
         const int d = d0 + (lane >> 1);
         const bool col = lane & 1;
         const bool ok = col ? (d > n2 && d <= D) : (use_row && d > n1 && d <= D);
-        if (ok) mx = max(mx, col ? colC[d - n2] : rowH[63 + d - n1]);
+        if (ok) mx = max(mx, col ? colC[d - n2] : rowH[63 + d - n1] - hofs);
     }
     const int best = wave_max(mx);
     int bi = 0, bj = 0;
@@ -253,7 +495,7 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
         const int d = d0 + (lane >> 1);
         const bool col = lane & 1;
         const bool ok = col ? (d > n2 && d <= D) : (use_row && d > n1 && d <= D);
-        const bool tie = ok && (col ? colC[d - n2] : rowH[63 + d - n1]) == best;
+        const bool tie = ok && (col ? colC[d - n2] : rowH[63 + d - n1] - hofs) == best;
         uint64_t m = __builtin_amdgcn_ballot_w64(tie);
         while (m) {
             const int l = __builtin_ctzll(m);
@@ -394,18 +636,21 @@ __global__ __launch_bounds__(256) void sw_trace_kernel(SwTraceArgs a)
 
 }  // namespace
 
-size_t dp_lds_bytes(int n1max, int n2max)
+size_t dp_lds_bytes(int n1max, int n2max, bool profile)
 {
-    return sizeof(int) * (size_t(row_slots(n2max)) + size_t(fslots(n1max, n2max))) + size_t(alt_slots(n2max));
+    // [rowH | rowF | altB or the profile | codeOf 256 | alpha 8]
+    const size_t rows = sizeof(int) * (size_t(row_slots(n2max)) + size_t(fslots(n1max, n2max)));
+    return profile ? rows + size_t(dp_tail_bytes(n2max)) + 256 + 8 : rows + size_t(alt_slots(n2max));
 }
 
 hipError_t launch_dp(const SwDpArgs& a, int n1max, hipStream_t s)
 {
     if (a.n <= 0) return hipSuccess;
+    const size_t lds = dp_lds_bytes(n1max, a.n2max, a.fast && a.profile);
     if (a.fast)
-        hipLaunchKernelGGL(sw_dp_kernel<true>, dim3(a.n), dim3(64), dp_lds_bytes(n1max, a.n2max), s, a);
+        hipLaunchKernelGGL(sw_dp_kernel<true>, dim3(a.n), dim3(64), lds, s, a);
     else
-        hipLaunchKernelGGL(sw_dp_kernel<false>, dim3(a.n), dim3(64), dp_lds_bytes(n1max, a.n2max), s, a);
+        hipLaunchKernelGGL(sw_dp_kernel<false>, dim3(a.n), dim3(64), lds, s, a);
     return hipGetLastError();
 }
 

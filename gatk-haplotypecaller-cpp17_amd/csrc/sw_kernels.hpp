@@ -14,18 +14,20 @@ constexpr int kMinCutoff = -100000000;   // MATRIX_MIN_CUTOFF (:50)
 constexpr int kStripe = 64;              // rows per stripe = lanes per wave
 constexpr int kGroup = 8;                // steps per 32-bit backtrack word (4 bits per cell)
 
-// Steps one stripe takes over n2 columns: n2 + 63 (the one-row skew), rounded
-// up to whole backtrack words.
-__host__ __device__ inline int stripe_steps(int n2) { return (n2 + kStripe - 1 + kGroup - 1) & ~(kGroup - 1); }
+// Steps one stripe takes over n2 columns: n2 + 63 (the one-row skew) plus one
+// (lane 63 hands column n2 on the step after it computed it), rounded up to
+// whole backtrack words.
+__host__ __device__ inline int stripe_steps(int n2) { return (n2 + kStripe + kGroup - 1) & ~(kGroup - 1); }
 // Backtrack words of one pair: per stripe, one word per lane per 8 steps.
 __host__ __device__ inline int64_t bt_words(int n1, int n2)
 {
     return int64_t((n1 + kStripe - 1) / kStripe) * (stripe_steps(n2) / kGroup) * kStripe;
 }
 // LDS row buffer entries (H or F): slot 63 + j holds column j; lanes still in
-// the skew write up to 64 slots before column 1 and up to 71 after column n2.
-// (A multiple of 4 entries, so that 16-byte reads of the buffers stay aligned.)
-__host__ __device__ inline int row_slots(int n2max) { return (n2max + 2 * kStripe + kGroup + 3) & ~3; }
+// the skew write up to 64 slots before column 1 and up to 72 after column n2,
+// and lane 0 reads one group ahead. (A multiple of 4 entries, so that 16-byte
+// reads of the buffers stay aligned.)
+__host__ __device__ inline int row_slots(int n2max) { return (n2max + 2 * kStripe + 4 * kGroup + 3) & ~3; }
 // rowF doubles as the last-column buffer (n1 + 1 entries) after the DP.
 __host__ __device__ inline int fslots(int n1max, int n2max)
 {
@@ -34,6 +36,20 @@ __host__ __device__ inline int fslots(int n1max, int n2max)
 // Haplotype bases (bytes): 64 leading pads (lanes still in the skew), then the
 // columns, then pads up to the last step of a stripe.
 __host__ __device__ inline int alt_slots(int n2max) { return (kStripe + n2max + kStripe + 2 * kGroup + 3) & ~3; }
+
+// Substitution profile of the fast path: for each distinct seq1 byte c (up
+// to kProfCodes per pair) and column slot 63 + j, int16 score(seq2[j-1], c) -
+// open. A lane reads its row's profile along its columns (no compare per cell).
+constexpr int kProfCodes = 5;
+__host__ __device__ inline int prof_slots(int n2max) { return (n2max + 2 * kStripe + 4 * kGroup + 7) & ~7; }
+
+// Bytes after the row buffers: the compare paths' haplotype bytes or the
+// profile path's kProfCodes int16 rows.
+__host__ __device__ inline int dp_tail_bytes(int n2max)
+{
+    const int p = 2 * kProfCodes * prof_slots(n2max), b = alt_slots(n2max);
+    return ((p > b ? p : b) + 7) & ~7;
+}
 
 struct SwPair {
     int64_t ref_off;   // seq1 bytes in refs[]
@@ -64,6 +80,7 @@ struct SwDpArgs {
     int shortcut;
     int n1max, n2max;   // size the dynamic LDS
     int fast;    // host-proven: no cutoff, no int32 overflow (sw_engine.cpp fast_ok)
+    int profile;   // fast path with the LDS substitution profile (scores - open fit int16)
 };
 
 struct SwTraceArgs {
@@ -85,7 +102,7 @@ constexpr int kSlotElems = 32;
 // CIGAR element op codes (smithwaterman_common.h:21-26).
 constexpr int kOpM = 0, kOpI = 1, kOpD = 2, kOpS = 9;
 
-size_t dp_lds_bytes(int n1max, int n2max);
+size_t dp_lds_bytes(int n1max, int n2max, bool profile);
 hipError_t launch_dp(const SwDpArgs& a, int n1max, hipStream_t s);
 hipError_t launch_trace(const SwTraceArgs& a, hipStream_t s);
 
