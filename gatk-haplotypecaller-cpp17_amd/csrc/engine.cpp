@@ -73,6 +73,12 @@ struct Slot {
     char* host = nullptr;
     size_t host_cap = 0;
     bool busy = false;
+    // Streams of the part in this slot: parts in different slots of one device
+    // run concurrently (a call cut into parts overlaps the planning of part
+    // k + 1 and the kernels of part k, and its kernels fill the chip together).
+    hipStream_t stream = nullptr, side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;   // side-stream fork / join (timing disabled)
+    hipEvent_t ev[6] = {};   // pack [2], fp32 / fp64 pass [3], done: reused by every part in the slot
 };
 
 struct Device {
@@ -96,8 +102,16 @@ void release_device(Device* d)
     (void)hipSetDevice(d->ordinal);
     if (d->stream) (void)hipStreamSynchronize(d->stream);
     for (Slot* s : d->slots) {
+        if (s->stream) (void)hipStreamSynchronize(s->stream);
+        if (s->side) (void)hipStreamSynchronize(s->side);
         if (s->dev) (void)hipFree(s->dev);
         if (s->host) (void)hipHostFree(s->host);
+        for (auto& e : s->ev)
+            if (e) (void)hipEventDestroy(e);
+        if (s->fork) (void)hipEventDestroy(s->fork);
+        if (s->join) (void)hipEventDestroy(s->join);
+        if (s->side) (void)hipStreamDestroy(s->side);
+        if (s->stream) (void)hipStreamDestroy(s->stream);
         delete s;
     }
     if (d->lut_f) (void)hipFree(d->lut_f);
@@ -192,16 +206,38 @@ int ensure_init()
     return init_devices_locked(&cur, 1, true);
 }
 
+// A free slot of device d (d current on the calling thread), its streams and
+// events created on first use; nullptr if they cannot be created.
 Slot* take_slot(Device& d)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
-    for (Slot* s : d.slots)
-        if (!s->busy) {
-            s->busy = true;
-            return s;
-        }
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        for (Slot* s : d.slots)
+            if (!s->busy) {
+                s->busy = true;
+                return s;
+            }
+    }
     auto* s = new Slot();
+    bool ok = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&s->fork, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&s->join, hipEventDisableTiming) == hipSuccess;
+    for (int k = 0; ok && k < 6; ++k)
+        ok = hipEventCreateWithFlags(&s->ev[k], k == 5 ? hipEventDisableTiming : 0) == hipSuccess;
+    if (!ok) {
+        for (auto& e : s->ev)
+            if (e) (void)hipEventDestroy(e);
+        if (s->fork) (void)hipEventDestroy(s->fork);
+        if (s->join) (void)hipEventDestroy(s->join);
+        if (s->side) (void)hipStreamDestroy(s->side);
+        if (s->stream) (void)hipStreamDestroy(s->stream);
+        delete s;
+        fail(HC_PHMM_EHIP, "slot stream / event creation");
+        return nullptr;
+    }
     s->busy = true;
+    std::lock_guard<std::mutex> lk(g_mu);
     d.slots.push_back(s);
     return s;
 }
@@ -381,6 +417,10 @@ struct Part {
     std::vector<std::array<hipEvent_t, 3>> ev_pool;
     size_t ev_used = 0;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    bool slot_ev = false;         // pack_ev / ev / done are the slot's (not destroyed here)
+    hipStream_t stream = nullptr;             // the part's stream: its slot's, else its device's
+    hipStream_t side = nullptr;               // segmented waves beside one-lane waves
+    hipEvent_t fork = nullptr, join = nullptr;
     hipStream_t last_stream = nullptr;
     int64_t launch_waves = 0;
     bool ran = false;
@@ -428,11 +468,13 @@ void free_part(Part* p)
     if (p->dev) (void)hipSetDevice(p->dev->ordinal);
     if (p->slot) give_slot(p->slot);
     else if (p->dev_base) (void)hipFree(p->dev_base);
-    for (auto& t : p->ev_pool)
-        for (auto& e : t) (void)hipEventDestroy(e);
-    for (auto& e : p->pack_ev)
-        if (e) (void)hipEventDestroy(e);
-    if (p->done) (void)hipEventDestroy(p->done);
+    if (!p->slot_ev) {
+        for (auto& t : p->ev_pool)
+            for (auto& e : t) (void)hipEventDestroy(e);
+        for (auto& e : p->pack_ev)
+            if (e) (void)hipEventDestroy(e);
+        if (p->done) (void)hipEventDestroy(p->done);
+    }
     delete p;
 }
 
@@ -813,7 +855,19 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             double best = 0;
             for (int c = 0; c < kNCaps; ++c) {
                 const double waves = double(lanes_at[c].load()) / 60.0;   // ~60 of 64 lanes filled
-                const double est = std::max(2.0, std::ceil(waves / simds)) * work_at[size_t(c)] / 60.0 / waves;
+                // Up to two rounds of resident waves (3 per SIMD): the SIMD with
+                // the most waves sets the time, its last round issuing at half
+                // rate if it holds one wave (n waves: 3 floor(n/3) + {0, 2, 2}).
+                // More rounds: waves start as slots free up, so the pass time
+                // follows the total work (a ceil() there once picked cap 48 for
+                // a 415 x 128 region: 1.05 ms vs 0.94 at cap 64).
+                const double per_simd = waves / simds;
+                double rounds = per_simd;
+                if (per_simd <= 6.0) {
+                    const int n = std::max(1, int(std::ceil(per_simd - 1e-9)));
+                    rounds = 3.0 * (n / 3) + (n % 3 ? 2.0 : 0.0);
+                }
+                const double est = rounds * work_at[size_t(c)] / 60.0 / waves;
                 if (c == 0 || est < best * 0.98) {
                     best = est;
                     cap = kCaps[c];
@@ -867,6 +921,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     uint8_t *cls = S.cls.data(), *seg_bc = S.seg_bc.data(), *seg_nb = S.seg_nb.data();
     std::atomic<int64_t> cells_a{0};
     std::atomic<int> rmin_a{INT32_MAX}, rmax_a{0};
+    const int qforce = int(env_i64("HC_PHMM_SEG_Q", -1));   // sweeps: force the nb0 (0) or nb0 + 1 (1) candidate
     const int T = int(std::min<int64_t>(64, std::max<int64_t>(1, npairs / 8192)));
     const int64_t pchunk = (npairs + T - 1) / T;
     std::vector<std::array<int64_t, 4>> tcnt(size_t(T) + 1);
@@ -904,7 +959,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
                     const int nb = cd.nb[q];
                     return float(nb * (13 * cd.bc[q] + 26) * (R + nb - 1)) * waste[nb];
                 };
-                const int q = cost(1) < cost(0) ? 1 : 0;
+                const int q = qforce >= 0 ? qforce : cost(1) < cost(0) ? 1 : 0;
                 bco[k] = cd.bc[q];
                 nbo[k] = cd.nb[q];
                 rlo = R < rlo ? R : rlo;
@@ -1220,9 +1275,26 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     b->d_carry = carry_rows ? reinterpret_cast<float2*>(dev + o_carry) : nullptr;
     if (slot) b->host_res = host + host_res_off;
 
-    hipStream_t s = dv.stream;
+    if (slot) {
+        b->stream = slot->stream;
+        b->side = slot->side;
+        b->fork = slot->fork;
+        b->join = slot->join;
+        b->slot_ev = true;
+        b->pack_ev[0] = slot->ev[0];
+        b->pack_ev[1] = slot->ev[1];
+        b->ev_pool.push_back({slot->ev[2], slot->ev[3], slot->ev[4]});
+        b->done = slot->ev[5];
+    } else {
+        b->stream = dv.stream;
+        b->side = dv.side;
+        b->fork = dv.fork;
+        b->join = dv.join;
+    }
+    hipStream_t s = b->stream;
     auto enqueue = [&]() -> int {
-        for (auto& e : b->pack_ev) HIP_TRY(hipEventCreate(&e));
+        if (!b->slot_ev)
+            for (auto& e : b->pack_ev) HIP_TRY(hipEventCreate(&e));
         HIP_TRY(hipMemcpyAsync(dev, host, upload, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemsetAsync(b->d_count, 0, 4 * sizeof(int), s));
         HIP_TRY(hipEventRecord(b->pack_ev[0], s));
@@ -1237,7 +1309,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             const int r = run_part(b, s);
             if (r) return r;
             HIP_TRY(hipMemcpyAsync(b->host_res, dev + o_res, res_bytes, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipEventCreateWithFlags(&b->done, hipEventDisableTiming));
+            if (!b->done) HIP_TRY(hipEventCreateWithFlags(&b->done, hipEventDisableTiming));
             HIP_TRY(hipEventRecord(b->done, s));
         }
         // A part-owned staging buffer is freed on return: the copy must be done.
@@ -1304,18 +1376,18 @@ int run_part(Part* b, hipStream_t s)
             g.waves = b->d_lane_waves;
             g.n_waves = b->n_seg_waves;
             if (fork) {
-                HIP_TRY(hipEventRecord(dv.fork, s));
-                HIP_TRY(hipStreamWaitEvent(dv.side, dv.fork, 0));
+                HIP_TRY(hipEventRecord(b->fork, s));
+                HIP_TRY(hipStreamWaitEvent(b->side, b->fork, 0));
             }
-            HIP_TRY(launch_lane_seg_f32(g, fork ? dv.side : s));
-            if (fork) HIP_TRY(hipEventRecord(dv.join, dv.side));
+            HIP_TRY(launch_lane_seg_f32(g, fork ? b->side : s));
+            if (fork) HIP_TRY(hipEventRecord(b->join, b->side));
         }
         if (n_one > 0) {
             a.waves = b->d_lane_waves + b->n_seg_waves;
             a.n_waves = n_one;
             HIP_TRY(launch_lane_f32(b->lane_variant, a, s));
         }
-        if (fork) HIP_TRY(hipStreamWaitEvent(s, dv.join, 0));
+        if (fork) HIP_TRY(hipStreamWaitEvent(s, b->join, 0));
     }
     for (auto& c : b->cls) {
         if (c.n == 0) continue;
@@ -1435,21 +1507,30 @@ std::vector<int64_t> equal_cuts(const std::vector<int64_t>& prefix, int nparts)
     for (int j = 1; j < nparts; ++j) {
         const int64_t target = (tot * j + nparts / 2) / nparts;
         int64_t c = int64_t(std::lower_bound(prefix.begin(), prefix.end(), target) - prefix.begin());
+        // the nearer of the boundaries either side of the target (two halves of
+        // a region just under half each must not both land in the first part)
+        if (c > 0 && c <= n && target - prefix[size_t(c) - 1] < prefix[size_t(c)] - target) --c;
         cut[size_t(j)] = std::max(cut[size_t(j) - 1], std::min(n, c));
     }
     return cut;
 }
 
-// How many parts for `cells` over the configured devices: one part per device
-// above HC_PHMM_SHARD_MIN_CELLS, and chunks of about HC_PHMM_CHUNK_CELLS per
-// part above that, so planning overlaps the device passes.
+// How many parts for `cells` over the configured devices: one part below
+// HC_PHMM_SHARD_MIN_CELLS; above, per device at least HC_PHMM_MIN_CHUNKS (1)
+// and about one per HC_PHMM_CHUNK_CELLS, so the planning of part k + 1
+// overlaps the device pass of part k (the parts of one device run on their
+// slots' streams, concurrently). One 415 x 128 region (3.3e9 cells) stays
+// whole: cut in 2 / 3 / 4 parts it took 2.23 / 1.99 / 1.84 ms vs 1.89 ms
+// (tools/region_ab.py; each part pays its own planning fixed costs and fp64
+// pass).
 int part_count(int64_t cells, int ndev)
 {
     const int64_t shard_min = env_i64("HC_PHMM_SHARD_MIN_CELLS", int64_t(2000000000));
     const int64_t chunk = std::max<int64_t>(1, env_i64("HC_PHMM_CHUNK_CELLS", int64_t(12000000000)));
+    const int64_t min_chunks = std::max<int64_t>(1, env_i64("HC_PHMM_MIN_CHUNKS", 1));
     if (cells < shard_min) return 1;
     const int64_t per_dev = (cells + ndev - 1) / ndev;
-    const int64_t chunks = std::max<int64_t>(1, (per_dev + chunk / 2) / chunk);
+    const int64_t chunks = std::max<int64_t>(min_chunks, (per_dev + chunk / 2) / chunk);
     return int(std::min<int64_t>(int64_t(ndev) * chunks, 4096));
 }
 
@@ -1470,6 +1551,7 @@ int submit(const Src& src, const std::vector<PartSpec>& specs, const std::vector
     auto* J = new hc_phmm_job();
     J->out = out;
     const int G = int(g_devs.size());
+    if (std::getenv("HC_PHMM_TRACE")) std::fprintf(stderr, "[hc_phmm] submit: %zu part(s)\n", specs.size());
     Device* solo = specs.size() == 1 ? least_loaded() : nullptr;
     for (size_t j = 0; j < specs.size(); ++j) {
         Device& d = solo ? *solo : *g_devs[j % size_t(G)];
@@ -1481,7 +1563,7 @@ int submit(const Src& src, const std::vector<PartSpec>& specs, const std::vector
             if (sl) give_slot(sl);
             for (Part* q : J->parts) {
                 (void)hipSetDevice(q->dev->ordinal);
-                (void)hipStreamSynchronize(q->dev->stream);
+                (void)hipStreamSynchronize(q->stream);
                 free_part(q);
             }
             delete J;
@@ -1890,7 +1972,7 @@ int hc_phmm_batch_run(hc_phmm_batch* b, void* stream)
         return fail(HC_PHMM_EINVAL, "a caller stream selects one device; this batch spans several");
     for (Part* p : b->parts) {
         HIP_TRY(hipSetDevice(p->dev->ordinal));
-        const int rc = run_part(p, stream ? static_cast<hipStream_t>(stream) : p->dev->stream);
+        const int rc = run_part(p, stream ? static_cast<hipStream_t>(stream) : p->stream);
         if (rc) return rc;
     }
     return HC_PHMM_OK;
