@@ -115,6 +115,13 @@ def host_cpu():
 
 SW_OPS_PER_CELL = 22       # MAIN_CODE int32 vector ops per cell (PairWiseSW.h:4-38)
 INT32_VALU_PEAK_TOPS = 78.6   # 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz (wave64 issues over 2 cycles; no packed int32 ops)
+# gfx950 issues v_add/v_sub/logic at that rate but v_max, v_alignbit, compares
+# and DPP moves at half of it (profiles/r02_op_rate_ubench.jsonl). The DP
+# kernel's fast path issues 9 full-rate + 11 half-rate instructions per cell:
+# 31 full-rate issue slots, so its own instruction-mix ceiling is
+# 256 x 4 x 32 x 2.4e9 / 31 cells/s.
+SW_MIX_SLOTS_PER_CELL = 31
+SW_MIX_CEILING_TCUPS = 256 * 4 * 32 * 2.4e9 / SW_MIX_SLOTS_PER_CELL / 1e12
 
 
 def sw_secondary(no_cpu: bool):
@@ -145,7 +152,11 @@ def sw_secondary(no_cpu: bool):
                roofline=dict(bound="valu-int32", achieved=round(tcups * SW_OPS_PER_CELL, 2),
                              peak=INT32_VALU_PEAK_TOPS, unit="Top/s",
                              frac=round(tcups * SW_OPS_PER_CELL / INT32_VALU_PEAK_TOPS, 4),
-                             note=f"{SW_OPS_PER_CELL} int32 ops/cell x DP cells / sw_dp_kernel time"))
+                             note=f"{SW_OPS_PER_CELL} int32 ops/cell x DP cells / sw_dp_kernel time",
+                             mix_ceiling_tcups=round(SW_MIX_CEILING_TCUPS, 3),
+                             frac_of_mix_ceiling=round(tcups / SW_MIX_CEILING_TCUPS, 4),
+                             mix_note=f"{SW_MIX_SLOTS_PER_CELL} full-rate issue slots per cell (9 full-rate + 11 "
+                                      "half-rate VALU); includes the one-row skew and partial-stripe cells"))
     # one region through the host API (the real per-region call shape)
     one = SWW.config("W1")
     hcsw.align_flat(one)
