@@ -655,6 +655,7 @@ struct PlanScratch {
     std::vector<int32_t> rlen, gapw, hlen;
     std::vector<int64_t> row_off, gap_off, hap_w, hap_b;
     std::vector<uint8_t> hcls, cls, seg_bc, seg_nb, used, in_tail;
+    std::vector<uint32_t> srec;   // (BC, nb, R) of the segmented pairs in sorted order
     std::vector<uint32_t> hcand, key, id;
     std::vector<int> seg_in, one_ord, ord2[2], seg_ord, sort_tmp;
     std::vector<LaneWave> lw, ordered;
@@ -922,7 +923,10 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     std::atomic<int64_t> cells_a{0};
     std::atomic<int> rmin_a{INT32_MAX}, rmax_a{0};
     const int qforce = int(env_i64("HC_PHMM_SEG_Q", -1));   // sweeps: force the nb0 (0) or nb0 + 1 (1) candidate
-    const int T = int(std::min<int64_t>(64, std::max<int64_t>(1, npairs / 8192)));
+    // Pairs per planning task (a 415 x 128 region call on the GPU box: 2.0 ms
+    // at 8192, 2.96 ms on one task; tools/region_ab.py).
+    const int64_t task_pairs = std::max<int64_t>(1024, env_i64("HC_PHMM_TASK_PAIRS", 8192));
+    const int T = int(std::min<int64_t>(64, std::max<int64_t>(1, npairs / task_pairs)));
     const int64_t pchunk = (npairs + T - 1) / T;
     std::vector<std::array<int64_t, 4>> tcnt(size_t(T) + 1);
     WorkerPool::get().run(T, [&](int t) {
@@ -1029,20 +1033,40 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     std::vector<LaneWave>& lw = S.lw;
     lw.clear();
     {
-        const int T = int(std::min<int64_t>(64, std::max<int64_t>(1, ns / 16384)));
+        const int T = int(std::min<int64_t>(64, std::max<int64_t>(1, ns / task_pairs)));
         const int64_t chunk = (ns + T - 1) / T;
         std::vector<std::vector<LaneWave>>& part_w = S.part_w;
         if (part_w.size() < size_t(T)) part_w.resize(size_t(T));
         for (auto& W : part_w) W.clear();
         S.used.assign(size_t(ns), 0);
+        // The packing reads (BC, nb, R) of the pairs in sorted order: gather
+        // them once into a sequential array (one parallel pass of random
+        // reads, instead of three per look-ahead probe on one task per 16k
+        // pairs: 0.3 ms of a 415 x 128 region's planning on the GPU box).
+        std::vector<uint32_t>& srec = S.srec;
+        grow(srec, size_t(ns));
+        parallel_for(ns, [&](int64_t lo, int64_t hi) {
+            for (int64_t k = lo; k < hi; ++k) {
+                const int p = seg_in[size_t(k)];
+                srec[size_t(k)] = uint32_t(seg_bc[size_t(p)]) | uint32_t(seg_nb[size_t(p)]) << 8 |
+                                  uint32_t(std::min(pd[p].y, 65535)) << 16;
+            }
+        });
+        // Smallest nb of each width in the part: a wave whose free lanes drop
+        // below it cannot take another pair of its width, so its look-ahead
+        // stops there (a uniform region once scanned all 64 entries per wave).
+        std::array<uint8_t, kSegMaxBC + 1> minnb;
+        minnb.fill(64);
+        for (int64_t k = 0; k < ns; ++k) {
+            uint8_t& m = minnb[srec[size_t(k)] & 0xff];
+            m = std::min<uint8_t>(m, uint8_t(srec[size_t(k)] >> 8));
+        }
         WorkerPool::get().run(T, [&](int t) {
             const int64_t b = t * chunk, e = std::min(ns, b + chunk);
             if (b >= e) return;
             const int64_t m = e - b;
             const int* __restrict in = seg_in.data() + b;
-            const uint8_t* __restrict bcs = seg_bc;
-            const uint8_t* __restrict nbs = seg_nb;
-            const PairDesc* __restrict pdi = pd;
+            const uint32_t* __restrict rec = srec.data() + b;
             int* __restrict ordo = seg_ord.data();
             uint8_t* __restrict used = S.used.data() + b;
             auto& W = part_w[size_t(t)];
@@ -1050,24 +1074,25 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             constexpr int64_t kLook = 64;
             for (int64_t i = 0; i < m; ++i) {
                 if (used[i]) continue;
-                const int bc = bcs[in[i]];
+                const int bc = int(rec[i] & 0xff);
                 LaneWave w{};
                 w.slot0 = int(slot_n);
                 w.ncols = bc;
                 int rmin = INT32_MAX, rmax = 0, nst = 0, np = 0;
                 int free = 64;
+                const int need = minnb[size_t(bc)];
                 const int64_t jend = std::min(m, i + kLook);
-                for (int64_t j = i; j < jend && free > 0; ++j) {
+                for (int64_t j = i; j < jend && free >= need; ++j) {
                     if (used[j]) continue;
-                    const int p = in[j];
-                    if (bcs[p] != bc) break;
-                    const int nb = nbs[p];
+                    const uint32_t r = rec[j];
+                    if (int(r & 0xff) != bc) break;
+                    const int nb = int((r >> 8) & 0xff);
                     if (nb > free) continue;
                     used[j] = 1;
                     free -= nb;
-                    ordo[slot_n++] = p;
+                    ordo[slot_n++] = in[j];
                     ++np;
-                    const int R = pdi[p].y;
+                    const int R = int(r >> 16);
                     rmax = R > rmax ? R : rmax;
                     rmin = R < rmin ? R : rmin;
                     nst = R + nb - 1 > nst ? R + nb - 1 : nst;
@@ -1084,6 +1109,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         lw.reserve(nw);
         for (auto& W : part_w) lw.insert(lw.end(), W.begin(), W.end());
     }
+    tm.mark("seg pack: greedy");
     // Dispatch order: the bulk in packing order (co-resident waves share one
     // width's code), the shortest waves filling the last tail_rounds rounds of
     // wave slots last, longest first (LPT, duration ~ BC * nsteps), so the chip
@@ -1093,7 +1119,14 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         const size_t nw = lw.size();
         const size_t K = std::min(nw, size_t(tail_rounds) * 4 * size_t(dv.n_cu) * kSegWavesPerSimd);
         auto cost = [&](size_t k) { return int64_t(lw[k].ncols) * lw[k].nsteps; };
-        if (K > 0 && K < nw) {
+        int64_t cmin = INT64_MAX, cmax = 0;
+        for (size_t k = 0; k < nw; ++k) {
+            cmin = std::min(cmin, cost(k));
+            cmax = std::max(cmax, cost(k));
+        }
+        // Waves of (nearly) equal length (one region's cross product) drain
+        // evenly in any order: no reorder.
+        if (K > 0 && K < nw && cmax * 20 > cmin * 21) {
             std::vector<uint32_t>& id = S.id;
             id.resize(nw);
             std::iota(id.begin(), id.end(), 0u);
