@@ -376,6 +376,8 @@ def main():
                     help="rank 0 re-computes this many random pairs alone and compares them bit for bit "
                          "with the gathered multi-rank results")
     ap.add_argument("--check-out", default=None, help="with --check: save the reassembled results (npz)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="use the process group / gather path even at WORLD_SIZE=1 (tests of the RCCL path)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -394,7 +396,10 @@ def main():
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     gloo = args.dist_backend == "gloo"
-    if world > 1:
+    # --force-dist: the distributed path (process group, gathers, check) at one
+    # rank, so a one-GPU box exercises the RCCL code the 8-GPU run uses.
+    distributed = world > 1 or args.force_dist
+    if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if gloo:
             dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -412,43 +417,65 @@ def main():
     nmax = max(len(s) for s in shards)
 
     bt = hcphmm.Batch(sub)
-    raw32 = torch.zeros(nmax, dtype=torch.float32, device=dev)
-    raw64 = torch.zeros(nmax, dtype=torch.float64, device=dev)
-    flag = torch.zeros(nmax, dtype=torch.uint8, device=dev)
+    # Two output sets: with RCCL the gather of step k (on its own stream) runs
+    # while step k + 1's device pass writes the other set.
+    nsets = 2 if (distributed and not gloo) else 1
+    outs = [(torch.zeros(nmax, dtype=torch.float32, device=dev), torch.zeros(nmax, dtype=torch.float64, device=dev),
+             torch.zeros(nmax, dtype=torch.uint8, device=dev)) for _ in range(nsets)]
+    raw32, raw64, flag = outs[0]
     bt.bind_outputs(raw32.data_ptr(), raw64.data_ptr(), flag.data_ptr())
     gdev = torch.device("cpu") if gloo else dev
-    g32 = [torch.empty(nmax, dtype=torch.float32, device=gdev) for _ in range(world)] if (world > 1 and rank == 0) else None
-    g64 = [torch.empty(nmax, dtype=torch.float64, device=gdev) for _ in range(world)] if (world > 1 and rank == 0) else None
+    g32 = [torch.empty(nmax, dtype=torch.float32, device=gdev) for _ in range(world)] if (distributed and rank == 0) else None
+    g64 = [torch.empty(nmax, dtype=torch.float64, device=gdev) for _ in range(world)] if (distributed and rank == 0) else None
 
-    # The device pass and the gather run on one created stream: the library
-    # enqueues on it (a created stream's handle is non-zero; 0 would select the
-    # library's own stream, unordered with torch's), and RCCL / the gloo copy
-    # to host then wait for the pass.
+    # The device pass runs on a created stream: the library enqueues on it (a
+    # created stream's handle is non-zero; 0 would select the library's own
+    # stream, unordered with torch's). The gather of a step's outputs waits for
+    # that step's pass (event), and the pass that next writes the same output
+    # set waits for that gather (event): RCCL over xGMI overlaps the next pass.
     stream = torch.cuda.Stream(device=dev)
+    cstream = torch.cuda.Stream(device=dev) if nsets == 2 else stream
+    ran_ev = [torch.cuda.Event() for _ in range(nsets)]
+    gathered_ev = [None] * nsets
+    nstep = [0]
 
     def step():
+        k = nstep[0] % nsets
+        nstep[0] += 1
+        r32, r64, fl = outs[k]
         with torch.cuda.stream(stream):
+            if gathered_ev[k] is not None:
+                stream.wait_event(gathered_ev[k])
+            if nsets == 2:
+                bt.bind_outputs(r32.data_ptr(), r64.data_ptr(), fl.data_ptr())
             bt.run(stream.cuda_stream)
-            if world > 1:
-                s32, s64 = (raw32.cpu(), raw64.cpu()) if gloo else (raw32, raw64)
+            ran_ev[k].record(stream)
+        if distributed:
+            with torch.cuda.stream(cstream):
+                cstream.wait_event(ran_ev[k])
+                s32, s64 = (r32.cpu(), r64.cpu()) if gloo else (r32, r64)
                 dist.gather(s32, gather_list=g32, dst=0)   # RCCL gather over xGMI
                 dist.gather(s64, gather_list=g64, dst=0)
+                if nsets == 2:
+                    ev = torch.cuda.Event()
+                    ev.record(cstream)
+                    gathered_ev[k] = ev
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     bt.stats()   # reset the kernel event log: the averages below cover the timed steps only
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -526,21 +553,23 @@ def main():
         sec["smith_waterman"] = sw_secondary(args.no_cpu)
         sec["genotyper"] = gt_secondary(args.no_cpu)
         out["secondary"] = sec
-    if world > 1:
-        out["gather"] = f"dist.gather ({'gloo, rehearsal' if gloo else 'RCCL'}) of raw_f32 + raw_f64 per step"
-    if args.check and world > 1:
+    if distributed:
+        out["gather"] = (f"dist.gather ({'gloo, rehearsal' if gloo else 'RCCL'}) of raw_f32 + raw_f64 per step"
+                         + ("" if gloo else ", on its own stream overlapping the next step's pass (two output sets)"))
+    if args.check and distributed:
         # One more step into outputs poisoned with NaN on every rank (and in rank
         # 0's gather buffers): what is gathered must come from this very run.
         with torch.cuda.stream(stream):
-            raw32.fill_(float("nan"))
-            raw64.fill_(float("nan"))
+            for r32, r64, _fl in outs:
+                r32.fill_(float("nan"))
+                r64.fill_(float("nan"))
             for g in (g32 or []) + (g64 or []):
                 g.fill_(float("nan"))
         torch.cuda.synchronize()
         dist.barrier()
         step()
         torch.cuda.synchronize()
-    if args.check and world > 1 and rank == 0:
+    if args.check and distributed and rank == 0:
         # Reassemble batch order from the gathered shards and compare a random
         # sample with a single-process run of the same pairs.
         full32 = np.zeros(n_total, np.float32)
@@ -559,7 +588,7 @@ def main():
     bt.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 
