@@ -119,6 +119,7 @@ struct hc_sw_batch {
     int overhang = 9, shortcut = 1;
     int fast = 0;
     int profile = 0;
+    int spiral = 0;
     char* dev = nullptr;
     SwPair* pairs = nullptr;
     int32_t* order = nullptr;
@@ -217,9 +218,7 @@ int create(int64_t n, const int64_t* ref_off, const int32_t* ref_len, const uint
         P.alt_off = alt_off[k];
         P.n1 = n1;
         P.n2 = n2;
-        P.bt_off = bt_total;
         P.el_off = el_total;
-        bt_total += bt_words(n1, n2);
         el_total += n1 + n2 + 3;
         ref_ext = std::max(ref_ext, ref_off[k] + n1);
         alt_ext = std::max(alt_ext, alt_off[k] + n2);
@@ -250,6 +249,17 @@ int create(int64_t n, const int64_t* ref_off, const int32_t* ref_len, const uint
     if (const char* e = std::getenv("HC_SW_PROFILE"))
         if (e[0] == '1')
             b->profile = b->fast && pm >= INT16_MIN && pm <= INT16_MAX && pmm >= INT16_MIN && pmm <= INT16_MAX;
+    // The fast compare path in the spiral layout on request (HC_SW_SPIRAL=1):
+    // it removes the per-stripe skew (W2: 12 % fewer steps) but its stripe
+    // changes make 16 % of the groups run a heavier step, and it measured
+    // slower on MI355X (W2 DP 9.33 vs 8.72 ms, W3 3.66 vs 3.45 ms).
+    b->spiral = 0;
+    if (const char* e = std::getenv("HC_SW_SPIRAL"))
+        if (e[0] == '1') b->spiral = b->fast && !b->profile;
+    for (auto& P : pairs) {
+        P.bt_off = bt_total;
+        bt_total += b->spiral ? spiral_bt_words(P.n1, P.n2) : bt_words(P.n1, P.n2);
+    }
 
     // One device allocation: descriptors, inputs, outputs, scratch.
     size_t off = 0;
@@ -348,6 +358,7 @@ int run(hc_sw_batch* b, hipStream_t s)
     d.n2max = b->n2max;
     d.fast = b->fast;
     d.profile = b->profile;
+    d.spiral = b->spiral;
     SwTraceArgs t{};
     t.pairs = b->pairs;
     t.res = b->res;
@@ -358,6 +369,7 @@ int run(hc_sw_batch* b, hipStream_t s)
     t.slots = b->slots;
     t.n_elems = b->n_elems;
     t.offsets = b->offsets;
+    t.spiral = b->spiral;
     HIP_TRY(hipEventRecord(b->ev[0], s));
     HIP_TRY(launch_dp(d, b->n1max, s));
     HIP_TRY(hipEventRecord(b->ev[1], s));

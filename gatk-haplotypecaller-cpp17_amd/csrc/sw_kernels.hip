@@ -36,6 +36,7 @@
 // and writes run-length CIGAR elements.
 #include "sw_kernels.hpp"
 
+#include <algorithm>
 #include <climits>
 
 namespace hcsw {
@@ -306,6 +307,146 @@ __device__ __forceinline__ void pstripe(PLane& L, int lane, int n2, bool row_ok,
     }
 }
 
+// ---- spiral path (HC_SW_SPIRAL=1) -----------------------------------------
+// Lanes run on into the next stripe (sw_kernels.hpp spiral_period): one skew
+// per pair instead of one per stripe (W2: 12 % fewer steps). Bit-exact, but
+// the groups around each stripe change (16 % on W2) run a step with the
+// change's bookkeeping, and on MI355X it measured slower than the striped
+// sweep (W2 DP 9.33 vs 8.72 ms), so it is not the default.
+// Per lane: vm = v mod P of the current step (negative before the lane's
+// first step, kSpDone after its last stripe), the current row irow and the
+// LDS/alt base (slot of the current step's column = base + t). hd is the last
+// computed H before a stripe change resets h: the lane below still needs it
+// (H(i, n2) + open) on the step after.
+constexpr int kSpDone = INT_MIN / 2;
+
+struct SpLane {
+    int h, hd, ex, fx, dg;
+    uint32_t acc;
+    int rb;     // this row's seq1 byte (-1: no row)
+    int base;   // 63 - lane - stripe * P
+    int vm;
+    int irow;   // 1-based row of the current stripe
+    int okc;    // row buffer writes on (valid row, not done)
+    // next stripe's values, ready before the lane's stripe change
+    int rbn, okn, hbn, dgn;
+};
+
+struct SpConst {
+    int open, extend, mp, mmp, lowx;   // VGPR copies
+    int n1, n2, P, S;
+    int ovh, open_s, extend_s;         // scalar copies for the boundaries
+};
+
+__device__ __forceinline__ void sp_next(SpLane& L, const SpConst& c, const uint8_t* s1)
+{
+    const int in = L.irow + kStripe;   // the next stripe's row
+    L.okn = in <= c.n1;
+    L.rbn = L.okn ? int(s1[in - 1]) : -1;
+    L.hbn = boundary(c.ovh, c.open_s, c.extend_s, in);                // H(in, 0)
+    L.dgn = boundary(c.ovh, c.open_s, c.extend_s, in - 1) + c.open;   // H(in - 1, 0) + open
+}
+
+// One step. SLOW: stripe changes, idle lanes (before the first step, pads,
+// done), writes only from valid rows. Bulk: every lane computing a cell of
+// its stripe, no stripe change within this step or the one before.
+template <bool SLOW, bool GUARD>
+__device__ __forceinline__ void sp_step(SpLane& L, const SpConst& c, int t, int ho, int fxo, int ab, int* rowHo,
+                                        int* rowF, int* colG)
+{
+    const int eo = L.h + c.open;
+    const int eod = SLOW ? L.hd + c.open : eo;
+    const int fo = shr1(ho, eod);
+    const int fe = shr1(fxo, L.fx);
+    const int sc = ab == L.rb ? c.mp : c.mmp;
+    const int fn = max(fe, fo);
+    const int en = max(eo, L.ex);
+    const int hn0 = L.dg + sc;
+    const int hn1 = max(hn0, en);
+    const int hn = max(hn1, fn);
+    L.acc = __builtin_amdgcn_alignbit(L.acc, uint32_t(L.ex - eo), 31);
+    L.acc = __builtin_amdgcn_alignbit(L.acc, uint32_t(fe - fo), 31);
+    L.acc = __builtin_amdgcn_alignbit(L.acc, uint32_t(hn0 - en), 31);
+    L.acc = __builtin_amdgcn_alignbit(L.acc, uint32_t(hn1 - fn), 31);
+    L.fx = fn + c.extend;
+    L.dg = fo;
+    if (!SLOW) {
+        L.h = hn;
+        L.ex = en + c.extend;
+        if (!GUARD || L.okc) {
+            rowHo[L.base + t] = eo;
+            rowF[L.base + 1 + t] = L.fx;
+        }
+        return;
+    }
+    const bool act = unsigned(L.vm) < unsigned(c.n2);
+    const int hu = act ? hn : L.h;
+    const int exu = act ? en + c.extend : L.ex;
+    if (L.okc) {
+        rowHo[L.base + t] = eo;
+        rowF[L.base + 1 + t] = L.fx;
+    }
+    L.hd = hu;
+    L.h = hu;
+    L.ex = exu;
+    if (L.vm == c.P - 1) {   // the lane leaves column P of its stripe
+        if (L.irow <= c.n1) colG[L.irow] = hu;   // H(i, n2): frozen since column n2
+        if (L.okc) rowHo[L.base + t + 1] = hu + c.open;   // column n2's H + open for the next stripe's lane 0
+        if (L.irow + kStripe <= c.S * kStripe) {   // not the last stripe: start the next one
+            L.h = L.hbn;
+            L.ex = c.lowx;
+            L.dg = L.dgn;
+            L.rb = L.rbn;
+            L.okc = L.okn;
+            L.base -= c.P;
+            L.irow += kStripe;
+            L.vm = -1;
+        } else {
+            L.okc = 0;
+            L.base -= c.P;   // its haplotype reads stay inside the buffer
+            L.vm = kSpDone;
+        }
+    }
+    ++L.vm;
+}
+
+template <bool SLOW, bool GUARD>
+__device__ __forceinline__ void sp_group(SpLane& L, const SpConst& c, int t0, int q0, const int* rowHo_c,
+                                         const int* rowF_c, const uint8_t* altB, int* rowHo, int* rowF, int* colG)
+{
+    // lane 0's row-buffer inputs: column (t mod P) + 1 of the previous stripe's
+    // last row, slot 64 + (t mod P) (uniform); every lane's haplotype bytes at
+    // its base (the 8-byte cyclic pad behind column P serves a lane whose
+    // stripe changes inside the group).
+    int ho[kGroup], fxo[kGroup], ab[kGroup];
+    if (!SLOW) {
+        // no stripe change for any lane (lane 0 included): contiguous slots,
+        // one address for the group
+        LdsInt* h = (LdsInt*)rowHo_c + 64 + q0;
+        LdsInt* f = (LdsInt*)rowF_c + 64 + q0;
+#pragma unroll
+        for (int j = 0; j < kGroup; ++j) {
+            ho[j] = h[j];
+            fxo[j] = f[j];
+            ab[j] = ((LdsU8*)altB)[L.base + 1 + t0 + j];
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kGroup; ++j) {
+            const int q = q0 + j < c.P ? q0 + j : q0 + j - c.P;
+            ho[j] = ((LdsInt*)rowHo_c)[64 + q];
+            fxo[j] = ((LdsInt*)rowF_c)[64 + q];
+            ab[j] = ((LdsU8*)altB)[L.base + 1 + t0 + j];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) sp_step<SLOW, GUARD>(L, c, t0 + j, ho[j], fxo[j], ab[j], rowHo, rowF, colG);
+    if (!SLOW) {   // bulk steps leave the stripe bookkeeping alone
+        L.vm += kGroup;
+        L.hd = L.h;
+    }
+}
+
 // Rank the distinct bytes of seq1 (the row bases): codeOf[b] = rank, alpha[rank]
 // = b. Returns the number of distinct bytes (wave-uniform).
 __device__ int build_alphabet(const uint8_t* s1, int n1, int lane, uint8_t* codeOf, uint8_t* alpha)
@@ -386,7 +527,88 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
 
     const int K = (FAST && a.profile) ? build_alphabet(s1, n1, lane, codeOf, alpha) : 0;
     const bool use_prof = FAST && a.profile && K <= kProfCodes;
-    if (FAST) {
+    if (FAST && a.spiral) {
+        hofs = open;
+        const int Pp = spiral_period(n2);
+        const int Pmax = spiral_period(a.n2max);
+        const int Ts = spiral_steps(n1, n2);
+        // Row 0: H(0, j) + open, F(0, j) + extend; haplotype bytes at 64 + c with
+        // pads to P and an 8-byte cyclic copy of the first columns behind P.
+        for (int j = lane; j < Pmax + kStripe + 2 * kGroup; j += 64) {
+            rowH[j] = (j >= 64 ? boundary(ovh, open, extend, j - 63) : 0) + open;
+            rowF[j] = kLow + extend;
+        }
+        for (int x = lane; x < kStripe + Pp + 2 * kGroup; x += 64) {
+            const int cc = x - kStripe;
+            const int col = cc >= Pp ? cc - Pp : cc;
+            altB[x] = (cc >= 0 && col < n2) ? s2[col] : 0;
+        }
+        __syncthreads();
+        SpConst c;
+        c.open = in_vgpr(open);
+        c.extend = in_vgpr(extend);
+        c.mp = in_vgpr(a.match - open);
+        c.mmp = in_vgpr(a.mismatch - open);
+        c.lowx = in_vgpr(kLow + extend);
+        c.n1 = n1;
+        c.n2 = n2;
+        c.P = Pp;
+        c.S = nstripes;
+        c.ovh = ovh;
+        c.open_s = open;
+        c.extend_s = extend;
+        SpLane L;
+        L.irow = lane + 1;
+        L.h = L.hd = boundary(ovh, open, extend, L.irow);   // H(i, 0)
+        L.ex = kLow + extend;                                // E(i, 0) + extend
+        L.fx = kLow + extend;
+        L.dg = boundary(ovh, open, extend, lane) + open;     // lane 0: H(0, 0) + open
+        L.acc = 0;
+        L.okc = L.irow <= n1;
+        L.rb = L.okc ? int(s1[L.irow - 1]) : -1;
+        L.base = 63 - lane;
+        L.vm = -lane;
+        sp_next(L, c, s1);
+        const int V = nstripes * Pp;
+        const bool partial = (n1 % kStripe) != 0;
+        int q0 = 0;   // t0 mod P
+        // Groups whose lanes' v over the group and the step before
+        // ([t0 - 64, t0 + 7]) include a stripe change, an idle lane or the
+        // pair's end run the slow step; the rest the bulk step, with guarded
+        // row-buffer writes once some lane may be on a missing row of a
+        // partial last stripe (a separate loop: the two bulk forms must not
+        // share hoisted loads, which costs a copy per DPP destination).
+        const int tg = partial ? std::min(Ts, std::max(0, ((nstripes - 1) * Pp - kGroup + 1 + kGroup - 1) & ~(kGroup - 1))) : Ts;
+        auto slow_at = [&](int t0) {
+            const int vlo = t0 - kStripe, vhi = t0 + kGroup - 1;
+            const int lo = vlo > 0 ? vlo : 0;
+            return vlo < 0 || vhi >= V || Pp > n2 || (vhi + 1) / Pp > lo / Pp;
+        };
+        int t0 = 0;
+        for (; t0 < tg; t0 += kGroup) {
+            const bool slow = slow_at(t0);
+            if (slow)
+                sp_group<true, true>(L, c, t0, q0, rowH, rowF, altB, rowH, rowF, colG);
+            else
+                sp_group<false, false>(L, c, t0, q0, rowH, rowF, altB, rowH, rowF, colG);
+            bt[int64_t(t0 / kGroup) * kStripe + lane] = L.acc;
+            if (slow) sp_next(L, c, s1);
+            q0 += kGroup;
+            if (q0 >= Pp) q0 -= Pp;
+        }
+        for (; t0 < Ts; t0 += kGroup) {
+            const bool slow = slow_at(t0);
+            if (slow)
+                sp_group<true, true>(L, c, t0, q0, rowH, rowF, altB, rowH, rowF, colG);
+            else
+                sp_group<false, true>(L, c, t0, q0, rowH, rowF, altB, rowH, rowF, colG);
+            bt[int64_t(t0 / kGroup) * kStripe + lane] = L.acc;
+            if (slow) sp_next(L, c, s1);
+            q0 += kGroup;
+            if (q0 >= Pp) q0 -= Pp;
+        }
+        __syncthreads();
+    } else if (FAST) {
         hofs = open;
         // Row 0 in this path's form: H(0, j) + open, F(0, j) + extend.
         for (int j = lane; j < kStripe + T + 2 * kGroup; j += 64) {
@@ -513,11 +735,13 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
     if (lane == 0) a.res[p] = SwResult{best, bi, bj, 0};
 }
 
-// 4-bit backtrack code of cell (i, j), 1-based (layout of sw_dp_kernel).
-__device__ __forceinline__ int bt_nibble(const uint32_t* bt, int nw, int i, int j)
+// 4-bit backtrack code of cell (i, j), 1-based (layout of sw_dp_kernel):
+// striped ([stripe][word][lane], P = 0) or spiral ([group][lane], period P).
+__device__ __forceinline__ int bt_nibble(const uint32_t* bt, int nw, int P, int i, int j)
 {
-    const int k = (i - 1) & (kStripe - 1), s = (i - 1) / kStripe, t = j - 1 + k;
-    const uint32_t w = bt[(int64_t(s) * nw + (t >> 3)) * kStripe + k];
+    const int k = (i - 1) & (kStripe - 1), s = (i - 1) / kStripe;
+    const int t = P ? s * P + j - 1 + k : j - 1 + k;
+    const uint32_t w = bt[(P ? int64_t(t >> 3) : int64_t(s) * nw + (t >> 3)) * kStripe + k];
     return (w >> ((7 - (t & 7)) * 4)) & 15;
 }
 
@@ -548,6 +772,7 @@ __global__ __launch_bounds__(256) void sw_trace_kernel(SwTraceArgs a)
     }
     const uint32_t* bt = a.bt + P.bt_off;
     const int nw = stripe_steps(n2) / kGroup;
+    const int Psp = a.spiral ? spiral_period(n2) : 0;
     const int ovh = a.overhang;
     int i = __builtin_amdgcn_readfirstlane(r.max_i), j = __builtin_amdgcn_readfirstlane(r.max_j);
     if (ovh == 10) {
@@ -573,7 +798,7 @@ __global__ __launch_bounds__(256) void sw_trace_kernel(SwTraceArgs a)
         const int di = state == 4 ? 0 : lane, dj = state == 8 ? 0 : lane;
         const int ci = i - di, cj = j - dj;
         const bool valid = ci > 0 && cj > 0;
-        const int b = valid ? bt_nibble(bt, nw, ci, cj) : 0;
+        const int b = valid ? bt_nibble(bt, nw, Psp, ci, cj) : 0;
         // nibble [eo > ee][fo > fe][E wins][F wins] (see step): the reference's
         // code is op | INSERT_EXT(4) | DELETE_EXT(8), the EXT bits being "not open".
         const int op = (b & 1) ? kOpD : (b & 2) ? kOpI : kOpM;
@@ -636,17 +861,18 @@ __global__ __launch_bounds__(256) void sw_trace_kernel(SwTraceArgs a)
 
 }  // namespace
 
-size_t dp_lds_bytes(int n1max, int n2max, bool profile)
+size_t dp_lds_bytes(int n1max, int n2max, bool profile, bool spiral)
 {
     // [rowH | rowF | altB or the profile | codeOf 256 | alpha 8]
     const size_t rows = sizeof(int) * (size_t(row_slots(n2max)) + size_t(fslots(n1max, n2max)));
+    if (spiral) return rows + size_t(std::max(alt_slots(n2max), (kStripe + spiral_period(n2max) + 3 * kGroup + 3) & ~3));
     return profile ? rows + size_t(dp_tail_bytes(n2max)) + 256 + 8 : rows + size_t(alt_slots(n2max));
 }
 
 hipError_t launch_dp(const SwDpArgs& a, int n1max, hipStream_t s)
 {
     if (a.n <= 0) return hipSuccess;
-    const size_t lds = dp_lds_bytes(n1max, a.n2max, a.fast && a.profile);
+    const size_t lds = dp_lds_bytes(n1max, a.n2max, a.fast && a.profile, a.fast && a.spiral);
     if (a.fast)
         hipLaunchKernelGGL(sw_dp_kernel<true>, dim3(a.n), dim3(64), lds, s, a);
     else
