@@ -359,6 +359,12 @@ int run(hc_sw_batch* b, hipStream_t s)
     d.fast = b->fast;
     d.profile = b->profile;
     d.spiral = b->spiral;
+    // Pairs per workgroup: one for region-sized windows (W2, n2 <= ~650: 8.62 /
+    // 9.09 / 9.20 ms at 1 / 2 / 4), four for long ones (W3, n2 ~ 1000: 3.54 /
+    // 3.25 / 2.90 ms); HC_SW_WPG overrides.
+    d.wpg = b->n2max > 800 ? 4 : 1;
+    if (const char* e = std::getenv("HC_SW_WPG"))
+        if (std::atoi(e) > 0) d.wpg = std::atoi(e);
     SwTraceArgs t{};
     t.pairs = b->pairs;
     t.res = b->res;

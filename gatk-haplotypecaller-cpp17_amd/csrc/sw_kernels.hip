@@ -48,6 +48,16 @@ __device__ __forceinline__ int shr1(int old, int v)
     return __builtin_amdgcn_update_dpp(old, v, 0x138, 0xf, 0xf, false);
 }
 
+// LDS ordering between the lanes of one wave (a pair is one wave; several
+// pairs may share a workgroup, so no workgroup barrier): the LDS executes a
+// wave's operations in order, the fences keep the compiler from moving them.
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ int wave_max(int v)
 {
     for (int o = 32; o; o >>= 1) v = max(v, __shfl_xor(v, o));
@@ -452,9 +462,9 @@ __device__ __forceinline__ void sp_group(SpLane& L, const SpConst& c, int t0, in
 __device__ int build_alphabet(const uint8_t* s1, int n1, int lane, uint8_t* codeOf, uint8_t* alpha)
 {
     reinterpret_cast<int*>(codeOf)[lane] = 0;
-    __syncthreads();
+    wave_sync();
     for (int x = lane; x < n1; x += 64) codeOf[s1[x]] = 1;
-    __syncthreads();
+    wave_sync();
     const uint32_t w = reinterpret_cast<const uint32_t*>(codeOf)[lane];
     const int c0 = (w & 0xff) != 0, c1 = (w & 0xff00) != 0, c2 = (w & 0xff0000) != 0, c3 = (w >> 24) != 0;
     const int cnt = c0 + c1 + c2 + c3;
@@ -465,7 +475,7 @@ __device__ int build_alphabet(const uint8_t* s1, int n1, int lane, uint8_t* code
     }
     const int K = __shfl(incl, 63);
     int r = incl - cnt;
-    __syncthreads();
+    wave_sync();
     uint32_t out = 0;
     const int cs[4] = {c0, c1, c2, c3};
 #pragma unroll
@@ -477,17 +487,20 @@ __device__ int build_alphabet(const uint8_t* s1, int n1, int lane, uint8_t* code
         }
     }
     reinterpret_cast<uint32_t*>(codeOf)[lane] = out;
-    __syncthreads();
+    wave_sync();
     return K;
 }
 
-template <bool FAST>
-__global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
+template <bool FAST, int WPG>
+__global__ __launch_bounds__(64 * WPG) void sw_dp_kernel(SwDpArgs a)
 {
     extern __shared__ int4 lds4[];
-    int* lds = reinterpret_cast<int*>(lds4);
-    const int lane = threadIdx.x;
-    const int p = a.order[blockIdx.x];
+    const int wave = WPG > 1 ? int(threadIdx.x >> 6) : 0;
+    const int lane = threadIdx.x & 63;
+    const int idx = int(blockIdx.x) * WPG + wave;
+    if (idx >= a.n) return;
+    int* lds = reinterpret_cast<int*>(lds4) + size_t(wave) * (a.lds_wave_bytes / sizeof(int));
+    const int p = a.order[idx];
     const SwPair P = a.pairs[p];
     const int n1 = __builtin_amdgcn_readfirstlane(P.n1);
     const int n2 = __builtin_amdgcn_readfirstlane(P.n2);
@@ -543,7 +556,7 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
             const int col = cc >= Pp ? cc - Pp : cc;
             altB[x] = (cc >= 0 && col < n2) ? s2[col] : 0;
         }
-        __syncthreads();
+        wave_sync();
         SpConst c;
         c.open = in_vgpr(open);
         c.extend = in_vgpr(extend);
@@ -607,7 +620,7 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
             q0 += kGroup;
             if (q0 >= Pp) q0 -= Pp;
         }
-        __syncthreads();
+        wave_sync();
     } else if (FAST) {
         hofs = open;
         // Row 0 in this path's form: H(0, j) + open, F(0, j) + extend.
@@ -628,7 +641,7 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
             for (int c = lane; c < kStripe + T + kGroup; c += 64)
                 altB[c] = (c >= kStripe && c < kStripe + n2) ? s2[c - kStripe] : 0;
         }
-        __syncthreads();
+        wave_sync();
         const int open_v = in_vgpr(open), extend_v = in_vgpr(extend);
         Scorer sr;
         sr.mp = in_vgpr(a.match - open);
@@ -660,7 +673,7 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
                     pstripe<false, false>(L, lane, n2, row_ok, T, btw, open_v, extend_v, rowH, rowF, sr);
             }
             if (row_ok) colG[i] = L.h;   // H(i, n2): frozen since the lane left column n2
-            __syncthreads();
+            wave_sync();
         }
     } else {
     // Row 0: H(0, j) = boundary, F(0, j) = LOW (PairWiseSW.h:72-75,198).
@@ -669,7 +682,7 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
         rowF[j] = kLow;
     }
     for (int c = lane; c < kStripe + T + kGroup; c += 64) altB[c] = (c >= kStripe && c < kStripe + n2) ? s2[c - kStripe] : 0;
-    __syncthreads();
+    wave_sync();
 
     for (int s = 0; s < nstripes; ++s) {
         const int i = s * kStripe + lane + 1;
@@ -687,14 +700,14 @@ __global__ __launch_bounds__(64) void sw_dp_kernel(SwDpArgs a)
         else
             stripe<false, FAST>(L, lane, n2, rb, row_ok, T, btw, sc, rowH, rowF, altB);
         if (row_ok) colG[i] = L.h;   // H(i, n2): frozen since the lane left column n2
-        __syncthreads();
+        wave_sync();
     }
     }
 
     __threadfence_block();   // this wave's colG stores complete before its lanes read them back
     int* colC = rowF;
     for (int x = lane + 1; x <= n1; x += 64) colC[x] = colG[x];
-    __syncthreads();
+    wave_sync();
 
     // End point (PairWiseSW.h:201-226): candidates in anti-diagonal order d =
     // 1..n1+n2, the last-row cell (n1, d-n1) before the last-column cell
@@ -872,11 +885,20 @@ size_t dp_lds_bytes(int n1max, int n2max, bool profile, bool spiral)
 hipError_t launch_dp(const SwDpArgs& a, int n1max, hipStream_t s)
 {
     if (a.n <= 0) return hipSuccess;
-    const size_t lds = dp_lds_bytes(n1max, a.n2max, a.fast && a.profile, a.fast && a.spiral);
-    if (a.fast)
-        hipLaunchKernelGGL(sw_dp_kernel<true>, dim3(a.n), dim3(64), lds, s, a);
-    else
-        hipLaunchKernelGGL(sw_dp_kernel<false>, dim3(a.n), dim3(64), lds, s, a);
+    SwDpArgs b = a;
+    b.lds_wave_bytes = int((dp_lds_bytes(n1max, a.n2max, a.fast && a.profile, a.fast && a.spiral) + 15) & ~size_t(15));
+    const int wpg = a.wpg == 4 ? 4 : a.wpg == 2 ? 2 : 1;
+    const size_t lds = size_t(b.lds_wave_bytes) * wpg;
+    const dim3 grid((a.n + wpg - 1) / wpg), block(64 * wpg);
+    if (a.fast) {
+        if (wpg == 4) hipLaunchKernelGGL((sw_dp_kernel<true, 4>), grid, block, lds, s, b);
+        else if (wpg == 2) hipLaunchKernelGGL((sw_dp_kernel<true, 2>), grid, block, lds, s, b);
+        else hipLaunchKernelGGL((sw_dp_kernel<true, 1>), grid, block, lds, s, b);
+    } else {
+        if (wpg == 4) hipLaunchKernelGGL((sw_dp_kernel<false, 4>), grid, block, lds, s, b);
+        else if (wpg == 2) hipLaunchKernelGGL((sw_dp_kernel<false, 2>), grid, block, lds, s, b);
+        else hipLaunchKernelGGL((sw_dp_kernel<false, 1>), grid, block, lds, s, b);
+    }
     return hipGetLastError();
 }
 

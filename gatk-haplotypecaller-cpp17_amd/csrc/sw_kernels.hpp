@@ -103,6 +103,8 @@ struct SwDpArgs {
     int fast;    // host-proven: no cutoff, no int32 overflow (sw_engine.cpp fast_ok)
     int profile;   // fast path with the LDS substitution profile (scores - open fit int16)
     int spiral;    // fast compare path in the spiral layout (backtrack words [group][lane])
+    int wpg;       // pairs (waves) per workgroup: 1, 2 or 4
+    int lds_wave_bytes;   // set by launch_dp
 };
 
 struct SwTraceArgs {
