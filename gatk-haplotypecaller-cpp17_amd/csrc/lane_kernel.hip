@@ -178,17 +178,20 @@ __global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
 // Column-segmented fp32 waves (host-planned). The wave's npairs pairs are the
 // slots slot0 .. slot0+npairs-1; pair g takes nb_g = ceil(H_g / BC) consecutive
 // lanes in slot order. Lanes past the last group idle (s = 0, no output).
+#ifndef HC_SEG_WPB
+#define HC_SEG_WPB 4   // seg waves per workgroup (A/B builds: 1, 2)
+#endif
 template <int OCC>
-__global__ __launch_bounds__(256, OCC) void phmm_seg_kernel(LaneArgs a)
+__global__ __launch_bounds__(64 * HC_SEG_WPB, OCC) void phmm_seg_kernel(LaneArgs a)
 {
     __shared__ float slut[kSlutLen];
     load_slut(slut, a.lut);
-    const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int wid = blockIdx.x * HC_SEG_WPB + (threadIdx.x >> 6);
     if (wid >= a.n_waves) return;
     const int lane = threadIdx.x & 63;
     const LaneWave wv = load_wave(a.waves, wid);
     const int bc = wv.ncols;
-    __shared__ uint2 mtab[4][5 * 64];
+    __shared__ uint2 mtab[HC_SEG_WPB][5 * 64];
     uint2* mt = mtab[threadIdx.x >> 6];
     // Lane -> (group, block): group g's lanes start at the prefix sum of nb.
     int* gmap = reinterpret_cast<int*>(mt);   // 128 ints, used before the match table
@@ -432,8 +435,8 @@ int seg_width_ceil(int bc)
 hipError_t launch_lane_seg_f32(const LaneArgs& a, hipStream_t s)
 {
     if (a.n_waves <= 0) return hipSuccess;
-    const int grid = (a.n_waves + 3) / 4;
-    hipLaunchKernelGGL((phmm_seg_kernel<kSegOcc>), dim3(grid), dim3(256), 0, s, a);
+    const int grid = (a.n_waves + HC_SEG_WPB - 1) / HC_SEG_WPB;
+    hipLaunchKernelGGL((phmm_seg_kernel<kSegOcc>), dim3(grid), dim3(64 * HC_SEG_WPB), 0, s, a);
     return hipGetLastError();
 }
 
