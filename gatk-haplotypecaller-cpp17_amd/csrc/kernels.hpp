@@ -109,17 +109,20 @@ constexpr int kSegMaxBC = 64;
 constexpr int kSegMinBC = 8;    // narrowest compiled fp32 block width
 
 // fp64 rescue pass in column-segmented form, planned on the device
-// (lane_kernel.hip rescue_plan_kernel). Two width tiers: bc[0] for the whole
-// pass (32, or 16 / 8 when the list is short), bc[1] = 32 for the haps too
-// long for 64 lanes at bc[0]. Class c = tier * 7 + k holds pairs of 2^k lanes
-// (64 >> k pairs per wave); class 14 = haps wider than 64 blocks of 32
+// (lane_kernel.hip rescue_plan_kernel). A pair takes a slot of 2^k lanes
+// (64 >> k pairs per wave) and the narrowest fp64 block width that covers its
+// hap on those lanes, so the slot's lanes are all used: (k, width) is its
+// class. Classes are numbered widest slot and block first (the longest waves
+// are dispatched first); the last class holds haps wider than 64 blocks of 32
 // (anti-diagonal kernel, through `big`).
-constexpr int kSeg64Classes = 15;
+constexpr int kSeg64Widths = 7;   // fp64 block widths 8, 12, ..., 32
+constexpr int kSeg64Classes = 7 * kSeg64Widths + 1;
+__host__ __device__ constexpr int seg64_width(int wi) { return 8 + 4 * wi; }
 struct Seg64Plan {
-    int bc[2];
+    int bc0;                        // block width bound of the pass (32, or 16 / 8 for short lists)
     int n_class[kSeg64Classes];
     int off_class[kSeg64Classes];   // class c's entries in `sorted` start here
-    int wave_base[kSeg64Classes];   // first wave of class c; [14] = total waves
+    int wave_base[kSeg64Classes];   // first wave of class c; [last] = total waves
 };
 struct Seg64Args {
     const PairDesc* pairs;

@@ -251,24 +251,27 @@ __global__ __launch_bounds__(64 * HC_SEG_WPB, OCC) void phmm_seg_kernel(LaneArgs
 // fp64 rescue pass (intel_pairhmm.hpp:137-139) in column-segmented form.
 //
 // The rescue list is built on the device by the fp32 pass, so the waves are
-// planned on the device too: rescue_plan_kernel picks the block width bc[0]
-// for the pass (32 columns, narrower when the list is too short to give every
-// SIMD two waves: short lists are latency-bound), puts every pair in class k =
-// ceil(log2(ceil(H/bc))) — a slot of 2^k lanes, 64/2^k pairs per wave — with
-// bc = bc[0], or bc[1] = 32 if that needs more than 64 lanes, and scatters the
-// list into class order (order inside a class is arbitrary; each pair's result
-// is independent of it). Pairs needing more than 64 lanes at 32 columns go to
-// the anti-diagonal fp64 kernel through `big`.
+// planned on the device too: rescue_plan_kernel picks the pass's block width
+// bound bc0 (32 columns, narrower when the list is too short to give every
+// SIMD two waves: short lists are latency-bound), gives every pair a slot of
+// 2^k lanes with k = ceil(log2(ceil(H/bc0))) (64 lanes if that needs more),
+// and then the narrowest fp64 width covering the hap on those 2^k lanes, so a
+// pair's slot has no idle lanes (a 1 100-column hap: 64 lanes of 20 columns,
+// not 35 lanes of 32 in a 64-lane slot). The list is scattered into class
+// order, classes with the longest waves first (order inside a class is
+// arbitrary; each pair's result is independent of it). Pairs needing more
+// than 64 lanes of 32 columns go to the anti-diagonal fp64 kernel through `big`.
 
 __device__ __forceinline__ int ceil_log2(int nb) { return nb <= 1 ? 0 : 32 - __clz(nb - 1); }
 
 __device__ __forceinline__ int rescue_class(int H, int bc0)
 {
     const int nb0 = (H + bc0 - 1) / bc0;
-    if (nb0 <= 64) return ceil_log2(nb0);
-    const int nb1 = (H + 31) / 32;
-    if (nb1 <= 64) return 7 + ceil_log2(nb1);
-    return 14;
+    const int k = nb0 <= 64 ? ceil_log2(nb0) : 6;
+    const int need = (H + (1 << k) - 1) >> k;   // columns per lane on 2^k lanes (<= bc0 when nb0 <= 64)
+    if (need > seg64_width(kSeg64Widths - 1)) return kSeg64Classes - 1;
+    const int wi = need <= 8 ? 0 : (need - 8 + 3) / 4;
+    return (6 - k) * kSeg64Widths + (kSeg64Widths - 1 - wi);
 }
 
 __global__ __launch_bounds__(1024) void rescue_plan_kernel(Seg64Args a)
@@ -285,7 +288,7 @@ __global__ __launch_bounds__(1024) void rescue_plan_kernel(Seg64Args a)
         *a.inker_reset = 0;
     }
     __syncthreads();
-    // Width: 32 unless the lanes at width 32 give fewer than min_lanes
+    // Width bound: 32 unless the lanes at width 32 give fewer than min_lanes
     // (2 waves per SIMD), then 16, then 8.
     unsigned long long mine = 0;
     for (int i = t; i < n; i += blockDim.x) mine += (a.pairs[a.list[i]].w + 31) / 32;
@@ -297,8 +300,7 @@ __global__ __launch_bounds__(1024) void rescue_plan_kernel(Seg64Args a)
     __syncthreads();
     if (t == 0) {
         Seg64Plan p;
-        p.bc[0] = bc0;
-        p.bc[1] = 32;
+        p.bc0 = bc0;
         int off = 0, wb = 0;
         for (int c = 0; c < NC; ++c) {
             p.n_class[c] = cnt[c];
@@ -307,7 +309,7 @@ __global__ __launch_bounds__(1024) void rescue_plan_kernel(Seg64Args a)
             off += cnt[c];
             p.wave_base[c] = wb;
             if (c < NC - 1) {
-                const int per = 64 >> (c % 7);
+                const int per = 64 >> (6 - c / kSeg64Widths);
                 wb += (cnt[c] + per - 1) / per;
             }
         }
@@ -350,11 +352,13 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
     const int lane = threadIdx.x & 63;
     const Seg64Plan* __restrict__ p = a.plan;
     const int total = __builtin_amdgcn_readfirstlane(p->wave_base[kSeg64Classes - 1]);
+    // Lane l holds the first wave of class l + 1: a wave's class is the number
+    // of class starts at or below it (wave_base is non-decreasing).
+    const int next_base = lane < kSeg64Classes - 1 ? p->wave_base[lane + 1] : INT32_MAX;
     for (int w = blockIdx.x * 4 + (threadIdx.x >> 6); w < total; w += gridDim.x * 4) {
-        int c = 0;
-        while (c < kSeg64Classes - 2 && __builtin_amdgcn_readfirstlane(p->wave_base[c + 1]) <= w) ++c;
-        const int k = c % 7;
-        const int bc = __builtin_amdgcn_readfirstlane(p->bc[c / 7]);
+        const int c = __popcll(__builtin_amdgcn_ballot_w64(next_base <= w));
+        const int k = 6 - c / kSeg64Widths;
+        const int bc = seg64_width(kSeg64Widths - 1 - c % kSeg64Widths);
         const int nk = __builtin_amdgcn_readfirstlane(p->n_class[c]);
         const int ok = __builtin_amdgcn_readfirstlane(p->off_class[c]);
         const int wk = w - __builtin_amdgcn_readfirstlane(p->wave_base[c]);
@@ -373,9 +377,12 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
         const bool wave_eq = __builtin_amdgcn_ballot_w64(!read_eq(w1)) == 0;
         double sumM = 0.0, sumX = 0.0;
         switch (bc) {
-        case 8: run_seg_bc<double, 8>(a.lut, slut, st, lane, s, cx, T0, sumM, sumX, mt, wave_eq); break;
-        case 16: run_seg_bc<double, 16>(a.lut, slut, st, lane, s, cx, T0, sumM, sumX, mt, wave_eq); break;
-        default: run_seg_bc<double, 32>(a.lut, slut, st, lane, s, cx, T0, sumM, sumX, mt, wave_eq); break;
+#define HC_SEG64_CASE(WI) \
+    case seg64_width(WI): run_seg_bc<double, seg64_width(WI)>(a.lut, slut, st, lane, s, cx, T0, sumM, sumX, mt, wave_eq); break;
+            HC_SEG64_CASE(0) HC_SEG64_CASE(1) HC_SEG64_CASE(2) HC_SEG64_CASE(3) HC_SEG64_CASE(4) HC_SEG64_CASE(5)
+            HC_SEG64_CASE(6)
+#undef HC_SEG64_CASE
+        default: break;
         }
         if (owner) a.raw_out[pid] = sumM + sumX;
         __builtin_amdgcn_wave_barrier();   // the next wave's match table reuses mt
