@@ -656,9 +656,11 @@ struct PlanScratch {
     std::vector<int64_t> row_off, gap_off, hap_w, hap_b;
     std::vector<uint8_t> hcls, cls, seg_bc, seg_nb, used, in_tail;
     std::vector<uint32_t> srec;   // (BC, nb, R) of the segmented pairs in sorted order
-    std::vector<uint32_t> hcand, key, id;
+    std::vector<uint32_t> hcand, key;
     std::vector<int> seg_in, one_ord, ord2[2], seg_ord, sort_tmp;
     std::vector<LaneWave> lw, ordered;
+    std::vector<int64_t> wcost;
+    std::vector<uint64_t> wkey;
     std::vector<std::vector<LaneWave>> part_w;
     std::vector<int64_t> hist;
 };
@@ -668,6 +670,137 @@ template <typename T>
 void grow(std::vector<T>& v, size_t n)
 {
     if (v.size() < n) v.resize(n);
+}
+
+// A hap's two segmented-wave candidates: nb0 = ceil(H / cap) lanes or one more,
+// each with the narrowest compiled width covering H.
+struct Cand {
+    uint8_t bc[2], nb[2];
+};
+static_assert(sizeof(Cand) == sizeof(uint32_t), "Cand packs into a word");
+
+// Modelled wave instructions of nb lanes of bc columns over R rows: 13 per
+// column + 26 per step, R + nb - 1 steps, times the lane-waste weight.
+inline float seg_cost(int nb, int bc, int R, const float* waste)
+{
+    return float(nb * (13 * bc + 26) * (R + nb - 1)) * waste[nb];
+}
+
+// Cross-product fast path of the planner (regions: hc_phmm_cross,
+// cross_regions, submit_regions) when every hap takes segmented waves. The
+// pairs of a block are reads x haps, so their sorted order need not be found
+// by sorting pairs: each hap takes one (BC, nb) candidate (chosen at its
+// block's mean read length), the block's haps are grouped by (BC, nb) and its
+// reads sorted by R, and a group's pairs in (read by R descending) x (hap)
+// order fill waves of floor(64 / nb) pairs — the order the general planner's
+// sort + greedy packing reaches on such a batch, built in one parallel pass
+// over segments (one per block and group; a segment's last wave may be
+// partial). Segments run widest block first, so co-resident waves share a
+// width's code. Writes every pair's descriptor, the slot order and the waves;
+// returns the batch's cells.
+int64_t plan_grid(const Local& loc, const int32_t* rlen, const int32_t* hlen, const int64_t* row_off,
+                  const int64_t* hap_w, const Cand* hcand, const float* waste, int qforce, PairDesc* pd,
+                  std::vector<int>& seg_ord, std::vector<LaneWave>& lw, PhaseTimer& tm)
+{
+    const PartSpec& spec = *loc.spec;
+    const size_t nblk = spec.blocks.size();
+    // Per block: reads by R descending, haps grouped by their (BC, nb) key.
+    std::vector<int> rord(size_t(loc.nr)), hord(size_t(loc.nh));
+    std::vector<uint16_t> hkey(size_t(loc.nh));
+    struct Seg {
+        uint32_t key;   // bc << 8 | nb
+        int blk;
+        int g0, G;      // haps hord[g0 .. g0 + G) (local ids)
+        int64_t n, slot0, w0;
+    };
+    std::vector<std::vector<Seg>> bsegs(nblk);
+    parallel_for(int64_t(nblk), [&](int64_t lo, int64_t hi) {
+        for (int64_t b = lo; b < hi; ++b) {
+            const Block& B = spec.blocks[size_t(b)];
+            const int64_t r0 = loc.blk_r[size_t(b)], h0 = loc.blk_h[size_t(b)];
+            int64_t rs = 0;
+            for (int r = 0; r < B.nr; ++r) {
+                rord[size_t(r0 + r)] = int(r0 + r);
+                rs += rlen[r0 + r];
+            }
+            std::stable_sort(rord.begin() + r0, rord.begin() + r0 + B.nr,
+                             [&](int x, int y) { return rlen[x] > rlen[y]; });
+            const int Rm = int((rs + B.nr / 2) / std::max(1, B.nr));
+            for (int h = 0; h < B.nh; ++h) {
+                const int lh = int(h0 + h);
+                const Cand cd = hcand[lh];
+                const int q = qforce >= 0 ? qforce
+                              : seg_cost(cd.nb[1], cd.bc[1], Rm, waste) < seg_cost(cd.nb[0], cd.bc[0], Rm, waste) ? 1
+                                                                                                                 : 0;
+                hkey[size_t(lh)] = uint16_t(cd.bc[q] << 8 | cd.nb[q]);
+                hord[size_t(lh)] = lh;
+            }
+            std::stable_sort(hord.begin() + h0, hord.begin() + h0 + B.nh,
+                             [&](int x, int y) { return hkey[size_t(x)] > hkey[size_t(y)]; });
+            auto& out = bsegs[size_t(b)];
+            out.clear();
+            for (int g = 0; g < B.nh;) {
+                const uint16_t k = hkey[size_t(hord[size_t(h0 + g)])];
+                int e = g;
+                while (e < B.nh && hkey[size_t(hord[size_t(h0 + e)])] == k) ++e;
+                out.push_back(Seg{k, int(b), int(h0 + g), e - g, int64_t(B.nr) * (e - g), 0, 0});
+                g = e;
+            }
+        }
+    }, 1);
+    tm.mark("grid: blocks");
+    std::vector<Seg> segs;
+    for (auto& v : bsegs) segs.insert(segs.end(), v.begin(), v.end());
+    std::stable_sort(segs.begin(), segs.end(), [](const Seg& x, const Seg& y) { return x.key > y.key; });
+    int64_t slots = 0, waves = 0;
+    for (Seg& g : segs) {
+        g.slot0 = slots;
+        g.w0 = waves;
+        slots += g.n;
+        waves += (g.n + 64 / int(g.key & 0xff) - 1) / (64 / int(g.key & 0xff));
+    }
+    seg_ord.resize(size_t(slots));
+    lw.resize(size_t(waves));
+    parallel_for(int64_t(segs.size()), [&](int64_t lo, int64_t hi) {
+        for (int64_t t = lo; t < hi; ++t) {
+            const Seg& g = segs[size_t(t)];
+            const Block& B = spec.blocks[size_t(g.blk)];
+            const int64_t r0 = loc.blk_r[size_t(g.blk)], h0 = loc.blk_h[size_t(g.blk)], p0 = loc.blk_p[size_t(g.blk)];
+            const int bc = int(g.key >> 8), nb = int(g.key & 0xff), per = 64 / nb;
+            int* o = seg_ord.data() + g.slot0;
+            int64_t i = 0;
+            for (int rr = 0; rr < B.nr; ++rr) {
+                const int64_t rowbase = p0 + (rord[size_t(r0 + rr)] - r0) * int64_t(B.nh) - h0;
+                for (int hh = 0; hh < g.G; ++hh) o[i++] = int(rowbase + hord[size_t(g.g0 + hh)]);
+            }
+            for (int64_t w = 0; w * per < g.n; ++w) {
+                const int64_t a = w * per, e = std::min(g.n, a + per);
+                const int Rmax = rlen[rord[size_t(r0 + a / g.G)]];
+                const int Rmin = rlen[rord[size_t(r0 + (e - 1) / g.G)]];
+                LaneWave v{};
+                v.slot0 = int(g.slot0 + a);
+                v.ncols = bc;
+                v.npairs = int(e - a);
+                v.rmax = Rmax;
+                v.rmin = Rmin;
+                v.nsteps = Rmax + nb - 1;
+                lw[size_t(g.w0 + w)] = v;
+            }
+        }
+    }, 1);
+    tm.mark("grid: slots + waves");
+    // Pair descriptors (read-major within each block, as Local::pairs).
+    std::atomic<int64_t> cells{0};
+    parallel_for(loc.np, [&](int64_t lo, int64_t hi) {
+        int64_t c = 0;
+        loc.pairs(lo, hi, [&](int64_t k, int64_t r, int64_t h) {
+            const int R = rlen[r], H = hlen[h];
+            pd[k] = PairDesc{int(row_off[r]), R, int(hap_w[h]), H};
+            c += int64_t(R) * H;
+        });
+        cells += c;
+    }, 16384);
+    return cells.load();
 }
 
 // Plan one part on device d: host binning + staging, then the H2D, device
@@ -877,9 +1010,6 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             }
         }
     }
-    struct Cand {
-        uint8_t bc[2], nb[2];
-    };
     static const std::array<float, 65> kHalfWaste = [] {
         std::array<float, 65> f{};
         for (int nb = 1; nb <= 64; ++nb) f[size_t(nb)] = std::sqrt(64.f / float((64 / nb) * nb));
@@ -894,7 +1024,6 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         return f;
     }();
     const float* waste = few_waves ? kPerLane.data() : kHalfWaste.data();
-    static_assert(sizeof(Cand) == sizeof(uint32_t), "Cand packs into a word");
     grow(S.hcand, size_t(nh));
     Cand* hcand = reinterpret_cast<Cand*>(S.hcand.data());
     parallel_for(nh, [&](int64_t lo, int64_t hi) {
@@ -914,200 +1043,214 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     }, 1 << 14);
     tm.mark("hap classes");
 
-    // Per pair: descriptor straight into the staging image, class, and for
-    // segmented pairs the cheaper candidate for its R.
-    grow(S.cls, size_t(npairs));
-    grow(S.seg_bc, size_t(npairs));
-    grow(S.seg_nb, size_t(npairs));
-    uint8_t *cls = S.cls.data(), *seg_bc = S.seg_bc.data(), *seg_nb = S.seg_nb.data();
     std::atomic<int64_t> cells_a{0};
-    std::atomic<int> rmin_a{INT32_MAX}, rmax_a{0};
-    const int qforce = int(env_i64("HC_PHMM_SEG_Q", -1));   // sweeps: force the nb0 (0) or nb0 + 1 (1) candidate
-    // Pairs per planning task (a 415 x 128 region call on the GPU box: 2.0 ms
-    // at 8192, 2.96 ms on one task; tools/region_ab.py).
-    const int64_t task_pairs = std::max<int64_t>(1024, env_i64("HC_PHMM_TASK_PAIRS", 8192));
-    const int T = int(std::min<int64_t>(64, std::max<int64_t>(1, npairs / task_pairs)));
-    const int64_t pchunk = (npairs + T - 1) / T;
-    std::vector<std::array<int64_t, 4>> tcnt(size_t(T) + 1);
-    WorkerPool::get().run(T, [&](int t) {
-        const int64_t lo = t * pchunk, hi = std::min(npairs, lo + pchunk);
-        // Plain restrict locals: the uint8_t stores below may alias anything,
-        // so anything reached through a capture would be reloaded per pair.
-        const int32_t* __restrict rl = rlen;
-        const int32_t* __restrict hl = hlen;
-        const int64_t* __restrict ro = row_off.data();
-        const int64_t* __restrict hw = hap_w.data();
-        const uint8_t* __restrict hc = hcls;
-        const Cand* __restrict cand = hcand;
-        PairDesc* __restrict pdo = pd;
-        uint8_t* __restrict clo = cls;
-        uint8_t* __restrict bco = seg_bc;
-        uint8_t* __restrict nbo = seg_nb;
-        int64_t c = 0, cn0 = 0, cn1 = 0, cn2 = 0, cn3 = 0;
-        int rlo = INT32_MAX, rhi = 0;
-        auto one = [=, &c, &cn0, &cn1, &cn2, &cn3, &rlo, &rhi](int64_t k, int64_t r, int64_t h) {
-            const int R = rl[r], H = hl[h];
-            pdo[k] = PairDesc{int(ro[r]), R, int(hw[h]), H};
-            c += int64_t(R) * H;
-            const int cl = hc[h];
-            clo[k] = uint8_t(cl);
-            if (cl == 0) {
-                ++cn0;
-                const Cand cd = cand[h];
-                // modelled wave instructions: nb lanes x (13 per column + 26 per
-                // step) x (R + nb - 1) steps, times half the lane waste of a
-                // wave of such pairs alone (floor(64 / nb) groups): uniform
-                // batches pack like that, mixed ones fill the gaps with others;
-                // with few waves, the wave's own time (per lane)
-                auto cost = [&](int q) {
-                    const int nb = cd.nb[q];
-                    return float(nb * (13 * cd.bc[q] + 26) * (R + nb - 1)) * waste[nb];
-                };
-                const int q = qforce >= 0 ? qforce : cost(1) < cost(0) ? 1 : 0;
-                bco[k] = cd.bc[q];
-                nbo[k] = cd.nb[q];
-                rlo = R < rlo ? R : rlo;
-                rhi = R > rhi ? R : rhi;
-            } else {
-                cn1 += cl == 1;
-                cn2 += cl == 2;
-                cn3 += cl == 3;
-            }
-        };
-        if (spec.flat) {
-            for (int64_t k = lo; k < hi; ++k) one(k, k, k);
-        } else {
-            loc.pairs(lo, hi, one);
-        }
-        cells_a += c;
-        tcnt[size_t(t) + 1] = {cn0, cn1, cn2, cn3};
-        int cur = rmin_a.load();
-        while (rlo < cur && !rmin_a.compare_exchange_weak(cur, rlo)) {
-        }
-        cur = rmax_a.load();
-        while (rhi > cur && !rmax_a.compare_exchange_weak(cur, rhi)) {
-        }
-    });
-    // Stable split of the pairs by class (per-task offsets, parallel scatter).
-    std::array<int64_t, 4> cls_tot{};
-    for (int t = 1; t <= T; ++t)
-        for (int q = 0; q < 4; ++q) {
-            const int64_t v = tcnt[size_t(t)][size_t(q)];
-            tcnt[size_t(t)][size_t(q)] = cls_tot[size_t(q)];
-            cls_tot[size_t(q)] += v;
-        }
-    std::vector<int>&seg_in = S.seg_in, &one_ord = S.one_ord, (&ord2)[2] = S.ord2;
-    seg_in.resize(size_t(cls_tot[0]));
-    one_ord.resize(size_t(cls_tot[1]));
-    ord2[0].resize(size_t(cls_tot[2]));
-    ord2[1].resize(size_t(cls_tot[3]));
-    WorkerPool::get().run(T, [&](int t) {
-        int* dst[4] = {seg_in.data(), one_ord.data(), ord2[0].data(), ord2[1].data()};
-        int64_t pos[4];
-        for (int q = 0; q < 4; ++q) pos[q] = tcnt[size_t(t) + 1][size_t(q)];
-        for (int64_t k = t * pchunk, e = std::min(npairs, k + pchunk); k < e; ++k) {
-            const int q = cls[size_t(k)];
-            dst[q][pos[q]++] = int(k);
-        }
-    });
-    tm.mark("pairs");
-    if (!seg_in.empty()) {
-        const int rlo = rmin_a.load(), rspan = rmax_a.load() - rlo + 1;
-        const int nbk = (kSegMaxBC / 2 + 1) * rspan;
-        if (nbk <= (1 << 18)) {
-            counting_sort_desc(seg_in, S.sort_tmp, S.hist, nbk,
-                               [&](int p) { return (seg_bc[size_t(p)] / 2) * rspan + (pd[p].y - rlo); });
-        } else {
-            std::vector<uint32_t>& key = S.key;
-            grow(key, size_t(npairs));
-            for (int p : seg_in) key[size_t(p)] = (uint32_t(seg_bc[size_t(p)]) << 16) | uint32_t(std::min(pd[p].y, 65535));
-            sort_desc(seg_in, key);
-        }
-    }
-    tm.mark("seg sort");
-    // Greedy packing in independent segments of the sorted list (one per task;
-    // a segment boundary costs at most one partly filled wave).
-    const int64_t ns = int64_t(seg_in.size());
+    std::vector<int>&one_ord = S.one_ord, (&ord2)[2] = S.ord2;
     std::vector<int>& seg_ord = S.seg_ord;
-    seg_ord.resize(size_t(ns));
     std::vector<LaneWave>& lw = S.lw;
     lw.clear();
-    {
-        const int T = int(std::min<int64_t>(64, std::max<int64_t>(1, ns / task_pairs)));
-        const int64_t chunk = (ns + T - 1) / T;
-        std::vector<std::vector<LaneWave>>& part_w = S.part_w;
-        if (part_w.size() < size_t(T)) part_w.resize(size_t(T));
-        for (auto& W : part_w) W.clear();
-        S.used.assign(size_t(ns), 0);
-        // The packing reads (BC, nb, R) of the pairs in sorted order: gather
-        // them once into a sequential array (one parallel pass of random
-        // reads, instead of three per look-ahead probe on one task per 16k
-        // pairs: 0.3 ms of a 415 x 128 region's planning on the GPU box).
-        std::vector<uint32_t>& srec = S.srec;
-        grow(srec, size_t(ns));
-        parallel_for(ns, [&](int64_t lo, int64_t hi) {
-            for (int64_t k = lo; k < hi; ++k) {
-                const int p = seg_in[size_t(k)];
-                srec[size_t(k)] = uint32_t(seg_bc[size_t(p)]) | uint32_t(seg_nb[size_t(p)]) << 8 |
-                                  uint32_t(std::min(pd[p].y, 65535)) << 16;
-            }
-        });
-        // Smallest nb of each width in the part: a wave whose free lanes drop
-        // below it cannot take another pair of its width, so its look-ahead
-        // stops there (a uniform region once scanned all 64 entries per wave).
-        std::array<uint8_t, kSegMaxBC + 1> minnb;
-        minnb.fill(64);
-        for (int64_t k = 0; k < ns; ++k) {
-            uint8_t& m = minnb[srec[size_t(k)] & 0xff];
-            m = std::min<uint8_t>(m, uint8_t(srec[size_t(k)] >> 8));
-        }
+    const int qforce = int(env_i64("HC_PHMM_SEG_Q", -1));   // sweeps: force the nb0 (0) or nb0 + 1 (1) candidate
+    // Cross products whose haps all take segmented waves (every region call):
+    // the structured planner (plan_grid); HC_PHMM_GRID_PLAN=0 forces the
+    // general one (A/B, tests).
+    bool grid = !spec.flat && env_i64("HC_PHMM_GRID_PLAN", 1) != 0;
+    for (int64_t h = 0; grid && h < nh; ++h) grid = hcls[size_t(h)] == 0;
+    if (grid) {
+        one_ord.clear();
+        ord2[0].clear();
+        ord2[1].clear();
+        cells_a = plan_grid(loc, rlen, hlen, row_off.data(), hap_w.data(), hcand, waste, qforce, pd, seg_ord, lw, tm);
+        tm.mark("grid: pairs");
+    } else {
+        // Per pair: descriptor straight into the staging image, class, and for
+        // segmented pairs the cheaper candidate for its R.
+        grow(S.cls, size_t(npairs));
+        grow(S.seg_bc, size_t(npairs));
+        grow(S.seg_nb, size_t(npairs));
+        uint8_t *cls = S.cls.data(), *seg_bc = S.seg_bc.data(), *seg_nb = S.seg_nb.data();
+        std::atomic<int> rmin_a{INT32_MAX}, rmax_a{0};
+        // Pairs per planning task (a 415 x 128 region call on the GPU box: 2.0 ms
+        // at 8192, 2.96 ms on one task; tools/region_ab.py).
+        const int64_t task_pairs = std::max<int64_t>(1024, env_i64("HC_PHMM_TASK_PAIRS", 8192));
+        const int T = int(std::min<int64_t>(64, std::max<int64_t>(1, npairs / task_pairs)));
+        const int64_t pchunk = (npairs + T - 1) / T;
+        std::vector<std::array<int64_t, 4>> tcnt(size_t(T) + 1);
         WorkerPool::get().run(T, [&](int t) {
-            const int64_t b = t * chunk, e = std::min(ns, b + chunk);
-            if (b >= e) return;
-            const int64_t m = e - b;
-            const int* __restrict in = seg_in.data() + b;
-            const uint32_t* __restrict rec = srec.data() + b;
-            int* __restrict ordo = seg_ord.data();
-            uint8_t* __restrict used = S.used.data() + b;
-            auto& W = part_w[size_t(t)];
-            int64_t slot_n = b;
-            constexpr int64_t kLook = 64;
-            for (int64_t i = 0; i < m; ++i) {
-                if (used[i]) continue;
-                const int bc = int(rec[i] & 0xff);
-                LaneWave w{};
-                w.slot0 = int(slot_n);
-                w.ncols = bc;
-                int rmin = INT32_MAX, rmax = 0, nst = 0, np = 0;
-                int free = 64;
-                const int need = minnb[size_t(bc)];
-                const int64_t jend = std::min(m, i + kLook);
-                for (int64_t j = i; j < jend && free >= need; ++j) {
-                    if (used[j]) continue;
-                    const uint32_t r = rec[j];
-                    if (int(r & 0xff) != bc) break;
-                    const int nb = int((r >> 8) & 0xff);
-                    if (nb > free) continue;
-                    used[j] = 1;
-                    free -= nb;
-                    ordo[slot_n++] = in[j];
-                    ++np;
-                    const int R = int(r >> 16);
-                    rmax = R > rmax ? R : rmax;
-                    rmin = R < rmin ? R : rmin;
-                    nst = R + nb - 1 > nst ? R + nb - 1 : nst;
+            const int64_t lo = t * pchunk, hi = std::min(npairs, lo + pchunk);
+            // Plain restrict locals: the uint8_t stores below may alias anything,
+            // so anything reached through a capture would be reloaded per pair.
+            const int32_t* __restrict rl = rlen;
+            const int32_t* __restrict hl = hlen;
+            const int64_t* __restrict ro = row_off.data();
+            const int64_t* __restrict hw = hap_w.data();
+            const uint8_t* __restrict hc = hcls;
+            const Cand* __restrict cand = hcand;
+            PairDesc* __restrict pdo = pd;
+            uint8_t* __restrict clo = cls;
+            uint8_t* __restrict bco = seg_bc;
+            uint8_t* __restrict nbo = seg_nb;
+            int64_t c = 0, cn0 = 0, cn1 = 0, cn2 = 0, cn3 = 0;
+            int rlo = INT32_MAX, rhi = 0;
+            auto one = [=, &c, &cn0, &cn1, &cn2, &cn3, &rlo, &rhi](int64_t k, int64_t r, int64_t h) {
+                const int R = rl[r], H = hl[h];
+                pdo[k] = PairDesc{int(ro[r]), R, int(hw[h]), H};
+                c += int64_t(R) * H;
+                const int cl = hc[h];
+                clo[k] = uint8_t(cl);
+                if (cl == 0) {
+                    ++cn0;
+                    const Cand cd = cand[h];
+                    // modelled wave instructions: nb lanes x (13 per column + 26 per
+                    // step) x (R + nb - 1) steps, times half the lane waste of a
+                    // wave of such pairs alone (floor(64 / nb) groups): uniform
+                    // batches pack like that, mixed ones fill the gaps with others;
+                    // with few waves, the wave's own time (per lane)
+                    auto cost = [&](int q) {
+                        const int nb = cd.nb[q];
+                        return float(nb * (13 * cd.bc[q] + 26) * (R + nb - 1)) * waste[nb];
+                    };
+                    const int q = qforce >= 0 ? qforce : cost(1) < cost(0) ? 1 : 0;
+                    bco[k] = cd.bc[q];
+                    nbo[k] = cd.nb[q];
+                    rlo = R < rlo ? R : rlo;
+                    rhi = R > rhi ? R : rhi;
+                } else {
+                    cn1 += cl == 1;
+                    cn2 += cl == 2;
+                    cn3 += cl == 3;
                 }
-                w.npairs = np;
-                w.rmax = rmax;
-                w.rmin = rmin;
-                w.nsteps = nst;
-                W.push_back(w);
+            };
+            if (spec.flat) {
+                for (int64_t k = lo; k < hi; ++k) one(k, k, k);
+            } else {
+                loc.pairs(lo, hi, one);
+            }
+            cells_a += c;
+            tcnt[size_t(t) + 1] = {cn0, cn1, cn2, cn3};
+            int cur = rmin_a.load();
+            while (rlo < cur && !rmin_a.compare_exchange_weak(cur, rlo)) {
+            }
+            cur = rmax_a.load();
+            while (rhi > cur && !rmax_a.compare_exchange_weak(cur, rhi)) {
             }
         });
-        size_t nw = 0;
-        for (auto& W : part_w) nw += W.size();
-        lw.reserve(nw);
-        for (auto& W : part_w) lw.insert(lw.end(), W.begin(), W.end());
+        // Stable split of the pairs by class (per-task offsets, parallel scatter).
+        std::array<int64_t, 4> cls_tot{};
+        for (int t = 1; t <= T; ++t)
+            for (int q = 0; q < 4; ++q) {
+                const int64_t v = tcnt[size_t(t)][size_t(q)];
+                tcnt[size_t(t)][size_t(q)] = cls_tot[size_t(q)];
+                cls_tot[size_t(q)] += v;
+            }
+        std::vector<int>& seg_in = S.seg_in;
+        seg_in.resize(size_t(cls_tot[0]));
+        one_ord.resize(size_t(cls_tot[1]));
+        ord2[0].resize(size_t(cls_tot[2]));
+        ord2[1].resize(size_t(cls_tot[3]));
+        WorkerPool::get().run(T, [&](int t) {
+            int* dst[4] = {seg_in.data(), one_ord.data(), ord2[0].data(), ord2[1].data()};
+            int64_t pos[4];
+            for (int q = 0; q < 4; ++q) pos[q] = tcnt[size_t(t) + 1][size_t(q)];
+            for (int64_t k = t * pchunk, e = std::min(npairs, k + pchunk); k < e; ++k) {
+                const int q = cls[size_t(k)];
+                dst[q][pos[q]++] = int(k);
+            }
+        });
+        tm.mark("pairs");
+        if (!seg_in.empty()) {
+            const int rlo = rmin_a.load(), rspan = rmax_a.load() - rlo + 1;
+            const int nbk = (kSegMaxBC / 2 + 1) * rspan;
+            if (nbk <= (1 << 18)) {
+                counting_sort_desc(seg_in, S.sort_tmp, S.hist, nbk,
+                                   [&](int p) { return (seg_bc[size_t(p)] / 2) * rspan + (pd[p].y - rlo); });
+            } else {
+                std::vector<uint32_t>& key = S.key;
+                grow(key, size_t(npairs));
+                for (int p : seg_in) key[size_t(p)] = (uint32_t(seg_bc[size_t(p)]) << 16) | uint32_t(std::min(pd[p].y, 65535));
+                sort_desc(seg_in, key);
+            }
+        }
+        tm.mark("seg sort");
+        // Greedy packing in independent segments of the sorted list (one per task;
+        // a segment boundary costs at most one partly filled wave).
+        const int64_t ns = int64_t(seg_in.size());
+        seg_ord.resize(size_t(ns));
+        {
+            const int T = int(std::min<int64_t>(64, std::max<int64_t>(1, ns / task_pairs)));
+            const int64_t chunk = (ns + T - 1) / T;
+            std::vector<std::vector<LaneWave>>& part_w = S.part_w;
+            if (part_w.size() < size_t(T)) part_w.resize(size_t(T));
+            for (auto& W : part_w) W.clear();
+            S.used.assign(size_t(ns), 0);
+            // The packing reads (BC, nb, R) of the pairs in sorted order: gather
+            // them once into a sequential array (one parallel pass of random
+            // reads, instead of three per look-ahead probe on one task per 16k
+            // pairs: 0.3 ms of a 415 x 128 region's planning on the GPU box).
+            std::vector<uint32_t>& srec = S.srec;
+            grow(srec, size_t(ns));
+            parallel_for(ns, [&](int64_t lo, int64_t hi) {
+                for (int64_t k = lo; k < hi; ++k) {
+                    const int p = seg_in[size_t(k)];
+                    srec[size_t(k)] = uint32_t(seg_bc[size_t(p)]) | uint32_t(seg_nb[size_t(p)]) << 8 |
+                                      uint32_t(std::min(pd[p].y, 65535)) << 16;
+                }
+            });
+            // Smallest nb of each width in the part: a wave whose free lanes drop
+            // below it cannot take another pair of its width, so its look-ahead
+            // stops there (a uniform region once scanned all 64 entries per wave).
+            std::array<uint8_t, kSegMaxBC + 1> minnb;
+            minnb.fill(64);
+            for (int64_t k = 0; k < ns; ++k) {
+                uint8_t& m = minnb[srec[size_t(k)] & 0xff];
+                m = std::min<uint8_t>(m, uint8_t(srec[size_t(k)] >> 8));
+            }
+            WorkerPool::get().run(T, [&](int t) {
+                const int64_t b = t * chunk, e = std::min(ns, b + chunk);
+                if (b >= e) return;
+                const int64_t m = e - b;
+                const int* __restrict in = seg_in.data() + b;
+                const uint32_t* __restrict rec = srec.data() + b;
+                int* __restrict ordo = seg_ord.data();
+                uint8_t* __restrict used = S.used.data() + b;
+                auto& W = part_w[size_t(t)];
+                int64_t slot_n = b;
+                constexpr int64_t kLook = 64;
+                for (int64_t i = 0; i < m; ++i) {
+                    if (used[i]) continue;
+                    const int bc = int(rec[i] & 0xff);
+                    LaneWave w{};
+                    w.slot0 = int(slot_n);
+                    w.ncols = bc;
+                    int rmin = INT32_MAX, rmax = 0, nst = 0, np = 0;
+                    int free = 64;
+                    const int need = minnb[size_t(bc)];
+                    const int64_t jend = std::min(m, i + kLook);
+                    for (int64_t j = i; j < jend && free >= need; ++j) {
+                        if (used[j]) continue;
+                        const uint32_t r = rec[j];
+                        if (int(r & 0xff) != bc) break;
+                        const int nb = int((r >> 8) & 0xff);
+                        if (nb > free) continue;
+                        used[j] = 1;
+                        free -= nb;
+                        ordo[slot_n++] = in[j];
+                        ++np;
+                        const int R = int(r >> 16);
+                        rmax = R > rmax ? R : rmax;
+                        rmin = R < rmin ? R : rmin;
+                        nst = R + nb - 1 > nst ? R + nb - 1 : nst;
+                    }
+                    w.npairs = np;
+                    w.rmax = rmax;
+                    w.rmin = rmin;
+                    w.nsteps = nst;
+                    W.push_back(w);
+                }
+            });
+            size_t nw = 0;
+            for (auto& W : part_w) nw += W.size();
+            lw.reserve(nw);
+            for (auto& W : part_w) lw.insert(lw.end(), W.begin(), W.end());
+        }
     }
     tm.mark("seg pack: greedy");
     // Dispatch order: the bulk in packing order (co-resident waves share one
@@ -1118,35 +1261,34 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         const int64_t tail_rounds = std::max<int64_t>(0, env_i64("HC_PHMM_TAIL_ROUNDS", 2));
         const size_t nw = lw.size();
         const size_t K = std::min(nw, size_t(tail_rounds) * 4 * size_t(dv.n_cu) * kSegWavesPerSimd);
-        auto cost = [&](size_t k) { return int64_t(lw[k].ncols) * lw[k].nsteps; };
+        std::vector<int64_t>& wc = S.wcost;
+        wc.resize(nw);
         int64_t cmin = INT64_MAX, cmax = 0;
         for (size_t k = 0; k < nw; ++k) {
-            cmin = std::min(cmin, cost(k));
-            cmax = std::max(cmax, cost(k));
+            wc[k] = int64_t(lw[k].ncols) * lw[k].nsteps;
+            cmin = std::min(cmin, wc[k]);
+            cmax = std::max(cmax, wc[k]);
         }
         // Waves of (nearly) equal length (one region's cross product) drain
         // evenly in any order: no reorder.
         if (K > 0 && K < nw && cmax * 20 > cmin * 21) {
-            std::vector<uint32_t>& id = S.id;
-            id.resize(nw);
-            std::iota(id.begin(), id.end(), 0u);
-            std::nth_element(id.begin(), id.begin() + long(K), id.end(), [&](uint32_t x, uint32_t y) {
-                return cost(x) != cost(y) ? cost(x) < cost(y) : x < y;
-            });
+            // Keys (cost, index) in one word each: the K shortest by one
+            // nth_element, then those longest first, ties in packing order.
+            std::vector<uint64_t>& key = S.wkey;
+            key.resize(nw);
+            for (size_t k = 0; k < nw; ++k) key[k] = uint64_t(wc[k]) << 32 | k;
+            std::nth_element(key.begin(), key.begin() + long(K), key.end());
+            for (size_t k = 0; k < K; ++k) key[k] = uint64_t(cmax - int64_t(key[k] >> 32)) << 32 | (key[k] & 0xffffffffu);
+            std::sort(key.begin(), key.begin() + long(K));
             std::vector<uint8_t>& in_tail = S.in_tail;
             in_tail.assign(nw, 0);
-            for (size_t k = 0; k < K; ++k) in_tail[id[k]] = 1;
+            for (size_t k = 0; k < K; ++k) in_tail[key[k] & 0xffffffffu] = 1;
             std::vector<LaneWave>& ordered = S.ordered;
             ordered.clear();
             ordered.reserve(nw);
             for (size_t k = 0; k < nw; ++k)
                 if (!in_tail[k]) ordered.push_back(lw[k]);
-            const size_t t0 = ordered.size();
-            for (size_t k = 0; k < nw; ++k)
-                if (in_tail[k]) ordered.push_back(lw[k]);
-            std::stable_sort(ordered.begin() + long(t0), ordered.end(), [](const LaneWave& x, const LaneWave& y) {
-                return int64_t(x.ncols) * x.nsteps > int64_t(y.ncols) * y.nsteps;
-            });
+            for (size_t k = 0; k < K; ++k) ordered.push_back(lw[key[k] & 0xffffffffu]);
             lw.swap(ordered);
         }
     }

@@ -134,7 +134,7 @@ struct Seg64Args {
     int* count_reset;         // the other run parity's counter, zeroed for the next run
     int* inker_reset;         // the other run parity's in-wave rescue counter, likewise
     int* sorted;              // list in class order (n entries)
-    int* big;                 // class 7 pairs
+    int* big;                 // last-class pairs (anti-diagonal fp64 kernel)
     int* big_count;
     Seg64Plan* plan;
     double* raw_out;          // raw f64 sums by pair id

@@ -144,3 +144,37 @@ def test_per_base_gap_reads_take_the_full_upload(engine, oracle_lib):
     b["ins"][rows] = rng.integers(33 + 5, 33 + 60, n, dtype=np.uint8)
     b["gcp"][rows] = rng.integers(33 + 5, 33 + 30, n, dtype=np.uint8)
     assert_same(engine.pairs(b), oracle_lib.pairs(b, nthreads=16), "mixed gaps")
+
+
+def _ragged_region(seed, n_reads, n_haps, long_hap=False, vary_gaps=False):
+    """A region with reads of lengths 20-150 and haps of lengths 30-415 (the
+    structured planner sorts reads by R and groups haps by block width)."""
+    rng = np.random.default_rng(seed)
+    reads, haps = W.region(n_reads=n_reads, n_haps=n_haps, seed=seed)
+    haps = [h[:int(rng.integers(30, len(h) + 1))] for h in haps]
+    if long_hap:   # longer than 64 blocks of 64 columns: one-lane kernel, general planner
+        haps[0] = rng.choice(np.frombuffer(b"ACGT", np.uint8), 4200).tobytes()
+    out = []
+    for b, q, i, d, c in reads:
+        n = int(rng.integers(20, len(b) + 1))
+        if vary_gaps and rng.random() < 0.3:
+            i = bytes(rng.integers(33 + 5, 33 + 60, len(i), dtype=np.uint8))
+        out.append((b[:n], q[:n], i[:n], d[:n], c[:n]))
+    return out, haps
+
+
+@pytest.mark.parametrize("grid", ["1", "0"])
+def test_region_planner_ragged_vs_oracle(engine, oracle_lib, monkeypatch, grid):
+    """hc_phmm_cross_regions through the structured cross-product planner
+    (HC_PHMM_GRID_PLAN=1, the default) and the general one (0): ragged reads
+    and haps, reads with varying gap qualities, a region whose hap needs the
+    one-lane kernel (general planner for that call), empty regions."""
+    monkeypatch.setenv("HC_PHMM_GRID_PLAN", grid)
+    regions = [_ragged_region(500 + k, nr, nh, vary_gaps=k % 2 == 1)
+               for k, (nr, nh) in enumerate([(415, 24), (90, 7), (1, 1), (200, 40)])]
+    regions.insert(2, ([], []))
+    for batch in (regions, [_ragged_region(600, 60, 5, long_hap=True)] + regions[:2]):
+        got = engine.cross_regions(batch)
+        for k, (g, e) in enumerate(zip(got, _regions_ref(oracle_lib, batch))):
+            assert g.shape == e.shape
+            assert np.array_equal(bits(g), bits(e)), f"grid={grid} region {k}"
