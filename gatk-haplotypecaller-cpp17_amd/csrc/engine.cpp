@@ -1258,7 +1258,11 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     // wave slots last, longest first (LPT, duration ~ BC * nsteps), so the chip
     // drains evenly. Waves address their pairs through slot0: no pair moves.
     {
-        const int64_t tail_rounds = std::max<int64_t>(0, env_i64("HC_PHMM_TAIL_ROUNDS", 2));
+        // Structured (region) plans keep their order: their waves are in width
+        // then read-length order already, and the reorder measured slower there
+        // (415 x 128 region: fp32 0.937 -> 0.908 ms without it, call 1.43 -> 1.30 ms,
+        // profiles/r02_region_dev_sweep.jsonl).
+        const int64_t tail_rounds = std::max<int64_t>(0, env_i64("HC_PHMM_TAIL_ROUNDS", grid ? 0 : 2));
         const size_t nw = lw.size();
         const size_t K = std::min(nw, size_t(tail_rounds) * 4 * size_t(dv.n_cu) * kSegWavesPerSimd);
         std::vector<int64_t>& wc = S.wcost;

@@ -7,4 +7,6 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_engine.py tests/test_gpu_re
 timeout -k 10 200 python -u tools/region_ab.py 128 HC_PHMM_GRID_PLAN=1,0 > gpurun_out/rab_${TAG}.jsonl 2>&1 || exit 1
 timeout -k 10 200 python -u tools/region_ab.py 32 HC_PHMM_GRID_PLAN=1,0 >> gpurun_out/rab_${TAG}.jsonl 2>&1 || exit 1
 timeout -k 10 200 python -u tools/region_ab.py 128 HC_PHMM_TAIL_ROUNDS=2,0 >> gpurun_out/rab_${TAG}.jsonl 2>&1 || exit 1
+timeout -k 10 200 python -u tools/region_ab.py 128 HC_PHMM_SEG_Q=-1,0,1 >> gpurun_out/rab_${TAG}.jsonl 2>&1 || exit 1
+timeout -k 10 200 python -u tools/region_ab.py 32 HC_PHMM_SEG_Q=-1,0,1 >> gpurun_out/rab_${TAG}.jsonl 2>&1 || exit 1
 HC_PHMM_TRACE=1 timeout -k 10 100 python -u tools/region_trace.py 128 > gpurun_out/rtrace_${TAG}.log 2>&1 || exit 1
