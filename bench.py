@@ -25,6 +25,7 @@ import argparse
 import glob
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -310,7 +311,7 @@ def end_to_end(hcphmm, W, batch, total_cells):
 def region_calls(hcphmm, W, no_cpu):
     """One active region (415 reads x N haps, hap ~415 bp, read 150 bp), the
     call shape of IntelPairHMM::compute_likelihoods (haplotypecaller.hpp:103):
-    host buffers in, doubles out. `call_ms` times the C call (argument structs
+    host buffers in, doubles out. `call_ms` times the C call (median of 30; argument structs
     built once, as a C++ caller holds them); `python_call_ms` includes building
     them from Python bytes each time. Then 64 such regions (415 x 32) in one
     cross-region call, and the same 64 as a stream of 8 submits of 8 regions."""
@@ -318,19 +319,21 @@ def region_calls(hcphmm, W, no_cpu):
     for nh in (32, 128):
         reads, haps = W.region(415, nh)
         call = hcphmm.CrossCall(reads, haps)
-        for _ in range(3):
+        for _ in range(5):
             call()
-        reps = 20
-        t0 = time.perf_counter()
-        for _ in range(reps):
+        ts = []
+        for _ in range(30):
+            t0 = time.perf_counter()
             call()
-        dt = (time.perf_counter() - t0) / reps
+            ts.append(time.perf_counter() - t0)
+        dt = statistics.median(ts)   # host-clock jitter on a shared box: median, mean beside it
         t0 = time.perf_counter()
         for _ in range(5):
             hcphmm.cross(reads, haps)
         dpy = (time.perf_counter() - t0) / 5
         flat = W.region_flat(reads, haps)
         ent = dict(reads=len(reads), haps=nh, cells=W.cells(flat), call_ms=round(dt * 1e3, 3),
+                   call_ms_mean=round(sum(ts) / len(ts) * 1e3, 3), call_ms_min=round(min(ts) * 1e3, 3),
                    python_call_ms=round(dpy * 1e3, 3), gcups=round(W.cells(flat) / dt / 1e9, 2))
         if not no_cpu:
             c1, _ = cpu_baseline(flat, 1, 1, "same region, 1 thread")

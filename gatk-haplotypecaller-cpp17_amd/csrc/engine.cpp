@@ -1507,6 +1507,16 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     return HC_PHMM_OK;
 }
 
+// HC_PHMM_TIMELINE=1: per-wave start / end / HW_ID of the last segmented fp32
+// pass (diagnostics; read back by hcx_timeline).
+struct Timeline {
+    std::mutex mu;
+    unsigned long long* buf = nullptr;
+    size_t cap = 0;
+    int n = 0;
+    hipStream_t stream = nullptr;
+} g_tl;
+
 int run_part(Part* b, hipStream_t s)
 {
     Device& dv = *b->dev;
@@ -1542,9 +1552,29 @@ int run_part(Part* b, hipStream_t s)
         a.lut64 = dv.lut_d;
         if (env_i64("HC_PHMM_RESCUE_IN_WAVE", 1) != 0) {
             a.inker_count = b->d_count + 2 + par;
-            a.inker_limit = int(std::max<int64_t>(0, env_i64("HC_PHMM_RESCUE_IN_WAVE_MAX", int64_t(4) * 4 * dv.n_cu)));
+            // A wave that rescues in place runs up to ~2.5x longer; a few such
+            // waves hide inside the pass, hundreds of them (a region whose reads
+            // miss some haps: ~440 rescues) drain late and cost more than the
+            // separate fp64 pass they would save (415 x 128 region: fp32
+            // 0.925 -> 0.80 ms at a cap of 32, S2's 19 rescues unchanged;
+            // profiles/r02_in_wave_rescue_cap.jsonl). Past the cap, the list.
+            a.inker_limit = int(std::max<int64_t>(0, env_i64("HC_PHMM_RESCUE_IN_WAVE_MAX", 32)));
         }
         b->inker_limit = a.inker_limit;
+        if (env_i64("HC_PHMM_TIMELINE", 0) != 0 && b->n_seg_waves > 0) {
+            std::lock_guard<std::mutex> lk(g_tl.mu);
+            const size_t need = size_t(b->n_seg_waves) * 3;
+            if (g_tl.cap < need) {
+                if (g_tl.buf) (void)hipFree(g_tl.buf);
+                g_tl.buf = nullptr;
+                g_tl.cap = 0;
+                HIP_TRY(hipMalloc(&g_tl.buf, need * sizeof(unsigned long long)));
+                g_tl.cap = need;
+            }
+            g_tl.n = b->n_seg_waves;
+            g_tl.stream = s;
+            a.timeline = g_tl.buf;
+        }
         b->launch_waves += b->lane_waves;
         const int n_one = b->lane_waves - b->n_seg_waves;
         const bool fork = b->n_seg_waves > 0 && n_one > 0;
@@ -2284,6 +2314,19 @@ double hcx_plan_pairs(int64_t n, const int64_t* read_off, const int32_t* R, cons
     }
     g_dry = false;
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / reps;
+}
+
+// The last traced segmented pass (HC_PHMM_TIMELINE=1): up to max_waves
+// records of {start, end, HW_ID} into out; returns the record count.
+int hcx_timeline(unsigned long long* out, int max_waves)
+{
+    std::lock_guard<std::mutex> lk(g_tl.mu);
+    if (!g_tl.buf || g_tl.n == 0) return 0;
+    const int n = std::min(max_waves, g_tl.n);
+    if (hipStreamSynchronize(g_tl.stream) != hipSuccess) return -1;
+    if (hipMemcpy(out, g_tl.buf, size_t(n) * 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return n;
 }
 
 double hcx_plan_regions(const hc_phmm_region* regions, int32_t n_regions, int n_cu, int reps)

@@ -89,6 +89,9 @@ struct LaneArgs {
     const double* lut64;
     int* inker_count;
     int inker_limit;
+    // Diagnostics (HC_PHMM_TIMELINE=1, seg waves only): per wave
+    // {start, end} of s_memrealtime (100 MHz) and the HW_ID register; null = off.
+    unsigned long long* timeline;
 };
 
 constexpr int kInWaveRescueMaxH = 512;   // one pair over 64 lanes of 8 columns

@@ -189,6 +189,7 @@ __global__ __launch_bounds__(64 * HC_SEG_WPB, OCC) void phmm_seg_kernel(LaneArgs
     const int wid = blockIdx.x * HC_SEG_WPB + (threadIdx.x >> 6);
     if (wid >= a.n_waves) return;
     const int lane = threadIdx.x & 63;
+    const unsigned long long t_start = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
     const LaneWave wv = load_wave(a.waves, wid);
     const int bc = wv.ncols;
     __shared__ uint2 mtab[HC_SEG_WPB][5 * 64];
@@ -245,6 +246,12 @@ __global__ __launch_bounds__(64 * HC_SEG_WPB, OCC) void phmm_seg_kernel(LaneArgs
     }
     const uint64_t todo = __builtin_amdgcn_ballot_w64(resc);
     if (todo) rescue_in_wave(a, todo, pid, lane, mt);
+    if (a.timeline && lane == 0) {
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        a.timeline[3 * size_t(wid)] = t_start;
+        a.timeline[3 * size_t(wid) + 1] = t_end;
+        a.timeline[3 * size_t(wid) + 2] = unsigned(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));
+    }
 }
 
 // ---------------------------------------------------------------------------
