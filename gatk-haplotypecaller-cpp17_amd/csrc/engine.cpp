@@ -441,6 +441,7 @@ namespace {
 
 constexpr int kW64Threshold = 768;     // anti-diagonal kernel: H above this -> one pair per wave
 constexpr int kLaneMaxH = 4096;        // longer haps stay on the anti-diagonal kernel (policy "auto")
+constexpr size_t kRowPadBefore = 256;     // words of slack before the packed rows (run_seg prefetch)
 constexpr int kSegWavesPerSimd = 3;    // resident seg waves per SIMD (phmm_seg_kernel occupancy)
 
 int lane_variant_id() { return int(env_i64("HC_PHMM_LANE_VARIANT", 0)); }
@@ -824,8 +825,9 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     int32_t* rlen = S.rlen.data();
     int32_t* gapw = S.gapw.data();
     int32_t* hlen = S.hlen.data();
-    std::atomic<int> bad_read{0}, bad_hap{0};
+    std::atomic<int> bad_read{0}, bad_hap{0}, rlen_max{0};
     parallel_for(nr, [&](int64_t lo, int64_t hi) {
+        int rm = 0;
         for (int64_t r = lo; r < hi; ++r) {
             const ReadView v = src.read(loc.read_id(r));
             if (v.len <= 0 || v.len > HC_PHMM_MAX_READ_LEN || !v.bases || !v.q || !v.i || !v.d || !v.c) {
@@ -835,8 +837,12 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
                 continue;
             }
             rlen[size_t(r)] = v.len;
+            rm = std::max(rm, v.len);
             gapw[size_t(r)] = constant_gaps(v) ? int32_t((v.i[0] & 127) | ((v.d[0] & 127) << 7) | ((v.c[0] & 127) << 14))
                                                : -1;
+        }
+        int cur = rlen_max.load();
+        while (rm > cur && !rlen_max.compare_exchange_weak(cur, rm)) {
         }
     }, 2048);
     if (bad_read.load()) return fail(HC_PHMM_EINVAL, "read with invalid length or null array");
@@ -1384,7 +1390,13 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     // Device region: the upload image, then packed rows / tables, outputs, scratch.
     Layout L;
     L.off = (upload + 255) & ~size_t(255);
-    const size_t o_rows = L.take(sizeof(uint32_t) * (size_t(nrows) + 16));
+    // Packed rows with slack on both sides: the segmented kernels prefetch
+    // read words PD steps ahead without clamping to the read (run_seg), so a
+    // lane in pipeline fill reads up to 64 words before its read and a pair
+    // shorter than its wave's longest read up to that length + 64 past it;
+    // those words only feed rows that are never used.
+    const size_t row_pad = kRowPadBefore + size_t(rlen_max.load()) + 256;
+    const size_t o_rows = L.take(sizeof(uint32_t) * (size_t(nrows) + row_pad));
     const size_t o_hapw = L.take(sizeof(uint32_t) * (size_t(hap_w[size_t(nh)]) + 16));
     const size_t o_res = L.take(res_bytes);
     const size_t o_list = L.take(sizeof(int) * n1);
@@ -1423,7 +1435,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     b->lane_waves = int(lw.size());
     b->upload_bytes = upload;
     b->d_pairs = reinterpret_cast<PairDesc*>(dev + o_pairs);
-    b->d_rows = reinterpret_cast<uint32_t*>(dev + o_rows);
+    b->d_rows = reinterpret_cast<uint32_t*>(dev + o_rows) + kRowPadBefore;
     b->d_hapw = reinterpret_cast<uint32_t*>(dev + o_hapw);
     const int Wc[2] = {16, 64};
     int* d_ord = reinterpret_cast<int*>(dev + o_ord);

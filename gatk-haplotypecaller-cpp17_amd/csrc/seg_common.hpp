@@ -147,15 +147,24 @@ __device__ __forceinline__ bool read_eq(uint32_t w1) { return read_cg(w1) && row
 
 __device__ __forceinline__ float from_left(float v)
 {
-    // DPP wave_shr:1: lane l receives lane l-1's v (lane 0 receives 0).
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+    // DPP wave_shr:1: lane l receives lane l-1's v; lane 0 receives 0 by
+    // bound_ctrl (no zeroed destination to materialise first).
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true));
 }
 __device__ __forceinline__ double from_left(double v)
 {
     const long long x = __double_as_longlong(v);
-    const unsigned lo = unsigned(__builtin_amdgcn_update_dpp(0, int(x), 0x138, 0xf, 0xf, false));
-    const unsigned hi = unsigned(__builtin_amdgcn_update_dpp(0, int(x >> 32), 0x138, 0xf, 0xf, false));
+    const unsigned lo = unsigned(__builtin_amdgcn_mov_dpp(int(x), 0x138, 0xf, 0xf, true));
+    const unsigned hi = unsigned(__builtin_amdgcn_mov_dpp(int(x >> 32), 0x138, 0xf, 0xf, true));
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// v & mask bitwise (mask all ones or zero): one full-rate v_and per 32 bits.
+__device__ __forceinline__ float masked(float v, uint32_t m) { return __uint_as_float(__float_as_uint(v) & m); }
+__device__ __forceinline__ double masked(double v, uint32_t m)
+{
+    const unsigned long long x = (unsigned long long)__double_as_longlong(v);
+    return __longlong_as_double((long long)(x & ((unsigned long long)m << 32 | m)));
 }
 
 // Step bounds of a column-segmented wave (wave-uniform).
@@ -267,8 +276,15 @@ __device__ __forceinline__ void run_seg(const T* __restrict__ lut, const T* __re
     RowConst<T> k;
     row_const<T>(lut, wc, cx.rrow[min(2, R) - 1], k);
     uint2 mrow = mt[k.rc * 64 + lane];
-    T y_out = T(0), t_out = T(0);   // handed to lane s+1: Y past column c0+BC, T[BC-1] of the last row
-    T t_hold = T(0);                // lane s-1's right-edge T of the previous row
+    // A pair's last block (and any lane past it) hands zeros to the lane on its
+    // right, so a group's first lane needs no select: it receives Y = 0 entering
+    // column 1 and T = 0 (column 0 below row 0) from its left neighbour, and
+    // T0 (row 0's diagonal) from its own initial t_hold on row 1. Inside a
+    // group, lane s-1's initial t_out is T0: lane s's row-1 diagonal.
+    const uint32_t keep = (s + 1) * BC < cx.H ? 0xffffffffu : 0u;
+    T y_out = T(0);                      // handed to lane s+1: Y past column c0+BC,
+    T t_out = masked(T0, keep);          //   T[BC-1] of the last row
+    T t_hold = T0;                       // lane s-1's right-edge T of the previous row
     const int lim0 = cx.H - c0;     // columns of this block inside the hap (<= 0: none)
     auto step = [&](int kk, auto sum_tag, auto ph_tag) {
         constexpr bool SUM = decltype(sum_tag)::value;
@@ -277,7 +293,10 @@ __device__ __forceinline__ void run_seg(const T* __restrict__ lut, const T* __re
         const uint32_t wn = wq[P];   // row i+1, loaded PD steps ago
         T pm_n = T(0), px_n = T(0);
         uint2 m_n = mrow;
-        int ridx = min(max(i + PD + 1, 1), R) - 1;   // the word needed PD steps from now
+        // The word needed PD steps from now (row i + PD + 1). Not clamped to
+        // the read: outside rows 1..R it feeds only rows no result depends on,
+        // and the packed rows carry slack on both sides (engine.cpp o_rows).
+        int ridx = i + PD;
         if constexpr (CG) {   // next row's prior constants (LDS) and match words
             const int qo = row_q(wn), mo = row_rc(wn) * 64 + lane;
             // Order the load after the last use of wn, so the word can land in
@@ -299,9 +318,10 @@ __device__ __forceinline__ void run_seg(const T* __restrict__ lut, const T* __re
             sX_in = from_left(sumX);
         }
         // Row 1's diagonal is row 0's T at every column; below that, lane
-        // s-1's right edge (column 0 for block 0: T[i][0] = 0 for i >= 1).
-        const T Tdiag = i == 1 ? T0 : (s ? t_hold : T(0));
-        const T Yl0 = s ? y_in : T(0);   // block 0: Y[i][1] = 0*my + 0*yy = 0
+        // s-1's right edge (column 0 for block 0: T[i][0] = 0 for i >= 1,
+        // handed as 0 by the left neighbour, see keep).
+        const T Tdiag = t_hold;
+        const T Yl0 = y_in;   // block 0: Y[i][1] = 0*my + 0*yy = 0 (likewise)
         t_hold = t_in;
         if (unsigned(i - 1) < unsigned(st.rmax)) {
             if constexpr (!CG) {
@@ -317,8 +337,8 @@ __device__ __forceinline__ void run_seg(const T* __restrict__ lut, const T* __re
             T Ml = T(0), Yl = Yl0;
             const T M0 = Tdiag * prior_of<31>(mrow.x, k.pm, k.px);
             cell<T, BC, 0, BC, SUM, EQ>(Tt, X, M0, Ml, Yl, mrow.x, mrow.y, k.pm, k.px, k, lim, sumM, sumX);
-            y_out = y_next<EQ>(Ml, Yl, k.my, k.yy);
-            t_out = Tt[BC - 1];
+            y_out = masked(y_next<EQ>(Ml, Yl, k.my, k.yy), keep);
+            t_out = masked(Tt[BC - 1], keep);
             if constexpr (CG) {
                 k.pm = pm_n;
                 k.px = px_n;
