@@ -18,6 +18,7 @@
 #include "../../include/hc_gt.h"
 #include "../../include/hc_pairhmm.h"
 #include "gt_kernels.hpp"
+#include "pool.hpp"
 
 // MathUtils Jacobian table as g++ folds it at compile time (tools/gen_jacobian.py).
 #include "math_jacobian.inc"
@@ -92,8 +93,9 @@ size_t up(size_t x) { return (x + 255) & ~size_t(255); }
 int run(const hc_gt_site* sites, int32_t n)
 {
     // Validate; one upload per distinct matrix.
-    std::unordered_map<const double*, int64_t> mat_at;
-    std::vector<const hc_gt_site*> mats;
+    std::unordered_map<const double*, int32_t> mat_at;   // matrix -> index in mats
+    std::vector<const hc_gt_site*> mats;                  // first site naming each matrix
+    std::vector<int64_t> mat_off;                         // its offset in the L image
     std::vector<GtSite> ds(static_cast<size_t>(n));
     int64_t L_total = 0, keep_total = 0, map_total = 0, al_total = 0, out_total = 0;
     for (int32_t s = 0; s < n; ++s) {
@@ -110,12 +112,16 @@ int run(const hc_gt_site* sites, int32_t n)
                 return fail(HC_PHMM_EINVAL, "site " + std::to_string(s) + ": haplotype allele out of range");
         auto it = mat_at.find(x.L);
         if (it == mat_at.end()) {
-            it = mat_at.emplace(x.L, L_total).first;
+            it = mat_at.emplace(x.L, int32_t(mats.size())).first;
             mats.push_back(&x);
+            mat_off.push_back(L_total);
             L_total += int64_t(x.n_reads) * x.n_haps;
+        } else if (mats[size_t(it->second)]->n_reads != x.n_reads || mats[size_t(it->second)]->n_haps != x.n_haps) {
+            // A matrix pointer shared by sites must describe the same shape.
+            return fail(HC_PHMM_EINVAL, "sites sharing a matrix disagree on its shape");
         }
         GtSite& d = ds[size_t(s)];
-        d.L_off = it->second;
+        d.L_off = mat_off[size_t(it->second)];
         d.al_off = al_total;
         d.n_haps = x.n_haps;
         d.keep_off = int32_t(keep_total);
@@ -129,16 +135,6 @@ int run(const hc_gt_site* sites, int32_t n)
         out_total += x.n_alleles * (x.n_alleles + 1) / 2;
         if (keep_total > INT32_MAX || map_total > INT32_MAX || out_total > INT32_MAX)
             return fail(HC_PHMM_EINVAL, "too many sites for one call");
-    }
-    // A matrix pointer shared by sites must describe the same shape.
-    for (int32_t s = 0; s < n; ++s) {
-        const hc_gt_site& x = sites[s];
-        const hc_gt_site* m = mats[size_t(std::lower_bound(mats.begin(), mats.end(), x.L,
-                                                           [&](const hc_gt_site* a, const double* b) {
-                                                               return mat_at[a->L] < mat_at[b];
-                                                           }) - mats.begin())];
-        if (m->n_reads != x.n_reads || m->n_haps != x.n_haps)
-            return fail(HC_PHMM_EINVAL, "sites sharing a matrix disagree on its shape");
     }
     // Layout: [sites | L | keep | amap] uploaded, then [gl | gi | gq] read back, then scratch.
     const size_t o_sites = 0;
@@ -156,15 +152,31 @@ int run(const hc_gt_site* sites, int32_t n)
     if (rc) return rc;
     char* h = g_host;
     std::memcpy(h + o_sites, ds.data(), sizeof(GtSite) * size_t(n));
-    for (const auto* m : mats)
-        std::memcpy(h + o_L + sizeof(double) * size_t(mat_at[m->L]), m->L,
-                    sizeof(double) * size_t(m->n_reads) * size_t(m->n_haps));
+    // The likelihood matrices dominate the upload (512 regions of 415 x 32:
+    // 54 MB): staged by the engine's worker pool, in slices so each slice's
+    // H2D starts while the next is being copied.
+    const int64_t nm = int64_t(mats.size());
+    const int64_t slices = std::min<int64_t>(nm, 8);
+    size_t sent = 0;
+    for (int64_t sl = 0; sl < slices; ++sl) {
+        const int64_t m0 = nm * sl / slices, m1 = nm * (sl + 1) / slices;
+        hcphmm::parallel_for(m1 - m0, [&](int64_t lo, int64_t hi) {
+            for (int64_t k = m0 + lo; k < m0 + hi; ++k) {
+                const hc_gt_site* m = mats[size_t(k)];
+                std::memcpy(h + o_L + sizeof(double) * size_t(mat_off[size_t(k)]), m->L,
+                            sizeof(double) * size_t(m->n_reads) * size_t(m->n_haps));
+            }
+        }, 1);
+        const size_t end = m1 < nm ? o_L + sizeof(double) * size_t(mat_off[size_t(m1)]) : o_keep;
+        HIP_TRY(hipMemcpyAsync(g_dev + sent, h + sent, end - sent, hipMemcpyHostToDevice, g_stream));
+        sent = end;
+    }
     for (int32_t s = 0; s < n; ++s) {
         const hc_gt_site& x = sites[s];
         if (x.n_keep) std::memcpy(h + o_keep + sizeof(int32_t) * size_t(ds[size_t(s)].keep_off), x.keep, sizeof(int32_t) * size_t(x.n_keep));
         std::memcpy(h + o_map + sizeof(int32_t) * size_t(ds[size_t(s)].map_off), x.hap_allele, sizeof(int32_t) * size_t(x.n_haps));
     }
-    HIP_TRY(hipMemcpyAsync(g_dev, h, in_bytes, hipMemcpyHostToDevice, g_stream));
+    HIP_TRY(hipMemcpyAsync(g_dev + sent, h + sent, in_bytes - sent, hipMemcpyHostToDevice, g_stream));
     GtArgs a{};
     a.sites = reinterpret_cast<const GtSite*>(g_dev + o_sites);
     a.n = n;
