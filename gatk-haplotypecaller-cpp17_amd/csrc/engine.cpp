@@ -358,6 +358,16 @@ struct PhaseTimer {
 // of plan_part in a container without a GPU.
 bool g_dry = false;
 
+// The last dry-run plan (hcx_dump_sizes / hcx_dump_plan).
+struct DryDump {
+    std::mutex mu;
+    std::vector<int4> pairs;
+    std::vector<int> order;
+    std::vector<LaneWave> waves;
+    int n_seg_slots = 0;
+    bool grid = false;
+} g_dump;
+
 int64_t env_i64(const char* name, int64_t dflt)
 {
     const char* e = std::getenv(name);
@@ -1383,6 +1393,15 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     }, 256);
     tm.mark("staging fill");
     if (g_dry) {
+        // Dry runs keep the last part's plan for the host-logic tests
+        // (hcx_dump_*): pair descriptors, slot order, segmented waves.
+        std::lock_guard<std::mutex> lk(g_dump.mu);
+        g_dump.pairs.assign(pd, pd + npairs);
+        g_dump.order.assign(seg_ord.begin(), seg_ord.end());
+        g_dump.order.insert(g_dump.order.end(), one_ord.begin(), one_ord.end());
+        g_dump.waves.assign(lw.begin(), lw.begin() + n_seg_waves);
+        g_dump.n_seg_slots = n_seg_slots;
+        g_dump.grid = grid;
         *out = nullptr;
         return HC_PHMM_OK;
     }
@@ -2339,6 +2358,38 @@ int hcx_timeline(unsigned long long* out, int max_waves)
     if (hipMemcpy(out, g_tl.buf, size_t(n) * 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
         return -1;
     return n;
+}
+
+// Sizes of the last dry-run plan: {pairs, order entries, segmented slots,
+// segmented waves, structured (1) or general (0) planner}.
+void hcx_dump_sizes(int64_t* out5)
+{
+    std::lock_guard<std::mutex> lk(g_dump.mu);
+    out5[0] = int64_t(g_dump.pairs.size());
+    out5[1] = int64_t(g_dump.order.size());
+    out5[2] = g_dump.n_seg_slots;
+    out5[3] = int64_t(g_dump.waves.size());
+    out5[4] = g_dump.grid ? 1 : 0;
+}
+
+// The last dry-run plan: pairs as {row offset, R, table offset, H}, the slot
+// order, and per segmented wave {slot0, rmax, rmin, ncols, npairs, nsteps}.
+void hcx_dump_plan(int32_t* pairs4, int32_t* order, int32_t* waves6)
+{
+    std::lock_guard<std::mutex> lk(g_dump.mu);
+    for (size_t k = 0; k < g_dump.pairs.size(); ++k) {
+        const int4 p = g_dump.pairs[k];
+        pairs4[4 * k] = p.x;
+        pairs4[4 * k + 1] = p.y;
+        pairs4[4 * k + 2] = p.z;
+        pairs4[4 * k + 3] = p.w;
+    }
+    std::copy(g_dump.order.begin(), g_dump.order.end(), order);
+    for (size_t w = 0; w < g_dump.waves.size(); ++w) {
+        const LaneWave& v = g_dump.waves[w];
+        const int32_t f[6] = {v.slot0, v.rmax, v.rmin, v.ncols, v.npairs, v.nsteps};
+        std::copy(f, f + 6, waves6 + 6 * w);
+    }
 }
 
 double hcx_plan_regions(const hc_phmm_region* regions, int32_t n_regions, int n_cu, int reps)

@@ -1,0 +1,105 @@
+"""CPU: the host planner's output, checked without a GPU. The library plans a
+batch in dry-run mode (hcx_plan_* with a modelled device, no HIP calls) and
+hands back the plan (hcx_dump_*): pair descriptors, slot order, and the
+column-segmented waves the fp32 kernel would run. Both planners — the
+structured cross-product one (regions) and the general one (flat pairs, and
+regions with HC_PHMM_GRID_PLAN=0) — must give a plan the kernel can run
+exactly: every pair in exactly one slot, every wave's pairs fitting its 64
+lanes at its block width (phmm_seg_kernel's lane -> group map), the wave's
+row bounds and step count covering its pairs (run_seg's SegSteps)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import hcphmm
+import workloads as W
+
+WIDTHS = set(range(8, 65, 2))   # HC_SEG_WIDTHS (seg_common.hpp)
+
+
+@pytest.fixture(scope="module")
+def L():
+    lib = hcphmm.lib()
+    lib.hcx_plan_regions.restype = C.c_double
+    lib.hcx_plan_regions.argtypes = [C.c_void_p, C.c_int32, C.c_int, C.c_int]
+    lib.hcx_plan_pairs.restype = C.c_double
+    lib.hcx_dump_sizes.argtypes = [C.c_void_p]
+    lib.hcx_dump_plan.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    return lib
+
+
+def dump(L):
+    sz = np.zeros(5, np.int64)
+    L.hcx_dump_sizes(sz.ctypes.data)
+    n_pairs, n_order, n_seg, n_waves, grid = (int(x) for x in sz)
+    pairs = np.zeros((max(n_pairs, 1), 4), np.int32)
+    order = np.zeros(max(n_order, 1), np.int32)
+    waves = np.zeros((max(n_waves, 1), 6), np.int32)
+    L.hcx_dump_plan(pairs.ctypes.data, order.ctypes.data, waves.ctypes.data)
+    return pairs[:n_pairs], order[:n_order], n_seg, waves[:n_waves], grid
+
+
+def check_plan(pairs, order, n_seg, waves, R, H):
+    n = len(R)
+    assert len(pairs) == n
+    assert np.array_equal(pairs[:, 1], R) and np.array_equal(pairs[:, 3], H)
+    seg = order[:n_seg]
+    assert len(np.unique(order)) == len(order) == n          # every pair in exactly one slot
+    assert n_seg == n                                         # every hap here is in segmented reach
+    w = waves[np.argsort(waves[:, 0], kind="stable")]
+    starts = np.concatenate([[0], np.cumsum(w[:, 4])[:-1]])
+    assert np.array_equal(w[:, 0], starts) and w[:, 4].sum() == n_seg   # slots partitioned by waves
+    for slot0, rmax, rmin, bc, npairs, nsteps in w:
+        assert bc in WIDTHS and 1 <= npairs <= 64
+        p = seg[slot0:slot0 + npairs]
+        nb = -(-H[p] // bc)
+        assert nb.sum() <= 64 and nb.max() <= 64
+        assert rmax == R[p].max() and rmin == R[p].min()
+        assert nsteps == (R[p] + nb - 1).max()
+
+
+def ragged_region(seed, nr, nh):
+    rng = np.random.default_rng(seed)
+    reads, haps = W.region(n_reads=nr, n_haps=nh, seed=seed)
+    haps = [h[:int(rng.integers(30, len(h) + 1))] for h in haps]
+    reads = [tuple(x[:int(rng.integers(20, len(r[0]) + 1))] for x in r) for r in reads]
+    return reads, haps
+
+
+@pytest.mark.parametrize("grid", ["1", "0"])
+def test_region_plans_are_exact(L, monkeypatch, grid):
+    monkeypatch.setenv("HC_PHMM_GRID_PLAN", grid)
+    regions = [ragged_region(700 + k, nr, nh) for k, (nr, nh) in enumerate([(415, 24), (90, 7), (1, 1), (200, 40)])]
+    regions.insert(2, ([], []))
+    arr, outs, keep = hcphmm._region_array(regions)
+    assert L.hcx_plan_regions(arr, len(regions), 256, 1) >= 0
+    pairs, order, n_seg, waves, used_grid = dump(L)
+    assert used_grid == int(grid)
+    R = np.concatenate([np.repeat([len(r[0]) for r in rd], len(hp)) for rd, hp in regions if rd and hp])
+    H = np.concatenate([np.tile([len(h) for h in hp], len(rd)) for rd, hp in regions if rd and hp])
+    check_plan(pairs, order, n_seg, waves, R, H)
+
+
+@pytest.mark.parametrize("wl", ["S1", "S2:20000", "S4"])
+def test_flat_plans_are_exact(L, wl):
+    name, _, n = wl.partition(":")
+    b = W.config(name, int(n) if n else None)
+    args, keep = hcphmm._flat_args(b)
+    L.hcx_plan_pairs(*args, C.c_int(256), C.c_int(1), C.c_int(1))
+    pairs, order, n_seg, waves, used_grid = dump(L)
+    assert used_grid == 0
+    check_plan(pairs, order, n_seg, waves, b["R"].astype(np.int64), b["H"].astype(np.int64))
+
+
+def test_region_plan_uses_full_waves(L):
+    """The structured plan of a uniform region fills its waves: at most one
+    partly filled wave per (hap group)."""
+    reads, haps = W.region(415, 128)
+    arr, outs, keep = hcphmm._region_array([(reads, haps)])
+    L.hcx_plan_regions(arr, 1, 256, 1)
+    pairs, order, n_seg, waves, used_grid = dump(L)
+    assert used_grid == 1
+    lanes = [(-(-pairs[order[s0:s0 + np_], 3] // bc)).sum() for s0, _, _, bc, np_, _ in waves]
+    groups = len({(bc, -(-int(pairs[order[s0], 3]) // bc)) for s0, _, _, bc, _, _ in waves})
+    assert sum(1 for x in lanes if x + 7 < 64) <= groups
