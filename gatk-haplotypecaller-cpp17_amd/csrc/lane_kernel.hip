@@ -299,7 +299,7 @@ __global__ __launch_bounds__(1024) void rescue_plan_kernel(Seg64Args a)
     // (2 waves per SIMD), then 16, then 8.
     unsigned long long mine = 0;
     for (int i = t; i < n; i += blockDim.x) mine += (a.pairs[a.list[i]].w + 31) / 32;
-    atomicAdd(&lanes_sh, mine);
+    if (mine) atomicAdd(&lanes_sh, mine);   // an empty list (most runs) takes no atomics
     __syncthreads();
     const long long l32 = (long long)lanes_sh;
     const int bc0 = l32 >= a.min_lanes ? 32 : (2 * l32 >= a.min_lanes ? 16 : 8);
@@ -354,11 +354,12 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
 {
     __shared__ uint2 mtab[4][5 * 64];
     __shared__ double slut[kSlutLen];
+    const Seg64Plan* __restrict__ p = a.plan;
+    const int total = __builtin_amdgcn_readfirstlane(p->wave_base[kSeg64Classes - 1]);
+    if (int(blockIdx.x) * 4 >= total) return;   // workgroup-uniform: an empty or short list costs no LDS fill
     load_slut(slut, a.lut);
     uint2* mt = mtab[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
-    const Seg64Plan* __restrict__ p = a.plan;
-    const int total = __builtin_amdgcn_readfirstlane(p->wave_base[kSeg64Classes - 1]);
     // Lane l holds the first wave of class l + 1: a wave's class is the number
     // of class starts at or below it (wave_base is non-decreasing).
     const int next_base = lane < kSeg64Classes - 1 ? p->wave_base[lane + 1] : INT32_MAX;
