@@ -660,6 +660,13 @@ struct Local {
     }
 };
 
+// A hap's two segmented-wave candidates: nb0 = ceil(H / cap) lanes or one more,
+// each with the narrowest compiled width covering H.
+struct Cand {
+    uint8_t bc[2], nb[2];
+};
+static_assert(sizeof(Cand) == sizeof(uint32_t), "Cand packs into a word");
+
 // Grow-only per-thread scratch of the planner: fresh large vectors would be
 // fresh mmap'd pages, zero-filled by the kernel on first touch, every call.
 struct PlanScratch {
@@ -668,6 +675,7 @@ struct PlanScratch {
     std::vector<uint8_t> hcls, cls, seg_bc, seg_nb, used, in_tail;
     std::vector<uint32_t> srec;   // (BC, nb, R) of the segmented pairs in sorted order
     std::vector<uint32_t> hcand, key;
+    std::vector<Cand> ctab;
     std::vector<int> seg_in, one_ord, ord2[2], seg_ord, sort_tmp;
     std::vector<LaneWave> lw, ordered;
     std::vector<int64_t> wcost;
@@ -683,12 +691,6 @@ void grow(std::vector<T>& v, size_t n)
     if (v.size() < n) v.resize(n);
 }
 
-// A hap's two segmented-wave candidates: nb0 = ceil(H / cap) lanes or one more,
-// each with the narrowest compiled width covering H.
-struct Cand {
-    uint8_t bc[2], nb[2];
-};
-static_assert(sizeof(Cand) == sizeof(uint32_t), "Cand packs into a word");
 
 // Modelled wave instructions of nb lanes of bc columns over R rows: 13 per
 // column + 26 per step, R + nb - 1 steps, times the lane-waste weight.
@@ -951,49 +953,51 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const double ravg = double(nrows) / double(std::max<int64_t>(nr, 1));
     std::mutex work_mu;
     std::array<double, kNCaps> work_at{};
+    // The cap model needs only totals: past 8k haps it prices every stride-th
+    // hap (weighted by the stride), which is all the cap choice can resolve.
+    const int64_t cap_stride = std::max<int64_t>(1, nh / 8192);
     parallel_for(nh, [&](int64_t lo, int64_t hi) {
-        int64_t lanes[kNCaps] = {}, w = 0;
-        double work[kNCaps] = {};
+        int64_t w = 0;
         int hm = 0;
+        const int32_t* __restrict hl = hlen;
+        uint8_t* __restrict hc = hcls;
         for (int64_t h = lo; h < hi; ++h) {
-            const int H = hlen[size_t(h)];
-            const int64_t m = loc.hap_mult(h);
+            const int H = hl[h];
             int cl;
             if (use_lane && (pol == 1 || H <= kLaneMaxH))
                 cl = H > seg_max_h ? 1 : 0;
             else
                 cl = H > kW64Threshold ? 3 : 2;
-            hcls[size_t(h)] = uint8_t(cl);
-            if (cl == 0)
-                for (int q = 0; q < kNCaps; ++q) {
-                    const int nbq = std::min(64, (H + kCaps[q] - 1) / kCaps[q]);
-                    const int bc = kWidthCeil[size_t(std::min(kSegMaxBC, (H + nbq - 1) / nbq))];
-                    const int nb = (H + bc - 1) / bc;
-                    lanes[q] += m * nb;
-                    work[q] += double(m) * nb * (ravg + nb - 1) * (13.0 * bc + 30.0);
-                }
+            hc[h] = uint8_t(cl);
             hm = std::max(hm, H);
-            w += H > 64 * 32 ? m : 0;
-        }
-        for (int q = 0; q < kNCaps; ++q) lanes_at[q] += lanes[q];
-        {
-            std::lock_guard<std::mutex> lk(work_mu);
-            for (int q = 0; q < kNCaps; ++q) work_at[size_t(q)] += work[q];
+            w += H > 64 * 32 ? loc.hap_mult(h) : 0;
         }
         wide_a += w;
         int cur = hmax_a.load();
         while (hm > cur && !hmax_a.compare_exchange_weak(cur, hm)) {
         }
     }, 1 << 14);
-    // Column-segmented waves (lane_kernel.hip run_seg): a pair gets nb lanes of
-    // BC columns, BC from the compiled widths, choosing between nb0 =
-    // ceil(H/cap) and nb0 + 1 lanes by modelled instructions (below). The
-    // width cap minimises the modelled pass time: the waves one SIMD runs
-    // (at least 2: a lone wave issues at half rate) times a wave's modelled
-    // instructions (R + nb - 1 steps of 13 per column + ~30). Large batches get the widest cap (least
-    // per-step overhead); a batch that gives each SIMD only a few waves gets
-    // the width that balances waves per SIMD against steps per wave (measured
-    // on MI355X: S1 10k x 101x150 best at 16, S1w 10k x 101x250 at 24).
+    parallel_for((nh + cap_stride - 1) / cap_stride, [&](int64_t lo, int64_t hi) {
+        int64_t lanes[kNCaps] = {};
+        double work[kNCaps] = {};
+        for (int64_t i = lo; i < hi; ++i) {
+            const int64_t h = i * cap_stride;
+            if (hcls[size_t(h)] != 0) continue;
+            const int H = hlen[size_t(h)];
+            const int64_t m = cap_stride * loc.hap_mult(h);
+            for (int q = 0; q < kNCaps; ++q) {
+                const int nbq = std::min(64, (H + kCaps[q] - 1) / kCaps[q]);
+                const int bc = kWidthCeil[size_t(std::min(kSegMaxBC, (H + nbq - 1) / nbq))];
+                const int nb = (H + bc - 1) / bc;
+                lanes[q] += m * nb;
+                work[q] += double(m) * nb * (ravg + nb - 1) * (13.0 * bc + 30.0);
+            }
+        }
+        for (int q = 0; q < kNCaps; ++q) lanes_at[q] += lanes[q];
+        std::lock_guard<std::mutex> lk(work_mu);
+        for (int q = 0; q < kNCaps; ++q) work_at[size_t(q)] += work[q];
+    }, 4096);
+    tm.mark("hap classes: cost");
     int cap = kSegMaxBC;
     bool few_waves = false;   // the pass gives each SIMD at most ~3 waves: latency-bound, prefer more lanes
     {
@@ -1042,19 +1046,31 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const float* waste = few_waves ? kPerLane.data() : kHalfWaste.data();
     grow(S.hcand, size_t(nh));
     Cand* hcand = reinterpret_cast<Cand*>(S.hcand.data());
+    auto cand_of = [&](int H) {
+        const int nb0 = std::min(64, (H + cap - 1) / cap);
+        Cand c{};
+        for (int q = 0; q < 2; ++q) {
+            const int nb = std::min(nb0 + q, 64);
+            const int bc = kWidthCeil[size_t(std::min(kSegMaxBC, (H + nb - 1) / nb))];
+            c.bc[q] = uint8_t(bc);
+            c.nb[q] = uint8_t((H + bc - 1) / bc);
+        }
+        return c;
+    };
+    // Many haps (flat batches: one per pair): the candidates by H from a table
+    // (divisions once per length, not per hap).
+    const int hmax_seg = std::min(hmax_a.load(), seg_max_h);
+    std::vector<Cand>& ctab = S.ctab;
+    const bool by_table = nh > 4 * int64_t(hmax_seg + 1);
+    if (by_table) {
+        ctab.resize(size_t(hmax_seg) + 1);
+        for (int H = 1; H <= hmax_seg; ++H) ctab[size_t(H)] = cand_of(H);
+    }
     parallel_for(nh, [&](int64_t lo, int64_t hi) {
         for (int64_t h = lo; h < hi; ++h) {
             if (hcls[size_t(h)] != 0) continue;
             const int H = hlen[size_t(h)];
-            const int nb0 = std::min(64, (H + cap - 1) / cap);
-            Cand c{};
-            for (int q = 0; q < 2; ++q) {
-                const int nb = std::min(nb0 + q, 64);
-                const int bc = kWidthCeil[size_t(std::min(kSegMaxBC, (H + nb - 1) / nb))];
-                c.bc[q] = uint8_t(bc);
-                c.nb[q] = uint8_t((H + bc - 1) / bc);
-            }
-            hcand[size_t(h)] = c;
+            hcand[size_t(h)] = by_table ? ctab[size_t(H)] : cand_of(H);
         }
     }, 1 << 14);
     tm.mark("hap classes");
