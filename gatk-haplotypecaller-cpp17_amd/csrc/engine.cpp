@@ -713,7 +713,7 @@ inline float seg_cost(int nb, int bc, int R, const float* waste)
 // returns the batch's cells.
 int64_t plan_grid(const Local& loc, const int32_t* rlen, const int32_t* hlen, const int64_t* row_off,
                   const int64_t* hap_w, const Cand* hcand, const float* waste, int qforce, PairDesc* pd,
-                  std::vector<int>& seg_ord, std::vector<LaneWave>& lw, PhaseTimer& tm)
+                  bool write_pairs, std::vector<int>& seg_ord, std::vector<LaneWave>& lw, PhaseTimer& tm)
 {
     const PartSpec& spec = *loc.spec;
     const size_t nblk = spec.blocks.size();
@@ -802,6 +802,17 @@ int64_t plan_grid(const Local& loc, const int32_t* rlen, const int32_t* hlen, co
         }
     }, 1);
     tm.mark("grid: slots + waves");
+    if (!write_pairs) {   // descriptors built on the device (launch_grid_pairs): cells from block sums
+        int64_t cells = 0;
+        for (size_t b = 0; b < nblk; ++b) {
+            const Block& B = spec.blocks[b];
+            int64_t sr = 0, sh = 0;
+            for (int r = 0; r < B.nr; ++r) sr += rlen[loc.blk_r[b] + r];
+            for (int h = 0; h < B.nh; ++h) sh += hlen[loc.blk_h[b] + h];
+            cells += sr * sh;
+        }
+        return cells;
+    }
     // Pair descriptors (read-major within each block, as Local::pairs).
     std::atomic<int64_t> cells{0};
     parallel_for(loc.np, [&](int64_t lo, int64_t hi) {
@@ -895,7 +906,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
 
     // Pinned staging: upper bound for the waves (one per seg pair at most, plus
     // one-lane waves) and the results image after the upload.
-    const size_t waves_max = sizeof(LaneWave) * (size_t(npairs) + 1);
+    const size_t waves_max = sizeof(LaneWave) * (size_t(npairs) + 1) + sizeof(GridBlock) * spec.blocks.size() + 256;
     const size_t n1 = size_t(std::max<int64_t>(npairs, 1));
     const size_t res_o64 = (sizeof(float) * n1 + 255) & ~size_t(255);
     const size_t res_ofl = res_o64 + ((sizeof(double) * n1 + 255) & ~size_t(255));
@@ -1090,7 +1101,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         one_ord.clear();
         ord2[0].clear();
         ord2[1].clear();
-        cells_a = plan_grid(loc, rlen, hlen, row_off.data(), hap_w.data(), hcand, waste, qforce, pd, seg_ord, lw, tm);
+        cells_a = plan_grid(loc, rlen, hlen, row_off.data(), hap_w.data(), hcand, waste, qforce, pd, g_dry, seg_ord, lw, tm);
         tm.mark("grid: pairs");
     } else {
         // Per pair: descriptor straight into the staging image, class, and for
@@ -1376,7 +1387,20 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     std::memcpy(ordp + o_ord0, ord2[0].data(), sizeof(int) * ord2[0].size());
     std::memcpy(ordp + o_ord0 + ord2[0].size(), ord2[1].data(), sizeof(int) * ord2[1].size());
     std::memcpy(host + o_lw, lw.data(), sizeof(LaneWave) * lw.size());
-    const size_t upload = o_lw + sizeof(LaneWave) * lw.size();
+    size_t upload = o_lw + sizeof(LaneWave) * lw.size();
+    // Structured plans: the pair descriptors are built on the device from the
+    // read / hap descriptors (launch_grid_pairs), so the upload skips them and
+    // carries the block table instead.
+    const bool dev_pairs = grid && !g_dry;
+    const size_t up0 = dev_pairs ? o_rd : 0;
+    size_t o_gb = 0;
+    if (dev_pairs) {
+        o_gb = (upload + 15) & ~size_t(15);
+        GridBlock* gb = reinterpret_cast<GridBlock*>(host + o_gb);
+        for (size_t b = 0; b < spec.blocks.size(); ++b)
+            gb[b] = GridBlock{loc.blk_p[b], spec.blocks[b].nr, spec.blocks[b].nh, int(loc.blk_r[b]), int(loc.blk_h[b])};
+        upload = o_gb + sizeof(GridBlock) * spec.blocks.size();
+    }
     int4* rdesc = reinterpret_cast<int4*>(host + o_rd);
     uint8_t* hb = reinterpret_cast<uint8_t*>(host + o_bases);
     uint8_t* hq = reinterpret_cast<uint8_t*>(host + o_quals);
@@ -1468,7 +1492,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     b->n_seg_waves = n_seg_waves;
     b->lane_variant = lane_var;
     b->lane_waves = int(lw.size());
-    b->upload_bytes = upload;
+    b->upload_bytes = upload - up0;
     b->d_pairs = reinterpret_cast<PairDesc*>(dev + o_pairs);
     b->d_rows = reinterpret_cast<uint32_t*>(dev + o_rows) + kRowPadBefore;
     b->d_hapw = reinterpret_cast<uint32_t*>(dev + o_hapw);
@@ -1521,7 +1545,11 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     auto enqueue = [&]() -> int {
         if (!b->slot_ev)
             for (auto& e : b->pack_ev) HIP_TRY(hipEventCreate(&e));
-        HIP_TRY(hipMemcpyAsync(dev, host, upload, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(dev + up0, host + up0, upload - up0, hipMemcpyHostToDevice, s));
+        if (dev_pairs)
+            HIP_TRY(launch_grid_pairs(reinterpret_cast<const GridBlock*>(dev + o_gb), int(spec.blocks.size()),
+                                      (long long)npairs, reinterpret_cast<const int4*>(dev + o_rd),
+                                      reinterpret_cast<const int4*>(dev + o_hd), b->d_pairs, s));
         HIP_TRY(hipMemsetAsync(b->d_count, 0, 4 * sizeof(int), s));
         HIP_TRY(hipEventRecord(b->pack_ev[0], s));
         HIP_TRY(launch_pack_reads(reinterpret_cast<const uint8_t*>(dev + o_bases),

@@ -159,5 +159,16 @@ hipError_t configure_kernels();   // raise the dynamic-LDS limit once
 hipError_t launch_pack_reads(const uint8_t* bases, const uint8_t* quals, const uint8_t* gaps, long long gap_stride,
                              const int4* rdesc, int nreads, uint32_t* rows, hipStream_t s);
 hipError_t launch_hap_tables(const uint8_t* hap_bytes, const int4* haps, int nhaps, uint32_t* hapw, hipStream_t s);
+// Pair descriptors of a structured (cross-product) plan, built on the device
+// instead of uploaded: block b's pairs [p0, p0 + nr * nh) are its reads
+// [r0, r0 + nr) x haps [h0, h0 + nh) (part-local ids), read-major; blocks in
+// ascending p0. pairs[k] = {rows offset, R, table offset, H} from the read and
+// hap descriptors (rdesc .x/.y, hdesc .z/.y).
+struct GridBlock {
+    long long p0;
+    int nr, nh, r0, h0;
+};
+hipError_t launch_grid_pairs(const GridBlock* blocks, int nblocks, long long npairs, const int4* rdesc,
+                             const int4* hdesc, PairDesc* pairs, hipStream_t s);
 
 }  // namespace hcphmm

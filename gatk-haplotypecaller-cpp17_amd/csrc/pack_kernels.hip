@@ -90,6 +90,25 @@ __global__ __launch_bounds__(256) void hap_tables_kernel(const uint8_t* __restri
     }
 }
 
+__global__ __launch_bounds__(256) void grid_pairs_kernel(const GridBlock* __restrict__ blocks, int nblocks,
+                                                         long long npairs, const int4* __restrict__ rdesc,
+                                                         const int4* __restrict__ hdesc, PairDesc* __restrict__ pairs)
+{
+    for (long long k = blockIdx.x * 256ll + threadIdx.x; k < npairs; k += 256ll * gridDim.x) {
+        int lo = 0, hi = nblocks;   // the last block with p0 <= k (empty blocks share their successor's p0)
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (blocks[mid].p0 <= k) lo = mid;
+            else hi = mid;
+        }
+        const GridBlock b = blocks[lo];
+        const long long off = k - b.p0;
+        const int r = b.r0 + int(off / b.nh), h = b.h0 + int(off % b.nh);
+        const int4 rd = rdesc[r], hd = hdesc[h];
+        pairs[k] = make_int4(rd.x, rd.y, hd.z, hd.y);
+    }
+}
+
 int grid_for(long long waves)
 {
     const long long blocks = (waves + 3) / 4;
@@ -111,6 +130,16 @@ hipError_t launch_hap_tables(const uint8_t* hap_bytes, const int4* haps, int nha
 {
     if (nhaps <= 0) return hipSuccess;
     hipLaunchKernelGGL(hap_tables_kernel, dim3(grid_for(nhaps)), dim3(256), 0, s, hap_bytes, haps, nhaps, hapw);
+    return hipGetLastError();
+}
+
+hipError_t launch_grid_pairs(const GridBlock* blocks, int nblocks, long long npairs, const int4* rdesc,
+                             const int4* hdesc, PairDesc* pairs, hipStream_t s)
+{
+    if (npairs <= 0 || nblocks <= 0) return hipSuccess;
+    const long long g = (npairs + 255) / 256;
+    hipLaunchKernelGGL(grid_pairs_kernel, dim3(unsigned(g < 8192 ? g : 8192)), dim3(256), 0, s, blocks, nblocks, npairs,
+                       rdesc, hdesc, pairs);
     return hipGetLastError();
 }
 
