@@ -29,6 +29,14 @@ import statistics
 import sys
 import time
 
+# The CPU baseline runs the reference's OpenMP kernel in this process; with the
+# default wait policy its 16 threads keep spinning after each parallel region
+# and take the host cores from the engine's planner threads in the host-path
+# timings that follow (415 x 128 region 1.16 -> 1.23 ms, S2 end-to-end 1.55 ->
+# 1.1-1.4 TCUPS). Passive waiting leaves the baseline itself unchanged (31.3
+# GCUPS either way).
+os.environ.setdefault("OMP_WAIT_POLICY", "passive")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "gatk-haplotypecaller-cpp17_amd")
 sys.path.insert(0, PKG)
