@@ -667,6 +667,13 @@ struct Cand {
 };
 static_assert(sizeof(Cand) == sizeof(uint32_t), "Cand packs into a word");
 
+// A structured plan's segment tables for the device (launch_grid_waves).
+struct GridDev {
+    std::vector<GridSeg> segs;
+    std::vector<int> rord, hord;
+    int64_t slots = 0, waves = 0;
+};
+
 // Grow-only per-thread scratch of the planner: fresh large vectors would be
 // fresh mmap'd pages, zero-filled by the kernel on first touch, every call.
 struct PlanScratch {
@@ -676,6 +683,7 @@ struct PlanScratch {
     std::vector<uint32_t> srec;   // (BC, nb, R) of the segmented pairs in sorted order
     std::vector<uint32_t> hcand, key;
     std::vector<Cand> ctab;
+    GridDev gdev;
     std::vector<int> seg_in, one_ord, ord2[2], seg_ord, sort_tmp;
     std::vector<LaneWave> lw, ordered;
     std::vector<int64_t> wcost;
@@ -713,7 +721,8 @@ inline float seg_cost(int nb, int bc, int R, const float* waste)
 // returns the batch's cells.
 int64_t plan_grid(const Local& loc, const int32_t* rlen, const int32_t* hlen, const int64_t* row_off,
                   const int64_t* hap_w, const Cand* hcand, const float* waste, int qforce, PairDesc* pd,
-                  bool write_pairs, std::vector<int>& seg_ord, std::vector<LaneWave>& lw, PhaseTimer& tm)
+                  bool write_pairs, std::vector<int>& seg_ord, std::vector<LaneWave>& lw, PhaseTimer& tm,
+                  GridDev* gd)
 {
     const PartSpec& spec = *loc.spec;
     const size_t nblk = spec.blocks.size();
@@ -772,6 +781,22 @@ int64_t plan_grid(const Local& loc, const int32_t* rlen, const int32_t* hlen, co
         slots += g.n;
         waves += (g.n + 64 / int(g.key & 0xff) - 1) / (64 / int(g.key & 0xff));
     }
+    if (gd) {   // order and waves built on the device from the segments (launch_grid_waves)
+        gd->slots = slots;
+        gd->waves = waves;
+        gd->segs.resize(segs.size());
+        for (size_t k = 0; k < segs.size(); ++k) {
+            const Seg& g = segs[k];
+            const Block& B = spec.blocks[size_t(g.blk)];
+            gd->segs[k] = GridSeg{g.slot0, loc.blk_p[size_t(g.blk)], int(g.w0), int(loc.blk_r[size_t(g.blk)]), B.nr,
+                                  B.nh, int(loc.blk_h[size_t(g.blk)]), g.g0, g.G, int(g.key >> 8),
+                                  int(g.key & 0xff), 0};
+        }
+        gd->rord.swap(rord);
+        gd->hord.swap(hord);
+        seg_ord.clear();
+        lw.clear();
+    } else {
     seg_ord.resize(size_t(slots));
     lw.resize(size_t(waves));
     parallel_for(int64_t(segs.size()), [&](int64_t lo, int64_t hi) {
@@ -801,6 +826,7 @@ int64_t plan_grid(const Local& loc, const int32_t* rlen, const int32_t* hlen, co
             }
         }
     }, 1);
+    }   // host order and waves
     tm.mark("grid: slots + waves");
     if (!write_pairs) {   // descriptors built on the device (launch_grid_pairs): cells from block sums
         int64_t cells = 0;
@@ -906,7 +932,8 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
 
     // Pinned staging: upper bound for the waves (one per seg pair at most, plus
     // one-lane waves) and the results image after the upload.
-    const size_t waves_max = sizeof(LaneWave) * (size_t(npairs) + 1) + sizeof(GridBlock) * spec.blocks.size() + 256;
+    const size_t waves_max = sizeof(LaneWave) * (size_t(npairs) + 1) + sizeof(GridBlock) * spec.blocks.size() +
+                             sizeof(GridSeg) * size_t(nh) + sizeof(int) * size_t(nr + nh) + 1024;
     const size_t n1 = size_t(std::max<int64_t>(npairs, 1));
     const size_t res_o64 = (sizeof(float) * n1 + 255) & ~size_t(255);
     const size_t res_ofl = res_o64 + ((sizeof(double) * n1 + 255) & ~size_t(255));
@@ -1097,11 +1124,16 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     // general one (A/B, tests).
     bool grid = !spec.flat && env_i64("HC_PHMM_GRID_PLAN", 1) != 0;
     for (int64_t h = 0; grid && h < nh; ++h) grid = hcls[size_t(h)] == 0;
+    // Structured plans outside dry runs: pair descriptors, slot order and waves
+    // are built on the device from the block and segment tables.
+    const bool dev_plan = grid && !g_dry;
+    GridDev& gd = S.gdev;
     if (grid) {
         one_ord.clear();
         ord2[0].clear();
         ord2[1].clear();
-        cells_a = plan_grid(loc, rlen, hlen, row_off.data(), hap_w.data(), hcand, waste, qforce, pd, g_dry, seg_ord, lw, tm);
+        cells_a = plan_grid(loc, rlen, hlen, row_off.data(), hap_w.data(), hcand, waste, qforce, pd, !dev_plan, seg_ord, lw, tm,
+                            dev_plan ? &gd : nullptr);
         tm.mark("grid: pairs");
     } else {
         // Per pair: descriptor straight into the staging image, class, and for
@@ -1340,8 +1372,8 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         }
     }
     tm.mark("seg pack");
-    const int n_seg_waves = int(lw.size());
-    const int n_seg_slots = int(seg_ord.size());
+    const int n_seg_waves = dev_plan ? int(gd.waves) : int(lw.size());
+    const int n_seg_slots = dev_plan ? int(gd.slots) : int(seg_ord.size());
     // One lane per pair with the carry buffer (haps longer than the segmented
     // kernel's reach, or policy "off"): binned by (H rounded up to 16, R).
     const int lane_var = lane_variant_id();
@@ -1382,24 +1414,31 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     // Staging fill: order, wave list, read descriptors + bytes, hap bytes.
     int* ordp = reinterpret_cast<int*>(host + o_ord);
     std::memcpy(ordp, seg_ord.data(), sizeof(int) * seg_ord.size());
-    std::memcpy(ordp + seg_ord.size(), one_ord.data(), sizeof(int) * one_ord.size());
-    const size_t o_ord0 = seg_ord.size() + one_ord.size();
+    std::memcpy(ordp + n_seg_slots, one_ord.data(), sizeof(int) * one_ord.size());
+    const size_t o_ord0 = size_t(n_seg_slots) + one_ord.size();
     std::memcpy(ordp + o_ord0, ord2[0].data(), sizeof(int) * ord2[0].size());
     std::memcpy(ordp + o_ord0 + ord2[0].size(), ord2[1].data(), sizeof(int) * ord2[1].size());
     std::memcpy(host + o_lw, lw.data(), sizeof(LaneWave) * lw.size());
-    size_t upload = o_lw + sizeof(LaneWave) * lw.size();
-    // Structured plans: the pair descriptors are built on the device from the
-    // read / hap descriptors (launch_grid_pairs), so the upload skips them and
-    // carries the block table instead.
-    const bool dev_pairs = grid && !g_dry;
+    size_t upload = o_lw + sizeof(LaneWave) * (dev_plan ? size_t(n_seg_waves) : lw.size());
+    // Structured plans: the pair descriptors, the slot order and the waves are
+    // built on the device (launch_grid_pairs, launch_grid_waves), so the upload
+    // skips them and carries the block and segment tables instead.
+    const bool dev_pairs = dev_plan;
     const size_t up0 = dev_pairs ? o_rd : 0;
-    size_t o_gb = 0;
+    const size_t up_mid = dev_plan ? o_ord : upload;   // [up0, up_mid) and [o_gb, upload) travel
+    size_t o_gb = 0, o_gs = 0, o_gr = 0, o_gh = 0;
     if (dev_pairs) {
         o_gb = (upload + 15) & ~size_t(15);
         GridBlock* gb = reinterpret_cast<GridBlock*>(host + o_gb);
         for (size_t b = 0; b < spec.blocks.size(); ++b)
             gb[b] = GridBlock{loc.blk_p[b], spec.blocks[b].nr, spec.blocks[b].nh, int(loc.blk_r[b]), int(loc.blk_h[b])};
-        upload = o_gb + sizeof(GridBlock) * spec.blocks.size();
+        o_gs = (o_gb + sizeof(GridBlock) * spec.blocks.size() + 15) & ~size_t(15);
+        std::memcpy(host + o_gs, gd.segs.data(), sizeof(GridSeg) * gd.segs.size());
+        o_gr = (o_gs + sizeof(GridSeg) * gd.segs.size() + 15) & ~size_t(15);
+        std::memcpy(host + o_gr, gd.rord.data(), sizeof(int) * gd.rord.size());
+        o_gh = (o_gr + sizeof(int) * gd.rord.size() + 15) & ~size_t(15);
+        std::memcpy(host + o_gh, gd.hord.data(), sizeof(int) * gd.hord.size());
+        upload = o_gh + sizeof(int) * gd.hord.size();
     }
     int4* rdesc = reinterpret_cast<int4*>(host + o_rd);
     uint8_t* hb = reinterpret_cast<uint8_t*>(host + o_bases);
@@ -1488,11 +1527,11 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     b->n = npairs;
     b->cells = cells_a.load();
     b->Hmax = Hmax;
-    b->n_lane = int(seg_ord.size() + one_ord.size());
+    b->n_lane = int(size_t(n_seg_slots) + one_ord.size());
     b->n_seg_waves = n_seg_waves;
     b->lane_variant = lane_var;
-    b->lane_waves = int(lw.size());
-    b->upload_bytes = upload - up0;
+    b->lane_waves = dev_plan ? n_seg_waves : int(lw.size());
+    b->upload_bytes = dev_pairs ? (up_mid - up0) + (o_lw - o_bases) + (upload - o_gb) : upload - up0;
     b->d_pairs = reinterpret_cast<PairDesc*>(dev + o_pairs);
     b->d_rows = reinterpret_cast<uint32_t*>(dev + o_rows) + kRowPadBefore;
     b->d_hapw = reinterpret_cast<uint32_t*>(dev + o_hapw);
@@ -1545,11 +1584,23 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     auto enqueue = [&]() -> int {
         if (!b->slot_ev)
             for (auto& e : b->pack_ev) HIP_TRY(hipEventCreate(&e));
-        HIP_TRY(hipMemcpyAsync(dev + up0, host + up0, upload - up0, hipMemcpyHostToDevice, s));
-        if (dev_pairs)
+        if (dev_pairs) {
+            // [o_rd, o_ord): read / hap descriptors; the order and waves between
+            // are built on the device; then the block and segment tables, bytes.
+            HIP_TRY(hipMemcpyAsync(dev + up0, host + up0, up_mid - up0, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemcpyAsync(dev + o_bases, host + o_bases, o_lw - o_bases, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemcpyAsync(dev + o_gb, host + o_gb, upload - o_gb, hipMemcpyHostToDevice, s));
             HIP_TRY(launch_grid_pairs(reinterpret_cast<const GridBlock*>(dev + o_gb), int(spec.blocks.size()),
                                       (long long)npairs, reinterpret_cast<const int4*>(dev + o_rd),
                                       reinterpret_cast<const int4*>(dev + o_hd), b->d_pairs, s));
+            HIP_TRY(launch_grid_waves(reinterpret_cast<const GridSeg*>(dev + o_gs), int(gd.segs.size()),
+                                      (long long)n_seg_slots, n_seg_waves, reinterpret_cast<const int*>(dev + o_gr),
+                                      reinterpret_cast<const int*>(dev + o_gh),
+                                      reinterpret_cast<const int4*>(dev + o_rd), reinterpret_cast<int*>(dev + o_ord),
+                                      reinterpret_cast<LaneWave*>(dev + o_lw), s));
+        } else {
+            HIP_TRY(hipMemcpyAsync(dev + up0, host + up0, upload - up0, hipMemcpyHostToDevice, s));
+        }
         HIP_TRY(hipMemsetAsync(b->d_count, 0, 4 * sizeof(int), s));
         HIP_TRY(hipEventRecord(b->pack_ev[0], s));
         HIP_TRY(launch_pack_reads(reinterpret_cast<const uint8_t*>(dev + o_bases),

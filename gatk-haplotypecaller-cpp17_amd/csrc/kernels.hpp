@@ -170,5 +170,16 @@ struct GridBlock {
 };
 hipError_t launch_grid_pairs(const GridBlock* blocks, int nblocks, long long npairs, const int4* rdesc,
                              const int4* hdesc, PairDesc* pairs, hipStream_t s);
+// Slot order and segmented waves of a structured plan, built on the device
+// from its segments (engine.cpp plan_grid): segment g holds the pairs of block
+// reads rord[r0 .. r0 + nr) (by R descending) x haps hord[g0 .. g0 + G),
+// read-major, in slots [slot0, slot0 + nr * G) and waves [w0, ...) of
+// floor(64 / nb) pairs at block width bc. Segments in ascending slot0 / w0.
+struct GridSeg {
+    long long slot0, p0;   // first slot; the block's first pair
+    int w0, r0, nr, nh, h0, g0, G, bc, nb, pad;
+};
+hipError_t launch_grid_waves(const GridSeg* segs, int nsegs, long long nslots, int nwaves, const int* rord,
+                             const int* hord, const int4* rdesc, int* order, LaneWave* waves, hipStream_t s);
 
 }  // namespace hcphmm

@@ -109,6 +109,49 @@ __global__ __launch_bounds__(256) void grid_pairs_kernel(const GridBlock* __rest
     }
 }
 
+__global__ __launch_bounds__(256) void grid_waves_kernel(const GridSeg* __restrict__ segs, int nsegs,
+                                                         long long nslots, int nwaves, const int* __restrict__ rord,
+                                                         const int* __restrict__ hord, const int4* __restrict__ rdesc,
+                                                         int* __restrict__ order, LaneWave* __restrict__ waves)
+{
+    const long long stride = 256ll * gridDim.x;
+    for (long long t = blockIdx.x * 256ll + threadIdx.x; t < nslots; t += stride) {
+        int lo = 0, hi = nsegs;   // the last segment with slot0 <= t
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (segs[mid].slot0 <= t) lo = mid;
+            else hi = mid;
+        }
+        const GridSeg g = segs[lo];
+        const long long i = t - g.slot0;
+        const int rr = int(i / g.G), hh = int(i % g.G);
+        order[t] = int(g.p0 + (long long)(rord[g.r0 + rr] - g.r0) * g.nh + (hord[g.g0 + hh] - g.h0));
+    }
+    for (long long w = blockIdx.x * 256ll + threadIdx.x; w < nwaves; w += stride) {
+        int lo = 0, hi = nsegs;   // the last segment with w0 <= w (segments without waves share w0)
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (segs[mid].w0 <= w) lo = mid;
+            else hi = mid;
+        }
+        const GridSeg g = segs[lo];
+        const int per = 64 / g.nb;
+        const long long n = (long long)g.nr * g.G, a = (w - g.w0) * (long long)per;
+        const long long e = a + per < n ? a + per : n;
+        const int rmax = rdesc[rord[g.r0 + int(a / g.G)]].y;
+        const int rmin = rdesc[rord[g.r0 + int((e - 1) / g.G)]].y;
+        LaneWave v;
+        v.slot0 = int(g.slot0 + a);
+        v.rmax = rmax;
+        v.rmin = rmin;
+        v.ncols = g.bc;
+        v.npairs = int(e - a);
+        v.nsteps = rmax + g.nb - 1;
+        v.carry_row = 0;
+        waves[w] = v;
+    }
+}
+
 int grid_for(long long waves)
 {
     const long long blocks = (waves + 3) / 4;
@@ -140,6 +183,16 @@ hipError_t launch_grid_pairs(const GridBlock* blocks, int nblocks, long long npa
     const long long g = (npairs + 255) / 256;
     hipLaunchKernelGGL(grid_pairs_kernel, dim3(unsigned(g < 8192 ? g : 8192)), dim3(256), 0, s, blocks, nblocks, npairs,
                        rdesc, hdesc, pairs);
+    return hipGetLastError();
+}
+
+hipError_t launch_grid_waves(const GridSeg* segs, int nsegs, long long nslots, int nwaves, const int* rord,
+                             const int* hord, const int4* rdesc, int* order, LaneWave* waves, hipStream_t s)
+{
+    if (nsegs <= 0 || (nslots <= 0 && nwaves <= 0)) return hipSuccess;
+    const long long g = (nslots + 255) / 256;
+    hipLaunchKernelGGL(grid_waves_kernel, dim3(unsigned(g < 4096 ? (g > 0 ? g : 1) : 4096)), dim3(256), 0, s, segs,
+                       nsegs, nslots, nwaves, rord, hord, rdesc, order, waves);
     return hipGetLastError();
 }
 
