@@ -37,7 +37,9 @@
  *
  * Every pointer is borrowed for the duration of the call (for hc_phmm_submit_*:
  * inputs until submit returns, outputs until hc_phmm_collect returns); nothing
- * else is retained. Calls are thread-safe. All entry points return 0 on success
+ * else is retained. Calls are thread-safe, except that one hc_phmm_batch or
+ * hc_phmm_job handle must not be used by two threads at once (different
+ * handles may be used concurrently). All entry points return 0 on success
  * or a negative HC_PHMM_E* code; the message of the calling thread's last
  * error is available from hc_phmm_last_error(). There is no CPU fallback:
  * without a usable MI355X the calls fail with HC_PHMM_ENODEV.
