@@ -1586,30 +1586,51 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             for (auto& e : b->pack_ev) HIP_TRY(hipEventCreate(&e));
         if (dev_pairs) {
             // [o_rd, o_ord): read / hap descriptors; the order and waves between
-            // are built on the device; then the block and segment tables, bytes.
+            // are built on the device; then the read / hap bytes and the block
+            // and segment tables. One fused launch prepares everything.
             HIP_TRY(hipMemcpyAsync(dev + up0, host + up0, up_mid - up0, hipMemcpyHostToDevice, s));
             HIP_TRY(hipMemcpyAsync(dev + o_bases, host + o_bases, o_lw - o_bases, hipMemcpyHostToDevice, s));
             HIP_TRY(hipMemcpyAsync(dev + o_gb, host + o_gb, upload - o_gb, hipMemcpyHostToDevice, s));
-            HIP_TRY(launch_grid_pairs(reinterpret_cast<const GridBlock*>(dev + o_gb), int(spec.blocks.size()),
-                                      (long long)npairs, reinterpret_cast<const int4*>(dev + o_rd),
-                                      reinterpret_cast<const int4*>(dev + o_hd), b->d_pairs, s));
-            HIP_TRY(launch_grid_waves(reinterpret_cast<const GridSeg*>(dev + o_gs), int(gd.segs.size()),
-                                      (long long)n_seg_slots, n_seg_waves, reinterpret_cast<const int*>(dev + o_gr),
-                                      reinterpret_cast<const int*>(dev + o_gh),
-                                      reinterpret_cast<const int4*>(dev + o_rd), reinterpret_cast<int*>(dev + o_ord),
-                                      reinterpret_cast<LaneWave*>(dev + o_lw), s));
+            HIP_TRY(hipEventRecord(b->pack_ev[0], s));
+            GridPrepArgs g{};
+            g.bases = reinterpret_cast<const uint8_t*>(dev + o_bases);
+            g.quals = reinterpret_cast<const uint8_t*>(dev + o_quals);
+            g.gaps = reinterpret_cast<const uint8_t*>(dev + o_gaps);
+            g.gap_stride = (long long)gap_stride;
+            g.rdesc = reinterpret_cast<const int4*>(dev + o_rd);
+            g.nreads = int(nr);
+            g.rows = b->d_rows;
+            g.hap_bytes = reinterpret_cast<const uint8_t*>(dev + o_hb);
+            g.hdesc = reinterpret_cast<const int4*>(dev + o_hd);
+            g.nhaps = int(nh);
+            g.hapw = b->d_hapw;
+            g.blocks = reinterpret_cast<const GridBlock*>(dev + o_gb);
+            g.nblocks = int(spec.blocks.size());
+            g.npairs = (long long)npairs;
+            g.pairs = b->d_pairs;
+            g.segs = reinterpret_cast<const GridSeg*>(dev + o_gs);
+            g.nsegs = int(gd.segs.size());
+            g.nslots = (long long)n_seg_slots;
+            g.nwaves = n_seg_waves;
+            g.rord = reinterpret_cast<const int*>(dev + o_gr);
+            g.hord = reinterpret_cast<const int*>(dev + o_gh);
+            g.order = reinterpret_cast<int*>(dev + o_ord);
+            g.waves = reinterpret_cast<LaneWave*>(dev + o_lw);
+            g.counters = b->d_count;
+            HIP_TRY(launch_prepare_grid(g, s));
+            HIP_TRY(hipEventRecord(b->pack_ev[1], s));
         } else {
             HIP_TRY(hipMemcpyAsync(dev + up0, host + up0, upload - up0, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemsetAsync(b->d_count, 0, 4 * sizeof(int), s));
+            HIP_TRY(hipEventRecord(b->pack_ev[0], s));
+            HIP_TRY(launch_pack_reads(reinterpret_cast<const uint8_t*>(dev + o_bases),
+                                      reinterpret_cast<const uint8_t*>(dev + o_quals),
+                                      reinterpret_cast<const uint8_t*>(dev + o_gaps), (long long)gap_stride,
+                                      reinterpret_cast<const int4*>(dev + o_rd), int(nr), b->d_rows, s));
+            HIP_TRY(launch_hap_tables(reinterpret_cast<const uint8_t*>(dev + o_hb),
+                                      reinterpret_cast<const int4*>(dev + o_hd), int(nh), b->d_hapw, s));
+            HIP_TRY(hipEventRecord(b->pack_ev[1], s));
         }
-        HIP_TRY(hipMemsetAsync(b->d_count, 0, 4 * sizeof(int), s));
-        HIP_TRY(hipEventRecord(b->pack_ev[0], s));
-        HIP_TRY(launch_pack_reads(reinterpret_cast<const uint8_t*>(dev + o_bases),
-                                  reinterpret_cast<const uint8_t*>(dev + o_quals),
-                                  reinterpret_cast<const uint8_t*>(dev + o_gaps), (long long)gap_stride,
-                                  reinterpret_cast<const int4*>(dev + o_rd), int(nr), b->d_rows, s));
-        HIP_TRY(launch_hap_tables(reinterpret_cast<const uint8_t*>(dev + o_hb), reinterpret_cast<const int4*>(dev + o_hd),
-                                  int(nh), b->d_hapw, s));
-        HIP_TRY(hipEventRecord(b->pack_ev[1], s));
         if (with_run) {
             const int r = run_part(b, s);
             if (r) return r;

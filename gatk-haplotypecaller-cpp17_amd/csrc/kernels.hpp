@@ -181,5 +181,32 @@ struct GridSeg {
 };
 hipError_t launch_grid_waves(const GridSeg* segs, int nsegs, long long nslots, int nwaves, const int* rord,
                              const int* hord, const int4* rdesc, int* order, LaneWave* waves, hipStream_t s);
+// The run counters zeroed, launch_pack_reads, launch_hap_tables,
+// launch_grid_pairs and launch_grid_waves of one structured part, fused into
+// one launch.
+struct GridPrepArgs {
+    const uint8_t *bases, *quals, *gaps;
+    long long gap_stride;
+    const int4* rdesc;
+    int nreads;
+    uint32_t* rows;
+    const uint8_t* hap_bytes;
+    const int4* hdesc;
+    int nhaps;
+    uint32_t* hapw;
+    const GridBlock* blocks;
+    int nblocks;
+    long long npairs;
+    PairDesc* pairs;
+    const GridSeg* segs;
+    int nsegs;
+    long long nslots;
+    int nwaves;
+    const int *rord, *hord;
+    int* order;
+    LaneWave* waves;
+    int* counters;   // 4 ints zeroed (run-parity rescue counters)
+};
+hipError_t launch_prepare_grid(const GridPrepArgs& a, hipStream_t s);
 
 }  // namespace hcphmm

@@ -12,6 +12,8 @@
 //
 // Both are byte-streaming kernels, one wave per read / per haplotype (coalesced
 // byte loads across the wave; the match words come from wave ballots).
+#include <algorithm>
+
 #include "kernels.hpp"
 
 namespace hcphmm {
@@ -26,11 +28,9 @@ __device__ __forceinline__ uint32_t base_code(uint32_t b)
 // One wave per read (grid-stride over reads). rdesc: {row offset, length,
 // constant gap qualities i | d << 7 | c << 14 (already & 127) or -1 when they
 // vary, offset of the read's rows in the i/d/c planes when they vary}.
-__global__ __launch_bounds__(256) void pack_reads_kernel(const uint8_t* __restrict__ bases,
-                                                         const uint8_t* __restrict__ quals,
-                                                         const uint8_t* __restrict__ gaps, long long gap_stride,
-                                                         const int4* __restrict__ rdesc, int nreads,
-                                                         uint32_t* __restrict__ rows)
+__device__ __forceinline__ void pack_reads(const uint8_t* __restrict__ bases, const uint8_t* __restrict__ quals,
+                                           const uint8_t* __restrict__ gaps, long long gap_stride,
+                                           const int4* __restrict__ rdesc, int nreads, uint32_t* __restrict__ rows)
 {
     const int lane = threadIdx.x & 63;
     for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < nreads; r += gridDim.x * 4) {
@@ -58,9 +58,8 @@ __global__ __launch_bounds__(256) void pack_reads_kernel(const uint8_t* __restri
 // 32w+1 .. 32w+32; lanes 0-31 take the columns of row w, lanes 32-63 those of
 // row w+1, and the wave ballot of "hap base matches read code rc" gives both
 // rows' words for rc at once (bit-reversed: column 1 is the MSB).
-__global__ __launch_bounds__(256) void hap_tables_kernel(const uint8_t* __restrict__ hap_bytes,
-                                                         const int4* __restrict__ haps, int nhaps,
-                                                         uint32_t* __restrict__ hapw)
+__device__ __forceinline__ void hap_tables(const uint8_t* __restrict__ hap_bytes, const int4* __restrict__ haps,
+                                           int nhaps, uint32_t* __restrict__ hapw)
 {
     const int lane = threadIdx.x & 63;
     for (int h = blockIdx.x * 4 + (threadIdx.x >> 6); h < nhaps; h += gridDim.x * 4) {
@@ -90,9 +89,9 @@ __global__ __launch_bounds__(256) void hap_tables_kernel(const uint8_t* __restri
     }
 }
 
-__global__ __launch_bounds__(256) void grid_pairs_kernel(const GridBlock* __restrict__ blocks, int nblocks,
-                                                         long long npairs, const int4* __restrict__ rdesc,
-                                                         const int4* __restrict__ hdesc, PairDesc* __restrict__ pairs)
+__device__ __forceinline__ void grid_pairs(const GridBlock* __restrict__ blocks, int nblocks, long long npairs,
+                                           const int4* __restrict__ rdesc, const int4* __restrict__ hdesc,
+                                           PairDesc* __restrict__ pairs)
 {
     for (long long k = blockIdx.x * 256ll + threadIdx.x; k < npairs; k += 256ll * gridDim.x) {
         int lo = 0, hi = nblocks;   // the last block with p0 <= k (empty blocks share their successor's p0)
@@ -109,10 +108,10 @@ __global__ __launch_bounds__(256) void grid_pairs_kernel(const GridBlock* __rest
     }
 }
 
-__global__ __launch_bounds__(256) void grid_waves_kernel(const GridSeg* __restrict__ segs, int nsegs,
-                                                         long long nslots, int nwaves, const int* __restrict__ rord,
-                                                         const int* __restrict__ hord, const int4* __restrict__ rdesc,
-                                                         int* __restrict__ order, LaneWave* __restrict__ waves)
+__device__ __forceinline__ void grid_waves(const GridSeg* __restrict__ segs, int nsegs, long long nslots, int nwaves,
+                                           const int* __restrict__ rord, const int* __restrict__ hord,
+                                           const int4* __restrict__ rdesc, int* __restrict__ order,
+                                           LaneWave* __restrict__ waves)
 {
     const long long stride = 256ll * gridDim.x;
     for (long long t = blockIdx.x * 256ll + threadIdx.x; t < nslots; t += stride) {
@@ -150,6 +149,50 @@ __global__ __launch_bounds__(256) void grid_waves_kernel(const GridSeg* __restri
         v.carry_row = 0;
         waves[w] = v;
     }
+}
+
+__global__ __launch_bounds__(256) void grid_pairs_kernel(const GridBlock* __restrict__ blocks, int nblocks,
+                                                         long long npairs, const int4* __restrict__ rdesc,
+                                                         const int4* __restrict__ hdesc, PairDesc* __restrict__ pairs)
+{
+    grid_pairs(blocks, nblocks, npairs, rdesc, hdesc, pairs);
+}
+
+__global__ __launch_bounds__(256) void grid_waves_kernel(const GridSeg* __restrict__ segs, int nsegs,
+                                                         long long nslots, int nwaves, const int* __restrict__ rord,
+                                                         const int* __restrict__ hord, const int4* __restrict__ rdesc,
+                                                         int* __restrict__ order, LaneWave* __restrict__ waves)
+{
+    grid_waves(segs, nsegs, nslots, nwaves, rord, hord, rdesc, order, waves);
+}
+
+__global__ __launch_bounds__(256) void pack_reads_kernel(const uint8_t* __restrict__ bases,
+                                                         const uint8_t* __restrict__ quals,
+                                                         const uint8_t* __restrict__ gaps, long long gap_stride,
+                                                         const int4* __restrict__ rdesc, int nreads,
+                                                         uint32_t* __restrict__ rows)
+{
+    pack_reads(bases, quals, gaps, gap_stride, rdesc, nreads, rows);
+}
+
+__global__ __launch_bounds__(256) void hap_tables_kernel(const uint8_t* __restrict__ hap_bytes,
+                                                         const int4* __restrict__ haps, int nhaps,
+                                                         uint32_t* __restrict__ hapw)
+{
+    hap_tables(hap_bytes, haps, nhaps, hapw);
+}
+
+// Everything a structured (region) part needs before its pass, in one launch
+// (each step is a grid-stride loop over its own items; none reads another's
+// output): the run counters zeroed, reads packed, hap tables, pair
+// descriptors, slot order and waves — four fewer launches per region call.
+__global__ __launch_bounds__(256) void prepare_grid_kernel(GridPrepArgs a)
+{
+    if (blockIdx.x == 0 && threadIdx.x < 4) a.counters[threadIdx.x] = 0;
+    pack_reads(a.bases, a.quals, a.gaps, a.gap_stride, a.rdesc, a.nreads, a.rows);
+    hap_tables(a.hap_bytes, a.hdesc, a.nhaps, a.hapw);
+    grid_pairs(a.blocks, a.nblocks, a.npairs, a.rdesc, a.hdesc, a.pairs);
+    grid_waves(a.segs, a.nsegs, a.nslots, a.nwaves, a.rord, a.hord, a.rdesc, a.order, a.waves);
 }
 
 int grid_for(long long waves)
@@ -193,6 +236,14 @@ hipError_t launch_grid_waves(const GridSeg* segs, int nsegs, long long nslots, i
     const long long g = (nslots + 255) / 256;
     hipLaunchKernelGGL(grid_waves_kernel, dim3(unsigned(g < 4096 ? (g > 0 ? g : 1) : 4096)), dim3(256), 0, s, segs,
                        nsegs, nslots, nwaves, rord, hord, rdesc, order, waves);
+    return hipGetLastError();
+}
+
+hipError_t launch_prepare_grid(const GridPrepArgs& a, hipStream_t s)
+{
+    const long long items = std::max<long long>({(long long)a.nreads, (long long)a.nhaps, a.npairs / 64, a.nslots / 64, 1});
+    const int grid = grid_for(items);
+    hipLaunchKernelGGL(prepare_grid_kernel, dim3(grid), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
