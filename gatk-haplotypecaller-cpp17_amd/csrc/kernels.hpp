@@ -70,7 +70,8 @@ struct LaneArgs {
     const PairDesc* pairs;
     const int* order;
     int n_slots;
-    int n_waves;
+    int n_waves;              // waves launched (an upper bound when n_waves_dev is set)
+    const int* n_waves_dev;   // device-planned parts: the wave count on the device
     const LaneWave* waves;
     float2* carry;            // block-to-block column carry {T, Y} per row and lane
     const uint32_t* rows;

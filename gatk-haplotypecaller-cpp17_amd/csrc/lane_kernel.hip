@@ -187,7 +187,8 @@ __global__ __launch_bounds__(64 * HC_SEG_WPB, OCC) void phmm_seg_kernel(LaneArgs
     __shared__ float slut[kSlutLen];
     load_slut(slut, a.lut);
     const int wid = blockIdx.x * HC_SEG_WPB + (threadIdx.x >> 6);
-    if (wid >= a.n_waves) return;
+    const int n_waves = a.n_waves_dev ? __builtin_amdgcn_readfirstlane(*a.n_waves_dev) : a.n_waves;
+    if (wid >= n_waves) return;
     const int lane = threadIdx.x & 63;
     const unsigned long long t_start = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
     const LaneWave wv = load_wave(a.waves, wid);

@@ -8,6 +8,7 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <cstdint>
+#include <exception>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -26,6 +27,9 @@ public:
 
     // Run fn(t) for t in [0, ntasks) on the workers and the calling thread;
     // returns when all have finished. Safe to call from several threads at once.
+    // A task that throws (e.g. std::bad_alloc in a planner) does not unwind
+    // past the other tasks: every task still runs or is skipped, the batch
+    // drains, and the first exception is rethrown here, in the caller.
     void run(int ntasks, const std::function<void(int)>& fn)
     {
         if (ntasks <= 1 || workers_.empty()) {
@@ -48,6 +52,7 @@ public:
                 queue_.erase(queue_.begin() + long(k));
                 break;
             }
+        if (b.error) std::rethrow_exception(b.error);
     }
 
     ~WorkerPool()
@@ -65,6 +70,8 @@ private:
         const std::function<void(int)>* fn;
         int n;
         std::atomic<int> next{0};
+        std::atomic<bool> failed{false};
+        std::exception_ptr error;   // the first task exception, set once (failed)
         int finished = 0;   // tasks run, guarded by mu_
         int users = 0;      // workers inside drain(), guarded by mu_
         Batch(const std::function<void(int)>* f, int k) : fn(f), n(k) {}
@@ -84,7 +91,15 @@ private:
     static int drain(Batch& b)
     {
         int mine = 0;
-        for (int t; (t = b.next.fetch_add(1)) < b.n; ++mine) (*b.fn)(t);
+        for (int t; (t = b.next.fetch_add(1)) < b.n; ++mine) {
+            if (b.failed.load(std::memory_order_relaxed)) continue;   // skip the rest after a failure
+            try {
+                (*b.fn)(t);
+            } catch (...) {
+                bool expect = false;
+                if (b.failed.compare_exchange_strong(expect, true)) b.error = std::current_exception();
+            }
+        }
         return mine;
     }
 
@@ -139,6 +154,30 @@ void parallel_for(int64_t n, F&& f, int64_t grain = 4096)
     P.run(int(tasks), [&](int t) {
         const int64_t b = int64_t(t) * chunk, e = std::min(n, b + chunk);
         if (b < e) f(b, e);
+    });
+}
+
+// Parallel exclusive prefix sum of f(k), k in [0, n), into out[0..n].
+template <typename F>
+void prefix_sum(int64_t n, std::vector<int64_t>& out, F f)
+{
+    out.assign(size_t(n) + 1, 0);
+    if (n <= 0) return;
+    const int T = int(std::min<int64_t>(32, std::max<int64_t>(1, n / 16384)));
+    const int64_t chunk = (n + T - 1) / T;
+    std::vector<int64_t> part(static_cast<size_t>(T) + 1, 0);
+    WorkerPool::get().run(T, [&](int t) {
+        int64_t s = 0;
+        for (int64_t k = t * chunk, e = std::min(n, k + chunk); k < e; ++k) {
+            out[size_t(k) + 1] = s += f(k);
+        }
+        part[size_t(t) + 1] = s;
+    });
+    for (int t = 1; t <= T; ++t) part[size_t(t)] += part[size_t(t) - 1];
+    WorkerPool::get().run(T, [&](int t) {
+        const int64_t add = part[size_t(t)];
+        if (add)
+            for (int64_t k = t * chunk, e = std::min(n, k + chunk); k < e; ++k) out[size_t(k) + 1] += add;
     });
 }
 

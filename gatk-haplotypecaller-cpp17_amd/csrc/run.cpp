@@ -1,0 +1,212 @@
+// The device pass of a prepared part (computeLikelihoodsNative's per-pair
+// loop, intel_pairhmm.hpp:128-146, as kernels over the whole part): the fp32
+// kernels emit raw sums, rescue flags and the rescue list; the fp64 rescue
+// pass recomputes the flagged pairs; then the host log10 finish.
+#include <algorithm>
+#include <cmath>
+
+#include "engine_core.hpp"
+#include "luts.hpp"
+#include "pool.hpp"
+
+namespace hcphmm {
+namespace eng {
+
+int run_part(Part* b, hipStream_t s)
+{
+    Device& dv = *b->dev;
+    b->last_stream = s;
+    b->launch_waves = 0;
+    if (b->ev_used == b->ev_pool.size()) {
+        std::array<hipEvent_t, 3> t{};
+        for (auto& e : t) HIP_TRY(hipEventCreate(&e));
+        b->ev_pool.push_back(t);
+    }
+    const auto& ev = b->ev_pool[b->ev_used++];
+    for (int k = 0; k < 3; ++k) b->ev[k] = ev[k];
+    HIP_TRY(hipEventRecord(b->ev[0], s));
+    // No memsets: the fp32 kernels zero each pair's raw f64 slot as they emit,
+    // and the rescue planner zeroes the other parity's counter for the next run.
+    const int par = b->parity;
+    b->parity ^= 1;
+    int* count = b->d_count + par;
+    if (b->n_lane > 0) {
+        LaneArgs a{};
+        a.pairs = b->d_pairs;
+        a.order = b->d_lane_order;
+        a.n_slots = b->n_lane;
+        a.carry = b->d_carry;
+        a.rows = b->d_rows;
+        a.hapw = b->d_hapw;
+        a.lut = dv.lut_f;
+        a.raw_out = b->d_raw32;
+        a.rescue_flag = b->d_flag;
+        a.rescue_list = b->d_list;
+        a.rescue_count = count;
+        a.raw64_zero = b->d_raw64;
+        a.lut64 = dv.lut_d;
+        if (env_i64("HC_PHMM_RESCUE_IN_WAVE", 1) != 0) {
+            a.inker_count = b->d_count + 2 + par;
+            // A wave that rescues in place runs up to ~2.5x longer; a few such
+            // waves hide inside the pass, hundreds of them (a region whose reads
+            // miss some haps: ~440 rescues) drain late and cost more than the
+            // separate fp64 pass they would save (415 x 128 region: fp32
+            // 0.925 -> 0.80 ms at a cap of 32, S2's 19 rescues unchanged;
+            // profiles/r02_in_wave_rescue_cap.jsonl). Past the cap, the list.
+            a.inker_limit = int(std::max<int64_t>(0, env_i64("HC_PHMM_RESCUE_IN_WAVE_MAX", 32)));
+        }
+        b->inker_limit = a.inker_limit;
+        if (env_i64("HC_PHMM_TIMELINE", 0) != 0 && b->n_seg_waves > 0) {
+            // Diagnostics: this part's own record buffer (parts run concurrently
+            // on slot streams); hcx_timeline reads the last traced part.
+            if (b->timeline_n < b->n_seg_waves) {
+                if (b->timeline) {
+                    HIP_TRY(hipStreamSynchronize(s));
+                    HIP_TRY(hipFree(b->timeline));
+                    b->timeline = nullptr;
+                }
+                HIP_TRY(hipMalloc(&b->timeline, size_t(b->n_seg_waves) * 3 * sizeof(unsigned long long)));
+                b->timeline_n = b->n_seg_waves;
+            }
+            std::lock_guard<std::mutex> lk(g_tl.mu);
+            g_tl.part = b;
+            a.timeline = b->timeline;
+        }
+        b->launch_waves += b->lane_waves;
+        const int n_one = b->lane_waves - b->n_seg_waves;
+        const bool fork = b->n_seg_waves > 0 && n_one > 0;
+        if (b->n_seg_waves > 0) {
+            // Segmented waves; beside one-lane waves (long haps) they go on the
+            // side stream, launched first so they are dispatched first.
+            LaneArgs g = a;
+            g.waves = b->d_lane_waves;
+            g.n_waves = b->n_seg_waves;
+            g.n_waves_dev = b->d_nwaves;
+            if (fork) {
+                HIP_TRY(hipEventRecord(b->fork, s));
+                HIP_TRY(hipStreamWaitEvent(b->side, b->fork, 0));
+            }
+            HIP_TRY(launch_lane_seg_f32(g, fork ? b->side : s));
+            if (fork) HIP_TRY(hipEventRecord(b->join, b->side));
+        }
+        if (n_one > 0) {
+            a.waves = b->d_lane_waves + b->n_seg_waves;
+            a.n_waves = n_one;
+            HIP_TRY(launch_lane_f32(b->lane_variant, a, s));
+        }
+        if (fork) HIP_TRY(hipStreamWaitEvent(s, b->join, 0));
+    }
+    for (auto& c : b->cls) {
+        if (c.n == 0) continue;
+        DiagArgs a{};
+        a.pairs = b->d_pairs;
+        a.order = c.d_order;
+        a.n_slots = c.n;
+        a.rows = b->d_rows;
+        a.hapw = b->d_hapw;
+        a.lut = dv.lut_f;
+        a.ring_len = c.ring_len;
+        a.raw_out = b->d_raw32;
+        a.rescue_flag = b->d_flag;
+        a.rescue_list = b->d_list;
+        a.rescue_count = count;
+        a.raw64_zero = b->d_raw64;
+        const int G = 64 / c.W;
+        const int grid = (c.n + G - 1) / G;
+        b->launch_waves += grid;
+        HIP_TRY(launch_diag_f32(c.W, a, grid, s));
+    }
+    HIP_TRY(hipEventRecord(b->ev[1], s));
+    if (b->n > 0) {
+        // fp64 rescue (intel_pairhmm.hpp:137-139) over the device-built list, no
+        // host round trip for its length: device planning + column-segmented
+        // fp64 waves (grid-stride), then the anti-diagonal fp64 kernel for haps
+        // wider than 64 blocks of 32 (only launched if the batch has any).
+        Seg64Args r{};
+        r.pairs = b->d_pairs;
+        r.rows = b->d_rows;
+        r.hapw = b->d_hapw;
+        r.lut = dv.lut_d;
+        r.list = b->d_list;
+        r.count = count;
+        r.count_reset = b->d_count + (par ^ 1);
+        r.inker_reset = b->d_count + 2 + (par ^ 1);
+        r.sorted = b->d_sorted;
+        r.big = b->d_big;
+        r.big_count = b->d_big_count;
+        r.plan = b->d_plan;
+        r.raw_out = b->d_raw64;
+        r.min_lanes = int64_t(2) * 4 * dv.n_cu * 64;
+        const int grid = int(std::min<int64_t>((b->n + 3) / 4, int64_t(2) * dv.n_cu));
+        HIP_TRY(launch_rescue_seg64(r, grid, s));
+        if (b->n_wide > 0) {
+            DiagArgs a{};
+            a.pairs = b->d_pairs;
+            a.order = b->d_big;
+            a.n_slots_dev = b->d_big_count;
+            a.rows = b->d_rows;
+            a.hapw = b->d_hapw;
+            a.lut = dv.lut_d;
+            a.ring_len = b->Hmax + 2 * 64 + 16;
+            a.raw_out = b->d_raw64;
+            HIP_TRY(launch_diag_f64(64, a, int(std::min<int64_t>(b->n_wide, 2048)), s));
+        }
+    }
+    HIP_TRY(hipEventRecord(b->ev[2], s));
+    b->ran = true;
+    return HC_PHMM_OK;
+}
+
+int enqueue_results(Part* b, hipStream_t s)
+{
+    HIP_TRY(hipMemcpyAsync(b->host_res, b->own_raw32, b->res_bytes, hipMemcpyDeviceToHost, s));
+    if (!b->done) HIP_TRY(hipEventCreateWithFlags(&b->done, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(b->done, s));
+    return HC_PHMM_OK;
+}
+
+// log10 finish (intel_pairhmm.hpp:137-143, glibc log10 / log10f as in the
+// reference) of a part's results, scattered into the caller's outputs.
+void finish_part(const Part& P, const float* f, const double* d, const uint8_t* fl, const Outputs& o)
+{
+    const Luts& L = luts();
+    const float l10f = L.log10_init_f;
+    const double l10d = L.log10_init_d;
+    auto ll = [&](int64_t k) { return fl[k] ? std::log10(d[k]) - l10d : double(std::log10(f[k]) - l10f); };
+    if (P.spec.flat) {
+        const int64_t id0 = P.spec.lo;
+        parallel_for(P.n, [&](int64_t lo, int64_t hi) {
+            for (int64_t k = lo; k < hi; ++k) {
+                if (o.loglik) o.loglik[id0 + k] = ll(k);
+                if (o.raw32) o.raw32[id0 + k] = f[k];
+                if (o.raw64) o.raw64[id0 + k] = d[k];
+                if (o.resc) o.resc[id0 + k] = fl[k];
+            }
+        }, 1 << 13);
+        return;
+    }
+    // Blocks: pair k of block b is (r, h) = divmod(k - base, nh).
+    std::vector<int64_t> base(P.spec.blocks.size() + 1, 0);
+    for (size_t b = 0; b < P.spec.blocks.size(); ++b)
+        base[b + 1] = base[b] + int64_t(P.spec.blocks[b].nr) * P.spec.blocks[b].nh;
+    parallel_for(P.n, [&](int64_t lo, int64_t hi) {
+        size_t b = size_t(std::upper_bound(base.begin(), base.end(), lo) - base.begin()) - 1;
+        int64_t k = lo;
+        while (k < hi) {
+            const Block& B = P.spec.blocks[b];
+            const int64_t end = std::min(hi, base[b + 1]);
+            int64_t r = (k - base[b]) / B.nh, h = (k - base[b]) % B.nh;
+            for (; k < end; ++k) {
+                B.out[r * B.ostride + h] = ll(k);
+                if (++h == B.nh) {
+                    h = 0;
+                    ++r;
+                }
+            }
+            ++b;
+        }
+    }, 1 << 13);
+}
+
+}  // namespace eng
+}  // namespace hcphmm
