@@ -62,6 +62,11 @@ void release_device(Device* d)
         if (s->stream) (void)hipStreamDestroy(s->stream);
         delete s;
     }
+    for (int k = 0; k < kRingN; ++k) {
+        if (d->ring.ev[k]) (void)hipEventSynchronize(d->ring.ev[k]);
+        if (d->ring.ev[k]) (void)hipEventDestroy(d->ring.ev[k]);
+        if (d->ring.buf[k]) (void)hipHostFree(d->ring.buf[k]);
+    }
     if (d->lut_f) (void)hipFree(d->lut_f);
     if (d->lut_d) (void)hipFree(d->lut_d);
     if (d->fork) (void)hipEventDestroy(d->fork);
@@ -94,6 +99,11 @@ int init_device(Device& d)
     HIP_TRY(hipMalloc(&d.lut_d, sizeof(double) * kTableLen));
     HIP_TRY(hipMemcpy(d.lut_f, L.dev_f.data(), sizeof(float) * kTableLen, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(d.lut_d, L.dev_d.data(), sizeof(double) * kTableLen, hipMemcpyHostToDevice));
+    for (int k = 0; k < kRingN; ++k) {
+        if (hipHostMalloc(&d.ring.buf[k], kRingChunk, hipHostMallocPortable) != hipSuccess)
+            return fail(HC_PHMM_ENOMEM, "pinned staging ring");
+        HIP_TRY(hipEventCreateWithFlags(&d.ring.ev[k], hipEventDisableTiming));
+    }
     return HC_PHMM_OK;
 }
 

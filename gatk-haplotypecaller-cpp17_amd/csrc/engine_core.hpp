@@ -85,6 +85,19 @@ struct Slot {
     hipEvent_t up_ev[2] = {};   // staging halves: H2D of a half done (timing disabled)
 };
 
+// Pinned staging ring of a device: the flat call path streams its upload
+// through these chunks (fill chunk k on the host while chunk k-1 is copied),
+// so no call allocates pinned memory; allocated once at init.
+constexpr int kRingN = 4;
+constexpr size_t kRingChunk = size_t(32) << 20;
+struct Ring {
+    std::mutex mu;   // held by one part's fill at a time
+    char* buf[kRingN] = {};
+    hipEvent_t ev[kRingN] = {};   // the last H2D out of each chunk
+    bool used[kRingN] = {};
+    int next = 0;
+};
+
 struct Device {
     int ordinal = 0;
     int n_cu = 256;   // compute units (4 SIMDs each): sizes the latency models
@@ -96,6 +109,7 @@ struct Device {
     double* lut_d = nullptr;
     std::vector<Slot*> slots;
     double outstanding = 0;   // cells submitted and not yet collected
+    Ring ring;
 };
 
 // Engine state, guarded by g_mu: the device list, the slot pools, the

@@ -1,12 +1,412 @@
-// Flat batches planned on the device (placeholder until the device planner lands).
+// Flat calls (hc_phmm_pairs_flat / hc_phmm_submit_pairs: independent pairs in
+// the caller's host pools) planned on the device. The host does only what
+// needs the caller's memory, in two parallel passes over the pairs:
+//   pass 1  validate, gap-quality constancy (the reference's constant 'I'/'+'
+//           strings, sam.hpp:30-32, travel as three bytes per read), lengths
+//           and record sizes per mini-task, a sample of haplotype lengths for
+//           the width-cap model;
+//   pass 2  copy each pair's record (read bases, base qualities, gap planes
+//           only when they vary, hap bytes) and descriptor into the device's
+//           pinned staging ring, chunk by chunk, each chunk's H2D overlapping
+//           the fill of the next.
+// The device then packs rows and hap tables, chooses each pair's
+// column-segmented shape by the planner's cost model (plan_model.hpp), sorts
+// the pairs by (block width, lanes, R) and cuts the sorted runs into waves
+// (pack_kernels.hip flat_*), and runs the pass. No per-call pinned allocation.
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+
 #include "engine_core.hpp"
+#include "plan_model.hpp"
+#include "pool.hpp"
 
 namespace hcphmm {
 namespace eng {
+namespace {
 
-int plan_flat_device(Device&, const Src&, const PartSpec&, Slot*, bool, Part** out)
+constexpr int kMini = 512;              // pairs per mini-task of the host passes
+constexpr size_t kRowPadBefore = 256;   // words of slack before the packed rows (run_seg prefetch)
+constexpr int kMaxGroups = 1024;        // flat_scan_kernel: one group per thread
+constexpr int kMaxBins = 1 << 20;
+
+// Per mini-task results of pass 1.
+struct Mini {
+    int64_t rec = 0, rows = 0, hapw = 0;   // sums, then (after the scan) offsets
+    int rmax = 0, rmin = INT32_MAX, hmax = 0, hmin = INT32_MAX;
+    int nwide = 0;
+    bool bad = false;
+};
+
+struct FlatScratch {
+    std::vector<int32_t> gapw;
+    std::vector<Mini> mini;
+    std::vector<int32_t> hsamp;
+};
+thread_local FlatScratch t_fs;
+
+template <typename T>
+void grow(std::vector<T>& v, size_t n)
+{
+    if (v.size() < n) v.resize(n);
+}
+
+// Gap qualities of a read constant over its rows (blocks of 64 without early
+// exit inside a block, so the compiler vectorises the compare).
+bool constant_gaps(const uint8_t* i, const uint8_t* d, const uint8_t* c, int len)
+{
+    const uint8_t i0 = i[0], d0 = d[0], c0 = c[0];
+    int k = 0;
+    for (; k + 64 <= len; k += 64) {
+        uint8_t a = 0;
+        for (int j = 0; j < 64; ++j) a |= uint8_t((i[k + j] ^ i0) | (d[k + j] ^ d0) | (c[k + j] ^ c0));
+        if (a) return false;
+    }
+    uint8_t a = 0;
+    for (; k < len; ++k) a |= uint8_t((i[k] ^ i0) | (d[k] ^ d0) | (c[k] ^ c0));
+    return a == 0;
+}
+
+bool default_policies()
+{
+    for (const char* e : {"HC_PHMM_KERNEL", "HC_PHMM_LANE_SEG"}) {
+        const char* v = std::getenv(e);
+        if (v && *v && std::strcmp(v, "auto") != 0) return false;
+    }
+    return env_i64("HC_PHMM_SEG_CAP", 0) <= 0 && env_i64("HC_PHMM_SEG_Q", -1) < 0 &&
+           env_i64("HC_PHMM_FLAT_PLAN", 1) != 0;
+}
+
+}  // namespace
+
+int plan_flat_device(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool with_run, Part** out)
 {
     *out = nullptr;
+    if (!spec.flat || !src.R || !slot || !default_policies()) return HC_PHMM_OK;
+    PhaseTimer tm;
+    const int64_t lo = spec.lo, n = spec.hi - spec.lo;
+    if (n <= 0 || n > (int64_t(1) << 31) - 1) return HC_PHMM_OK;
+    FlatScratch& S = t_fs;
+    grow(S.gapw, size_t(n));
+    const int64_t nmini = (n + kMini - 1) / kMini;
+    S.mini.assign(size_t(nmini), Mini{});
+    const int64_t stride = std::max<int64_t>(1, n / 8192);   // cap-model sample of hap lengths
+    const int64_t nsamp = (n + stride - 1) / stride;
+    grow(S.hsamp, size_t(nsamp));
+    int32_t* gapw = S.gapw.data();
+    Mini* mini = S.mini.data();
+    int32_t* hsamp = S.hsamp.data();
+
+    // Pass 1.
+    parallel_for(nmini, [&](int64_t m0, int64_t m1) {
+        for (int64_t m = m0; m < m1; ++m) {
+            Mini& M = mini[m];
+            const int64_t a = m * kMini, e = std::min(n, a + kMini);
+            for (int64_t k = a; k < e; ++k) {
+                const int64_t p = lo + k;
+                const int R = src.R[p], H = src.H[p];
+                if (R <= 0 || R > HC_PHMM_MAX_READ_LEN || H <= 0 || H > HC_PHMM_MAX_HAP_LEN) {
+                    M.bad = true;
+                    gapw[k] = 0;
+                    continue;
+                }
+                const int64_t o = src.read_off[p];
+                const uint8_t *ip = src.ins + o, *dp = src.del + o, *cp = src.gcp + o;
+                const int32_t g = constant_gaps(ip, dp, cp, R)
+                                      ? int32_t((ip[0] & 127) | ((dp[0] & 127) << 7) | ((cp[0] & 127) << 14))
+                                      : -1;
+                gapw[k] = g;
+                M.rec += 2 * int64_t(R) + (g < 0 ? 3 * int64_t(R) : 0) + H;
+                M.rows += R;
+                M.hapw += hap_table_words(H);
+                M.rmax = std::max(M.rmax, R);
+                M.rmin = std::min(M.rmin, R);
+                M.hmax = std::max(M.hmax, H);
+                M.hmin = std::min(M.hmin, H);
+                M.nwide += H > 64 * 32;
+                if (k % stride == 0) hsamp[k / stride] = H;
+            }
+        }
+    }, 8);
+    tm.mark("flat: scan");
+
+    int rmax = 0, rmin = INT32_MAX, hmax = 0, hmin = INT32_MAX;
+    int64_t nwide = 0, rec = 0, rows = 0, hapw = 0;
+    for (int64_t m = 0; m < nmini; ++m) {
+        Mini& M = mini[m];
+        if (M.bad) return fail(HC_PHMM_EINVAL, "pair with invalid read length (1.." +
+                                                   std::to_string(HC_PHMM_MAX_READ_LEN) + ") or hap length (1.." +
+                                                   std::to_string(HC_PHMM_MAX_HAP_LEN) + ")");
+        rmax = std::max(rmax, M.rmax);
+        rmin = std::min(rmin, M.rmin);
+        hmax = std::max(hmax, M.hmax);
+        hmin = std::min(hmin, M.hmin);
+        nwide += M.nwide;
+        const int64_t r = M.rec, w = M.rows, h = M.hapw;
+        M.rec = rec;
+        M.rows = rows;
+        M.hapw = hapw;
+        rec += r;
+        rows += w;
+        hapw += h;
+    }
+    // Every pair must fit the column-segmented kernel (64 lanes of 64 columns);
+    // the host planner takes the others. So must the row and table pools.
+    if (hmax > 64 * kSegMaxBC || rows > INT32_MAX - 4096 || hapw > INT32_MAX) return HC_PHMM_OK;
+
+    // Width cap and the per-length candidates; groups = distinct (BC, nb),
+    // widest block first.
+    const double ravg = double(rows) / double(n);
+    int64_t lanes_at[kNCaps] = {};
+    double work_at[kNCaps] = {};
+    for (int64_t s = 0; s < nsamp; ++s) cap_sample(hsamp[s], ravg, stride, lanes_at, work_at);
+    const CapChoice cc = choose_cap(lanes_at, work_at, dv.n_cu);
+    const float* waste = cc.few_waves ? waste_per_lane() : waste_full();
+    std::vector<Cand> cand(size_t(hmax) + 1);
+    std::vector<uint16_t> keys;
+    for (int H = hmin; H <= hmax; ++H) {
+        cand[size_t(H)] = cand_of(H, cc.cap);
+        for (int q = 0; q < 2; ++q) keys.push_back(uint16_t(cand[size_t(H)].bc[q] << 8 | cand[size_t(H)].nb[q]));
+    }
+    std::sort(keys.begin(), keys.end(), std::greater<uint16_t>());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    const int ngroups = int(keys.size());
+    if (ngroups > kMaxGroups) return HC_PHMM_OK;
+    std::vector<int> gid(1 << 16, -1);
+    for (int g = 0; g < ngroups; ++g) gid[keys[size_t(g)]] = g;
+    // Counting-sort bins: (group, R descending), R coarsened if the span is wide.
+    int rshift = 0;
+    while (int64_t(ngroups) * (((rmax - rmin) >> rshift) + 1) > kMaxBins) ++rshift;
+    const int rspan = ((rmax - rmin) >> rshift) + 1;
+    const int nbins = ngroups * rspan;
+    // Waves the launch must cover: at most ceil(pairs / per) per group, per =
+    // floor(64 / nb) with nb the larger of a length's two candidates.
+    std::vector<float> inv_per(size_t(hmax) + 1, 0.f);
+    for (int H = hmin; H <= hmax; ++H)
+        inv_per[size_t(H)] = 1.f / float(64 / std::max(cand[size_t(H)].nb[0], cand[size_t(H)].nb[1]));
+    std::atomic<int64_t> wsum{0};
+    parallel_for(n, [&](int64_t a, int64_t e) {
+        double s = 0;
+        for (int64_t k = a; k < e; ++k) s += inv_per[size_t(src.H[lo + k])];
+        wsum += int64_t(s) + 2;
+    }, 16384);
+    const int64_t max_waves = wsum.load() + ngroups + 1;
+    if (max_waves > INT32_MAX / 4) return HC_PHMM_OK;
+    tm.mark("flat: model");
+
+    // Upload chunks: runs of mini-tasks whose records + descriptors fit a ring chunk.
+    std::vector<int64_t> chunk_m{0};
+    {
+        int64_t m = 0;
+        while (m < nmini) {
+            int64_t e = m;
+            auto bytes = [&](int64_t m1) {
+                const int64_t r1 = m1 < nmini ? mini[m1].rec : rec;
+                const int64_t pairs = std::min(n, m1 * kMini) - m * kMini;
+                return ((r1 - mini[m].rec + 255) & ~int64_t(255)) + int64_t(sizeof(FlatDesc)) * pairs;
+            };
+            while (e < nmini && bytes(e + 1) <= int64_t(kRingChunk)) ++e;
+            if (e == m) return HC_PHMM_OK;   // one mini-task larger than a chunk: host planner
+            chunk_m.push_back(e);
+            m = e;
+        }
+    }
+
+    // Device layout: the upload image, descriptors and tables, then what the
+    // device builds, the outputs and the rescue scratch.
+    const size_t n1 = size_t(n);
+    const size_t res_o64 = (sizeof(float) * n1 + 255) & ~size_t(255);
+    const size_t res_ofl = res_o64 + ((sizeof(double) * n1 + 255) & ~size_t(255));
+    const size_t res_bytes = res_ofl + n1;
+    struct Lay {
+        size_t off = 0;
+        size_t take(size_t b)
+        {
+            const size_t o = off;
+            off += (b + 255) & ~size_t(255);
+            return o;
+        }
+    } L;
+    const size_t o_img = L.take(size_t(rec) + 16);
+    const size_t o_desc = L.take(sizeof(FlatDesc) * n1);
+    const size_t tab_bytes = sizeof(int2) * (size_t(hmax) + 1) + sizeof(float) * 65 + sizeof(int2) * size_t(ngroups);
+    const size_t o_tab = L.take(tab_bytes);
+    const size_t row_pad = kRowPadBefore + size_t(rmax) + 256;
+    const size_t o_rows = L.take(sizeof(uint32_t) * (size_t(rows) + row_pad));
+    const size_t o_hapw = L.take(sizeof(uint32_t) * (size_t(hapw) + 16));
+    const size_t o_pairs = L.take(sizeof(PairDesc) * n1);
+    const size_t o_binof = L.take(sizeof(int) * n1);
+    const size_t o_hist = L.take(sizeof(int) * size_t(nbins));
+    const size_t o_gtab = L.take(sizeof(int) * 3 * size_t(ngroups));
+    const size_t o_order = L.take(sizeof(int) * n1);
+    const size_t o_waves = L.take(sizeof(LaneWave) * size_t(max_waves));
+    const size_t o_nw = L.take(sizeof(int));
+    const size_t o_res = L.take(res_bytes);
+    const size_t o_list = L.take(sizeof(int) * n1);
+    const size_t o_count = L.take(kNumCounters * sizeof(int));
+    const size_t o_sorted = L.take(sizeof(int) * n1);
+    const size_t o_big = L.take(sizeof(int) * n1);
+    const size_t o_bigc = L.take(sizeof(int));
+    const size_t o_plan = L.take(sizeof(Seg64Plan));
+    const size_t total = L.off;
+    const size_t host_res_off = (tab_bytes + 255) & ~size_t(255);
+    int rc = slot_reserve(*slot, total, host_res_off + res_bytes);
+    if (rc) return rc;
+    char* dev = slot->dev;
+    char* host = slot->host;
+    tm.mark("flat: layout");
+
+    // Tables (the slot's pinned area; its results image follows).
+    {
+        int2* ct = reinterpret_cast<int2*>(host);
+        for (int H = 0; H <= hmax; ++H) {
+            if (H < hmin) {
+                ct[H] = make_int2(0, 0);
+                continue;
+            }
+            const Cand c = cand[size_t(H)];
+            ct[H] = make_int2(c.bc[0] | c.nb[0] << 8 | gid[size_t(c.bc[0] << 8 | c.nb[0])] << 16,
+                              c.bc[1] | c.nb[1] << 8 | gid[size_t(c.bc[1] << 8 | c.nb[1])] << 16);
+        }
+        float* wt = reinterpret_cast<float*>(ct + hmax + 1);
+        std::memcpy(wt, waste, sizeof(float) * 65);
+        int2* gt = reinterpret_cast<int2*>(wt + 65);
+        for (int g = 0; g < ngroups; ++g) gt[g] = make_int2(keys[size_t(g)] >> 8, keys[size_t(g)] & 0xff);
+    }
+
+    auto* b = new_part(&dv);
+    b->spec = spec;
+    b->slot = slot;
+    b->dev_base = dev;
+    b->n = n;
+    b->Hmax = hmax;
+    b->n_lane = int(n);
+    b->n_seg_waves = int(max_waves);
+    b->lane_waves = int(max_waves);
+    b->d_nwaves = reinterpret_cast<int*>(dev + o_nw);
+    b->d_pairs = reinterpret_cast<PairDesc*>(dev + o_pairs);
+    b->d_rows = reinterpret_cast<uint32_t*>(dev + o_rows) + kRowPadBefore;
+    b->d_hapw = reinterpret_cast<uint32_t*>(dev + o_hapw);
+    b->d_lane_order = reinterpret_cast<int*>(dev + o_order);
+    b->d_lane_waves = reinterpret_cast<LaneWave*>(dev + o_waves);
+    b->res_bytes = res_bytes;
+    b->res_o64 = res_o64;
+    b->res_ofl = res_ofl;
+    b->own_raw32 = b->d_raw32 = reinterpret_cast<float*>(dev + o_res);
+    b->own_raw64 = b->d_raw64 = reinterpret_cast<double*>(dev + o_res + res_o64);
+    b->own_flag = b->d_flag = reinterpret_cast<uint8_t*>(dev + o_res + res_ofl);
+    b->d_list = reinterpret_cast<int*>(dev + o_list);
+    b->d_count = reinterpret_cast<int*>(dev + o_count);
+    b->d_sorted = reinterpret_cast<int*>(dev + o_sorted);
+    b->d_big = reinterpret_cast<int*>(dev + o_big);
+    b->d_big_count = reinterpret_cast<int*>(dev + o_bigc);
+    b->d_plan = reinterpret_cast<Seg64Plan*>(dev + o_plan);
+    b->n_wide = nwide;
+    b->host_res = host + host_res_off;
+    b->stream = slot->stream;
+    b->side = slot->side;
+    b->fork = slot->fork;
+    b->join = slot->join;
+    b->slot_ev = true;
+    b->pack_ev[0] = slot->ev[0];
+    b->pack_ev[1] = slot->ev[1];
+    b->ev_pool.push_back({slot->ev[2], slot->ev[3], slot->ev[4]});
+    b->done = slot->ev[5];
+    b->upload_bytes = size_t(rec) + sizeof(FlatDesc) * n1 + tab_bytes;
+    hipStream_t s = b->stream;
+
+    auto enqueue = [&]() -> int {
+        // Pass 2: chunks through the ring, each H2D'd as soon as it is filled.
+        {
+            std::lock_guard<std::mutex> lk(dv.ring.mu);
+            for (size_t c = 0; c + 1 < chunk_m.size(); ++c) {
+                const int64_t m0 = chunk_m[c], m1 = chunk_m[c + 1];
+                const int64_t p0 = m0 * kMini, p1 = std::min(n, m1 * kMini);
+                const int64_t r0 = mini[m0].rec, r1 = m1 < nmini ? mini[m1].rec : rec;
+                const int ri = dv.ring.next;
+                dv.ring.next = (ri + 1) % kRingN;
+                if (dv.ring.used[ri]) HIP_TRY(hipEventSynchronize(dv.ring.ev[ri]));
+                char* buf = dv.ring.buf[ri];
+                const size_t dbase = (size_t(r1 - r0) + 255) & ~size_t(255);
+                FlatDesc* dd = reinterpret_cast<FlatDesc*>(buf + dbase);
+                parallel_for(m1 - m0, [&](int64_t a, int64_t e) {
+                    for (int64_t m = m0 + a; m < m0 + e; ++m) {
+                        int64_t ro = mini[m].rec, rw = mini[m].rows, hw = mini[m].hapw;
+                        const int64_t k1 = std::min(n, (m + 1) * kMini);
+                        for (int64_t k = m * kMini; k < k1; ++k) {
+                            const int64_t p = lo + k;
+                            const int R = src.R[p], H = src.H[p];
+                            const int32_t g = gapw[k];
+                            const int64_t o = src.read_off[p];
+                            uint8_t* d = reinterpret_cast<uint8_t*>(buf + (ro - r0));
+                            std::memcpy(d, src.rs + o, size_t(R));
+                            std::memcpy(d + R, src.q + o, size_t(R));
+                            size_t at = 2 * size_t(R);
+                            if (g < 0) {
+                                std::memcpy(d + at, src.ins + o, size_t(R));
+                                std::memcpy(d + at + R, src.del + o, size_t(R));
+                                std::memcpy(d + at + 2 * R, src.gcp + o, size_t(R));
+                                at += 3 * size_t(R);
+                            }
+                            std::memcpy(d + at, src.hap + src.hap_off[p], size_t(H));
+                            dd[k - p0] = FlatDesc{ro, int(rw), R, H, int(hw), g, 0};
+                            ro += int64_t(at) + H;
+                            rw += R;
+                            hw += hap_table_words(H);
+                        }
+                    }
+                }, 1);
+                HIP_TRY(hipMemcpyAsync(dev + o_img + r0, buf, size_t(r1 - r0), hipMemcpyHostToDevice, s));
+                HIP_TRY(hipMemcpyAsync(dev + o_desc + sizeof(FlatDesc) * size_t(p0), dd,
+                                       sizeof(FlatDesc) * size_t(p1 - p0), hipMemcpyHostToDevice, s));
+                HIP_TRY(hipEventRecord(dv.ring.ev[ri], s));
+                dv.ring.used[ri] = true;
+            }
+        }
+        tm.mark("flat: fill + H2D");
+        HIP_TRY(hipMemcpyAsync(dev + o_tab, host, tab_bytes, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipEventRecord(b->pack_ev[0], s));
+        FlatPlanArgs a{};
+        a.img = reinterpret_cast<const uint8_t*>(dev + o_img);
+        a.desc = reinterpret_cast<const FlatDesc*>(dev + o_desc);
+        a.n = int(n);
+        a.rows = b->d_rows;
+        a.hapw = b->d_hapw;
+        a.pairs = b->d_pairs;
+        a.ctab = reinterpret_cast<const int2*>(dev + o_tab);
+        a.waste = reinterpret_cast<const float*>(dev + o_tab + sizeof(int2) * (size_t(hmax) + 1));
+        a.groups = reinterpret_cast<const int2*>(dev + o_tab + sizeof(int2) * (size_t(hmax) + 1) + sizeof(float) * 65);
+        a.rmax = rmax;
+        a.rshift = rshift;
+        a.rspan = rspan;
+        a.bin_of = reinterpret_cast<int*>(dev + o_binof);
+        a.hist = reinterpret_cast<int*>(dev + o_hist);
+        a.nbins = nbins;
+        a.ngroups = ngroups;
+        a.gtab = reinterpret_cast<int*>(dev + o_gtab);
+        a.order = b->d_lane_order;
+        a.waves = b->d_lane_waves;
+        a.max_waves = int(max_waves);
+        a.nwaves = reinterpret_cast<int*>(dev + o_nw);
+        a.counters = b->d_count;
+        HIP_TRY(launch_flat_plan(a, s));
+        HIP_TRY(hipEventRecord(b->pack_ev[1], s));
+        if (with_run) {
+            const int r = run_part(b, s);
+            if (r) return r;
+            return enqueue_results(b, s);
+        }
+        return HC_PHMM_OK;
+    };
+    rc = enqueue();
+    tm.mark("flat: enqueue");
+    if (rc) {
+        (void)hipStreamSynchronize(s);
+        b->slot = nullptr;   // the caller returns the slot
+        free_part(b);
+        return rc;
+    }
+    *out = b;
     return HC_PHMM_OK;
 }
 

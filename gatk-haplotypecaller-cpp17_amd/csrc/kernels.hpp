@@ -33,6 +33,11 @@ inline int hap_table_words(int H) { return ((H + 31) / 32 + kHapPadWords) * 5; }
 // Per pair descriptor: {row offset into rows[], R, word offset into hapw[], H}.
 using PairDesc = int4;
 
+// Run counters of a part (zeroed when the part is prepared): [0, 1] rescue
+// list lengths and [2, 3] in-wave rescue counts, by run parity (a run zeroes
+// the other parity's for the next run: no memset per run).
+constexpr int kNumCounters = 4;
+
 struct DiagArgs {
     const PairDesc* pairs;
     const int* order;         // slot -> pair id (caller order)
@@ -52,6 +57,38 @@ struct DiagArgs {
                               // zeroed for the next run (no memset per run)
 };
 
+// fp64 rescue pass in column-segmented form, planned on the device
+// (lane_kernel.hip rescue_plan_kernel). A pair takes a slot of 2^k lanes
+// (64 >> k pairs per wave) and the narrowest fp64 block width that covers its
+// hap on those lanes, so the slot's lanes are all used: (k, width) is its
+// class. Classes are numbered widest slot and block first (the longest waves
+// are dispatched first); the last class holds haps wider than 64 blocks of 32
+// (anti-diagonal kernel, through `big`).
+constexpr int kSeg64Widths = 7;   // fp64 block widths 8, 12, ..., 32
+constexpr int kSeg64Classes = 7 * kSeg64Widths + 1;
+__host__ __device__ constexpr int seg64_width(int wi) { return 8 + 4 * wi; }
+struct Seg64Plan {
+    int bc0;                        // block width bound of the pass (32, or 16 / 8 for short lists)
+    int n_class[kSeg64Classes];
+    int off_class[kSeg64Classes];   // class c's entries in `sorted` start here
+    int wave_base[kSeg64Classes];   // first wave of class c; [last] = total waves
+};
+struct Seg64Args {
+    const PairDesc* pairs;
+    const uint32_t* rows;
+    const uint32_t* hapw;
+    const double* lut;
+    const int* list;          // rescue list (fp32 pass, arbitrary order)
+    const int* count;         // its length
+    int* count_reset;         // the other run parity's counter, zeroed for the next run
+    int* inker_reset;         // the other run parity's in-wave rescue counter, likewise
+    int* sorted;              // list in class order (n entries)
+    int* big;                 // last-class pairs (anti-diagonal fp64 kernel)
+    int* big_count;
+    Seg64Plan* plan;
+    double* raw_out;          // raw f64 sums by pair id
+    long long min_lanes;      // narrower blocks below this many lanes at bc = 32
+};
 // Lane-per-pair kernel (large batches): one lane owns one pair and sweeps it
 // row by row over register-resident blocks of kLaneBlock columns. A wave holds
 // 64 length-binned pairs; wave_meta gives its rows (max R) and column coverage.
@@ -112,38 +149,6 @@ int seg_width_ceil(int bc);   // narrowest compiled width >= bc (-1: none)
 constexpr int kSegMaxBC = 64;
 constexpr int kSegMinBC = 8;    // narrowest compiled fp32 block width
 
-// fp64 rescue pass in column-segmented form, planned on the device
-// (lane_kernel.hip rescue_plan_kernel). A pair takes a slot of 2^k lanes
-// (64 >> k pairs per wave) and the narrowest fp64 block width that covers its
-// hap on those lanes, so the slot's lanes are all used: (k, width) is its
-// class. Classes are numbered widest slot and block first (the longest waves
-// are dispatched first); the last class holds haps wider than 64 blocks of 32
-// (anti-diagonal kernel, through `big`).
-constexpr int kSeg64Widths = 7;   // fp64 block widths 8, 12, ..., 32
-constexpr int kSeg64Classes = 7 * kSeg64Widths + 1;
-__host__ __device__ constexpr int seg64_width(int wi) { return 8 + 4 * wi; }
-struct Seg64Plan {
-    int bc0;                        // block width bound of the pass (32, or 16 / 8 for short lists)
-    int n_class[kSeg64Classes];
-    int off_class[kSeg64Classes];   // class c's entries in `sorted` start here
-    int wave_base[kSeg64Classes];   // first wave of class c; [last] = total waves
-};
-struct Seg64Args {
-    const PairDesc* pairs;
-    const uint32_t* rows;
-    const uint32_t* hapw;
-    const double* lut;
-    const int* list;          // rescue list (fp32 pass, arbitrary order)
-    const int* count;         // its length
-    int* count_reset;         // the other run parity's counter, zeroed for the next run
-    int* inker_reset;         // the other run parity's in-wave rescue counter, likewise
-    int* sorted;              // list in class order (n entries)
-    int* big;                 // last-class pairs (anti-diagonal fp64 kernel)
-    int* big_count;
-    Seg64Plan* plan;
-    double* raw_out;          // raw f64 sums by pair id
-    long long min_lanes;      // narrower blocks below this many lanes at bc = 32
-};
 hipError_t launch_rescue_seg64(const Seg64Args& a, int grid, hipStream_t s);
 
 // Launchers (kernels.hip). W = lanes per pair: 16, 32 or 64.
@@ -206,8 +211,47 @@ struct GridPrepArgs {
     const int *rord, *hord;
     int* order;
     LaneWave* waves;
-    int* counters;   // 4 ints zeroed (run-parity rescue counters)
+    int* counters;   // kNumCounters ints zeroed (run counters)
 };
 hipError_t launch_prepare_grid(const GridPrepArgs& a, hipStream_t s);
+
+// Flat batches planned on the device (flat_plan.cpp, pack_kernels.hip): the
+// host uploads one record per pair — its read bases, base qualities, gap
+// qualities only when they vary, then its hap bytes — and a descriptor; the
+// device packs rows and hap tables, picks each pair's column-segmented shape
+// (the host planner's cost model, from per-length candidate tables), sorts the
+// pairs by (block width, lanes, R) with a counting sort and cuts the sorted
+// runs into waves of floor(64 / nb) pairs.
+struct FlatDesc {
+    long long rec;   // byte offset of the pair's record in the upload image
+    int row_off;     // first packed row of the read
+    int R, H;
+    int hapw_off;    // first word of the hap's match table
+    int gapw;        // constant gap qualities i | d << 7 | c << 14, or -1 (planes in the record)
+    int pad;
+};
+struct FlatPlanArgs {
+    const uint8_t* img;
+    const FlatDesc* desc;
+    int n;
+    uint32_t* rows;
+    uint32_t* hapw;
+    PairDesc* pairs;
+    const int2* ctab;      // [H]: the two candidates, bc | nb << 8 | group << 16
+    const float* waste;    // [65]: lane-waste weight of nb lanes
+    int rmax, rshift, rspan;   // bin = group * rspan + ((rmax - R) >> rshift)
+    int* bin_of;           // per pair
+    int* hist;             // nbins counters (zeroed by the launcher), then slot cursors
+    int nbins;
+    const int2* groups;    // per group: {bc, nb}, widest block first
+    int ngroups;
+    int* gtab;             // per group: {first slot, pairs, first wave}
+    int* order;            // slot -> pair
+    LaneWave* waves;
+    int max_waves;         // waves the launch covers (upper bound of the plan's)
+    int* nwaves;           // the plan's wave count
+    int* counters;         // kNumCounters run counters, zeroed
+};
+hipError_t launch_flat_plan(const FlatPlanArgs& a, hipStream_t s);
 
 }  // namespace hcphmm

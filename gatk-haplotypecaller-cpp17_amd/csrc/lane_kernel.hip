@@ -11,7 +11,8 @@
 // operations in the reference's order, evaluated one row earlier.
 //
 // Three kernels:
-//   phmm_seg_kernel   (fp32)  column-segmented waves planned on the host: a pair
+//   phmm_seg_kernel   (fp32)  column-segmented waves (planned on the host or, for
+//                             flat calls, on the device): a pair
 //                             over ceil(H/BC) consecutive lanes, one row of skew
 //                             per lane, values handed right by DPP (run_seg);
 //   phmm_seg64_kernel (fp64)  the rescue pass in the same form, planned on the
@@ -178,83 +179,9 @@ __global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
 // Column-segmented fp32 waves (host-planned). The wave's npairs pairs are the
 // slots slot0 .. slot0+npairs-1; pair g takes nb_g = ceil(H_g / BC) consecutive
 // lanes in slot order. Lanes past the last group idle (s = 0, no output).
-#ifndef HC_SEG_WPB
-#define HC_SEG_WPB 4   // seg waves per workgroup (A/B builds: 1, 2)
-#endif
-template <int OCC>
-__global__ __launch_bounds__(64 * HC_SEG_WPB, OCC) void phmm_seg_kernel(LaneArgs a)
-{
-    __shared__ float slut[kSlutLen];
-    load_slut(slut, a.lut);
-    const int wid = blockIdx.x * HC_SEG_WPB + (threadIdx.x >> 6);
-    const int n_waves = a.n_waves_dev ? __builtin_amdgcn_readfirstlane(*a.n_waves_dev) : a.n_waves;
-    if (wid >= n_waves) return;
-    const int lane = threadIdx.x & 63;
-    const unsigned long long t_start = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
-    const LaneWave wv = load_wave(a.waves, wid);
-    const int bc = wv.ncols;
-    __shared__ uint2 mtab[HC_SEG_WPB][5 * 64];
-    uint2* mt = mtab[threadIdx.x >> 6];
-    // Lane -> (group, block): group g's lanes start at the prefix sum of nb.
-    int* gmap = reinterpret_cast<int*>(mt);   // 128 ints, used before the match table
-    int nb_g = 0;
-    if (lane < wv.npairs) nb_g = (a.pairs[a.order[wv.slot0 + lane]].w + bc - 1) / bc;
-    int start = nb_g;   // inclusive scan of nb over lanes (Hillis-Steele through LDS)
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        gmap[lane] = start;
-        __builtin_amdgcn_wave_barrier();
-        const int v = lane >= d ? gmap[lane - d] : 0;
-        __builtin_amdgcn_wave_barrier();
-        start += v;
-    }
-    start -= nb_g;
-    gmap[lane] = -1;
-    __builtin_amdgcn_wave_barrier();
-    if (lane < wv.npairs)
-        for (int t = 0; t < nb_g; ++t) {
-            gmap[start + t] = lane;
-            gmap[64 + start + t] = t;
-        }
-    __builtin_amdgcn_wave_barrier();
-    const int g = gmap[lane];
-    int s = gmap[64 + lane];
-    __builtin_amdgcn_wave_barrier();
-    const int pid = a.order[wv.slot0 + (g >= 0 ? g : 0)];
-    const LaneCtx cx = pair_ctx(a.pairs, a.rows, a.hapw, pid);
-    const bool owner = g >= 0 && s == (cx.H + bc - 1) / bc - 1;
-    if (g < 0) s = 0;
-    const uint32_t w1 = cx.rrow[0];
-    const float T0 = row0_t<float>(a.lut, w1, cx.H);
-    const bool wave_eq = __builtin_amdgcn_ballot_w64(!read_eq(w1)) == 0;
-    const SegSteps st{wv.rmax, wv.rmin, wv.nsteps};
-    float sumM = 0.f, sumX = 0.f;
-    switch (bc) {
-#define HC_SEG_CASE(W) \
-    case W: run_seg_bc<float, W>(a.lut, slut, st, lane, s, cx, T0, sumM, sumX, mt, wave_eq); break;
-        HC_SEG_WIDTHS(HC_SEG_CASE)
-#undef HC_SEG_CASE
-    default: break;
-    }
-    // fp32 result and rescue decision (intel_pairhmm.hpp:133-139).
-    bool resc = false;
-    if (owner) {
-        const float raw = sumM + sumX;
-        resc = raw < 1e-28f;   // MIN_ACCEPTED, pairhmm_common.h:16
-        a.raw_out[pid] = raw;
-        a.rescue_flag[pid] = resc;
-        if (!resc) a.raw64_zero[pid] = 0.0;
-    }
-    const uint64_t todo = __builtin_amdgcn_ballot_w64(resc);
-    if (todo) rescue_in_wave(a, todo, pid, lane, mt);
-    if (a.timeline && lane == 0) {
-        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
-        a.timeline[3 * size_t(wid)] = t_start;
-        a.timeline[3 * size_t(wid) + 1] = t_end;
-        a.timeline[3 * size_t(wid) + 2] = unsigned(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));
-    }
-}
-
+// Seg waves per workgroup: 1, 2 and 4 time the same (profiles/
+// r02_seg_waves_per_workgroup_ab.txt); 4 shares the LDS prior table.
+constexpr int kSegWPB = 4;
 // ---------------------------------------------------------------------------
 // fp64 rescue pass (intel_pairhmm.hpp:137-139) in column-segmented form.
 //
@@ -336,6 +263,89 @@ __global__ __launch_bounds__(1024) void rescue_plan_kernel(Seg64Args a)
     }
 }
 
+// One column-segmented wave (wid) of the fp32 pass.
+__device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float* __restrict__ slut)
+{
+    const int lane = threadIdx.x & 63;
+    const unsigned long long t_start = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
+    const LaneWave wv = load_wave(a.waves, wid);
+    const int bc = wv.ncols;
+    __shared__ uint2 mtab[kSegWPB][5 * 64];
+    uint2* mt = mtab[threadIdx.x >> 6];
+    // Lane -> (group, block): group g's lanes start at the prefix sum of nb.
+    int* gmap = reinterpret_cast<int*>(mt);   // 128 ints, used before the match table
+    int nb_g = 0;
+    if (lane < wv.npairs) nb_g = (a.pairs[a.order[wv.slot0 + lane]].w + bc - 1) / bc;
+    int start = nb_g;   // inclusive scan of nb over lanes (Hillis-Steele through LDS)
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        gmap[lane] = start;
+        __builtin_amdgcn_wave_barrier();
+        const int v = lane >= d ? gmap[lane - d] : 0;
+        __builtin_amdgcn_wave_barrier();
+        start += v;
+    }
+    start -= nb_g;
+    gmap[lane] = -1;
+    __builtin_amdgcn_wave_barrier();
+    if (lane < wv.npairs)
+        for (int t = 0; t < nb_g; ++t) {
+            gmap[start + t] = lane;
+            gmap[64 + start + t] = t;
+        }
+    __builtin_amdgcn_wave_barrier();
+    const int g = gmap[lane];
+    int s = gmap[64 + lane];
+    __builtin_amdgcn_wave_barrier();
+    const int pid = a.order[wv.slot0 + (g >= 0 ? g : 0)];
+    const LaneCtx cx = pair_ctx(a.pairs, a.rows, a.hapw, pid);
+    const bool owner = g >= 0 && s == (cx.H + bc - 1) / bc - 1;
+    if (g < 0) s = 0;
+    const uint32_t w1 = cx.rrow[0];
+    const float T0 = row0_t<float>(a.lut, w1, cx.H);
+    const bool wave_eq = __builtin_amdgcn_ballot_w64(!read_eq(w1)) == 0;
+    const SegSteps st{wv.rmax, wv.rmin, wv.nsteps};
+    float sumM = 0.f, sumX = 0.f;
+    switch (bc) {
+#define HC_SEG_CASE(W) \
+    case W: run_seg_bc<float, W>(a.lut, slut, st, lane, s, cx, T0, sumM, sumX, mt, wave_eq); break;
+        HC_SEG_WIDTHS(HC_SEG_CASE)
+#undef HC_SEG_CASE
+    default: break;
+    }
+    // fp32 result and rescue decision (intel_pairhmm.hpp:133-139).
+    bool resc = false;
+    if (owner) {
+        const float raw = sumM + sumX;
+        resc = raw < 1e-28f;   // MIN_ACCEPTED, pairhmm_common.h:16
+        a.raw_out[pid] = raw;
+        a.rescue_flag[pid] = resc;
+        if (!resc) a.raw64_zero[pid] = 0.0;
+    }
+    const uint64_t todo = __builtin_amdgcn_ballot_w64(resc);
+    if (todo) rescue_in_wave(a, todo, pid, lane, mt);
+    if (a.timeline && lane == 0) {
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        a.timeline[3 * size_t(wid)] = t_start;
+        a.timeline[3 * size_t(wid) + 1] = t_end;
+        a.timeline[3 * size_t(wid) + 2] = unsigned(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));
+    }
+}
+
+
+template <int OCC>
+__global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
+{
+    __shared__ float slut[kSlutLen];
+    // Device-planned parts launch an upper bound of waves: surplus workgroups
+    // leave before the LDS fill (workgroup-uniform).
+    const int n_waves = a.n_waves_dev ? __builtin_amdgcn_readfirstlane(*a.n_waves_dev) : a.n_waves;
+    if (int(blockIdx.x) * kSegWPB >= n_waves) return;
+    load_slut(slut, a.lut);
+    const int wid = blockIdx.x * kSegWPB + (threadIdx.x >> 6);
+    if (wid < n_waves) seg_wave(a, wid, slut);
+}
+
 // Wave-uniform max / min of a per-lane int (once per wave).
 __device__ __forceinline__ int wave_max(int v)
 {
@@ -402,10 +412,10 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
 
 // One-lane kernel variants: {pairs per lane, block columns, waves per SIMD}.
 // Block widths are multiples of 32 (a block starts on a match-word boundary).
-#ifndef HC_SEG_OCC
-#define HC_SEG_OCC 3
-#endif
-constexpr int kSegOcc = HC_SEG_OCC;   // waves per SIMD of the fp32 column-segmented kernel
+// Waves per SIMD of the fp32 column-segmented kernel (168 VGPRs; a 128-VGPR
+// build at 4 waves per SIMD needs narrower blocks and measured 1-3 % slower,
+// profiles/r02_occ3_vs_occ4_caps.jsonl).
+constexpr int kSegOcc = 3;
 constexpr int kSeg64Occ = 2;   // fp64: 2 VGPRs per value
 static const LaneVariant kVariants[] = {
     {1, 64, 3}, {1, 64, 2}, {1, 32, 4},
@@ -451,15 +461,15 @@ int seg_width_ceil(int bc)
 hipError_t launch_lane_seg_f32(const LaneArgs& a, hipStream_t s)
 {
     if (a.n_waves <= 0) return hipSuccess;
-    const int grid = (a.n_waves + HC_SEG_WPB - 1) / HC_SEG_WPB;
-    hipLaunchKernelGGL((phmm_seg_kernel<kSegOcc>), dim3(grid), dim3(64 * HC_SEG_WPB), 0, s, a);
+    const int grid = (a.n_waves + kSegWPB - 1) / kSegWPB;
+    hipLaunchKernelGGL((phmm_seg_kernel<kSegOcc>), dim3(grid), dim3(64 * kSegWPB), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_rescue_seg64(const Seg64Args& a, int grid, hipStream_t s)
 {
     hipLaunchKernelGGL(rescue_plan_kernel, dim3(1), dim3(1024), 0, s, a);
-    hipError_t e = hipGetLastError();
+    const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((phmm_seg64_kernel<kSeg64Occ>), dim3(grid), dim3(256), 0, s, a);
     return hipGetLastError();

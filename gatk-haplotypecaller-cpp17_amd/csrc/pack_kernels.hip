@@ -1,6 +1,7 @@
-// Device-side packing of a batch (the reference's getData / precompute_masks
-// work, intel_pairhmm.hpp:154-203 and avx-pairhmm-template.h:3-35, done once
-// per read and once per haplotype instead of once per pair).
+// Device-side packing and planning of a batch (the reference's getData /
+// precompute_masks work, intel_pairhmm.hpp:154-203 and
+// avx-pairhmm-template.h:3-35, done once per read and once per haplotype
+// instead of once per pair).
 //
 //   pack_reads   uploaded read bytes -> one uint32 row word per base
 //                (kernels.hpp pack_row). The upload carries 2 bytes per base
@@ -9,9 +10,13 @@
 //                them once in its descriptor, the others send 3 more planes.
 //   hap_tables   hap bytes -> per-hap match table, (ceil(H/32) + 3) rows of 5
 //                words: bit (MSB first) per column for read codes 0..4.
+//   grid_*       descriptors, slot order and waves of a structured
+//                (cross-product) plan from its block and segment tables.
+//   flat_*       a flat batch planned on the device: rows, tables, each pair's
+//                segmented shape, a counting sort and the waves (flat_plan.cpp).
 //
-// Both are byte-streaming kernels, one wave per read / per haplotype (coalesced
-// byte loads across the wave; the match words come from wave ballots).
+// The packers are byte-streaming kernels, one wave per read / per haplotype
+// (coalesced byte loads across the wave; the match words come from ballots).
 #include <algorithm>
 
 #include "kernels.hpp"
@@ -25,9 +30,30 @@ __device__ __forceinline__ uint32_t base_code(uint32_t b)
     return b == 'C' ? 1u : b == 'T' ? 2u : b == 'G' ? 3u : b == 'N' ? 4u : 0u;
 }
 
-// One wave per read (grid-stride over reads). rdesc: {row offset, length,
-// constant gap qualities i | d << 7 | c << 14 (already & 127) or -1 when they
-// vary, offset of the read's rows in the i/d/c planes when they vary}.
+// Row words of one read, lanes over rows (a wave). gw: constant gap qualities
+// i | d << 7 | c << 14 (already & 127), or -1 when they vary: then the i, d, c
+// planes are at gi, gd, gc.
+__device__ __forceinline__ void pack_read(const uint8_t* __restrict__ bases, const uint8_t* __restrict__ quals,
+                                          const uint8_t* __restrict__ gi, const uint8_t* __restrict__ gd,
+                                          const uint8_t* __restrict__ gc, int len, int gw, uint32_t* __restrict__ rows,
+                                          int lane)
+{
+    for (int k = lane; k < len; k += 64) {
+        const uint32_t q = quals[k] & 127u;
+        const uint32_t code = base_code(bases[k]) << 28;
+        uint32_t w;
+        if (gw >= 0) {
+            w = q | (uint32_t(gw) << 7) | code;
+            if (k == 0) w |= 0x80000000u;   // constant-gap tag on the read's first row
+        } else {
+            w = q | ((gi[k] & 127u) << 7) | ((gd[k] & 127u) << 14) | ((gc[k] & 127u) << 21) | code;
+        }
+        rows[k] = w;
+    }
+}
+
+// One wave per read (grid-stride). rdesc: {row offset, length, constant gap
+// qualities or -1, offset of the read's rows in the i/d/c planes when they vary}.
 __device__ __forceinline__ void pack_reads(const uint8_t* __restrict__ bases, const uint8_t* __restrict__ quals,
                                            const uint8_t* __restrict__ gaps, long long gap_stride,
                                            const int4* __restrict__ rdesc, int nreads, uint32_t* __restrict__ rows)
@@ -37,55 +63,48 @@ __device__ __forceinline__ void pack_reads(const uint8_t* __restrict__ bases, co
         const int4 d = rdesc[r];
         const int off = __builtin_amdgcn_readfirstlane(d.x), len = __builtin_amdgcn_readfirstlane(d.y);
         const int gw = __builtin_amdgcn_readfirstlane(d.z), goff = __builtin_amdgcn_readfirstlane(d.w);
-        for (int k = lane; k < len; k += 64) {
-            const uint32_t q = quals[off + k] & 127u;
-            const uint32_t code = base_code(bases[off + k]) << 28;
-            uint32_t w;
-            if (gw >= 0) {
-                w = q | (uint32_t(gw) << 7) | code;
-                if (k == 0) w |= 0x80000000u;   // constant-gap tag on the read's first row
-            } else {
-                const uint32_t i = gaps[goff + k] & 127u, dd = gaps[gap_stride + goff + k] & 127u,
-                               c = gaps[2 * gap_stride + goff + k] & 127u;
-                w = q | (i << 7) | (dd << 14) | (c << 21) | code;
-            }
-            rows[off + k] = w;
-        }
+        const uint8_t* g = gaps + goff;
+        pack_read(bases + off, quals + off, g, g + gap_stride, g + 2 * gap_stride, len, gw, rows + off, lane);
     }
 }
 
-// One wave per haplotype (grid-stride). Table row w + kHapLead holds columns
+// Match table of one haplotype (a wave): row w + kHapLead holds columns
 // 32w+1 .. 32w+32; lanes 0-31 take the columns of row w, lanes 32-63 those of
 // row w+1, and the wave ballot of "hap base matches read code rc" gives both
 // rows' words for rc at once (bit-reversed: column 1 is the MSB).
+__device__ __forceinline__ void hap_table(const uint8_t* __restrict__ hb, int H, uint32_t* __restrict__ o, int lane)
+{
+    const int nw = (H + 31) / 32;
+    // Zero rows: kHapLead before the data, one after.
+    if (lane < 5 * kHapLead) o[lane] = 0u;
+    if (lane < 5) o[(kHapLead + nw) * 5 + lane] = 0u;
+    for (int w0 = 0; w0 < nw; w0 += 2) {
+        const int col = w0 * 32 + lane;   // 0-based hap column
+        const uint32_t hc = col < H ? base_code(hb[col]) : 7u;   // 7: past the hap, no match
+        uint32_t word = 0u;
+#pragma unroll
+        for (int rc = 0; rc < 5; ++rc) {
+            // read code rc matches: equal code, hap 'N' (matches every rc), or read 'N'
+            const bool m = hc != 7u && (hc == uint32_t(rc) || hc == 4u || rc == 4);
+            const uint64_t bl = __builtin_amdgcn_ballot_w64(m);
+            const uint32_t lo = __builtin_bitreverse32(uint32_t(bl)), hi = __builtin_bitreverse32(uint32_t(bl >> 32));
+            if (lane == rc) word = lo;
+            if (lane == 5 + rc) word = hi;
+        }
+        if (lane < 5) o[(kHapLead + w0) * 5 + lane] = word;
+        if (lane >= 5 && lane < 10 && w0 + 1 < nw) o[(kHapLead + w0 + 1) * 5 + lane - 5] = word;
+    }
+}
+
+// One wave per haplotype (grid-stride); haps[h] = {byte offset, H, table word offset, 0}.
 __device__ __forceinline__ void hap_tables(const uint8_t* __restrict__ hap_bytes, const int4* __restrict__ haps,
                                            int nhaps, uint32_t* __restrict__ hapw)
 {
     const int lane = threadIdx.x & 63;
     for (int h = blockIdx.x * 4 + (threadIdx.x >> 6); h < nhaps; h += gridDim.x * 4) {
-        const int4 hd = haps[h];   // {byte offset, H, table word offset, 0}
+        const int4 hd = haps[h];
         const int off = __builtin_amdgcn_readfirstlane(hd.x), H = __builtin_amdgcn_readfirstlane(hd.y);
-        uint32_t* __restrict__ o = hapw + __builtin_amdgcn_readfirstlane(hd.z);
-        const int nw = (H + 31) / 32;
-        // Zero rows: kHapLead before the data, one after.
-        if (lane < 5 * kHapLead) o[lane] = 0u;
-        if (lane < 5) o[(kHapLead + nw) * 5 + lane] = 0u;
-        for (int w0 = 0; w0 < nw; w0 += 2) {
-            const int col = w0 * 32 + lane;   // 0-based hap column
-            const uint32_t hc = col < H ? base_code(hap_bytes[off + col]) : 7u;   // 7: past the hap, no match
-            uint32_t word = 0u;
-#pragma unroll
-            for (int rc = 0; rc < 5; ++rc) {
-                // read code rc matches: equal code, hap 'N' (matches every rc), or read 'N'
-                const bool m = hc != 7u && (hc == uint32_t(rc) || hc == 4u || rc == 4);
-                const uint64_t b = __builtin_amdgcn_ballot_w64(m);
-                const uint32_t lo = __builtin_bitreverse32(uint32_t(b)), hi = __builtin_bitreverse32(uint32_t(b >> 32));
-                if (lane == rc) word = lo;
-                if (lane == 5 + rc) word = hi;
-            }
-            if (lane < 5) o[(kHapLead + w0) * 5 + lane] = word;
-            if (lane >= 5 && lane < 10 && w0 + 1 < nw) o[(kHapLead + w0 + 1) * 5 + lane - 5] = word;
-        }
+        hap_table(hap_bytes + off, H, hapw + __builtin_amdgcn_readfirstlane(hd.z), lane);
     }
 }
 
@@ -188,11 +207,147 @@ __global__ __launch_bounds__(256) void hap_tables_kernel(const uint8_t* __restri
 // descriptors, slot order and waves — four fewer launches per region call.
 __global__ __launch_bounds__(256) void prepare_grid_kernel(GridPrepArgs a)
 {
-    if (blockIdx.x == 0 && threadIdx.x < 4) a.counters[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < kNumCounters) a.counters[threadIdx.x] = 0;
     pack_reads(a.bases, a.quals, a.gaps, a.gap_stride, a.rdesc, a.nreads, a.rows);
     hap_tables(a.hap_bytes, a.hdesc, a.nhaps, a.hapw);
     grid_pairs(a.blocks, a.nblocks, a.npairs, a.rdesc, a.hdesc, a.pairs);
     grid_waves(a.segs, a.nsegs, a.nslots, a.nwaves, a.rord, a.hord, a.rdesc, a.order, a.waves);
+}
+
+// ---------------------------------------------------------------------------
+// Flat batches planned on the device (kernels.hpp FlatPlanArgs).
+
+// One wave per pair (grid-stride): its rows, its hap table, its pair
+// descriptor, and its plan key — the cheaper of its two (block width, lanes)
+// candidates by the host planner's cost model, and the counting-sort bin of
+// (candidate group, R descending).
+__global__ __launch_bounds__(256) void flat_prep_kernel(FlatPlanArgs a)
+{
+    if (blockIdx.x == 0 && threadIdx.x < kNumCounters) a.counters[threadIdx.x] = 0;
+    const int lane = threadIdx.x & 63;
+    for (int p = blockIdx.x * 4 + (threadIdx.x >> 6); p < a.n; p += gridDim.x * 4) {
+        const FlatDesc d = a.desc[p];
+        const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(d.rec & 0xffffffffll));
+        const unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(d.rec >> 32));
+        const uint8_t* bases = a.img + (long long)(((unsigned long long)hi << 32) | lo);
+        const int R = __builtin_amdgcn_readfirstlane(d.R), H = __builtin_amdgcn_readfirstlane(d.H);
+        const int ro = __builtin_amdgcn_readfirstlane(d.row_off), ho = __builtin_amdgcn_readfirstlane(d.hapw_off);
+        const int gw = __builtin_amdgcn_readfirstlane(d.gapw);
+        const uint8_t* quals = bases + R;
+        const uint8_t* gaps = quals + R;
+        pack_read(bases, quals, gaps, gaps + R, gaps + 2 * R, R, gw, a.rows + ro, lane);
+        hap_table(gaps + (gw < 0 ? 3 * R : 0), H, a.hapw + ho, lane);
+        if (lane == 0) {
+            a.pairs[p] = make_int4(ro, R, ho, H);
+            const int2 c = a.ctab[H];
+            // modelled wave instructions of each candidate (planner.cpp seg_cost)
+            const int bc0 = c.x & 0xff, nb0 = (c.x >> 8) & 0xff, bc1 = c.y & 0xff, nb1 = (c.y >> 8) & 0xff;
+            const float k0 = float((long long)nb0 * (13 * bc0 + 26) * (R + nb0 - 1)) * a.waste[nb0];
+            const float k1 = float((long long)nb1 * (13 * bc1 + 26) * (R + nb1 - 1)) * a.waste[nb1];
+            const int g = k1 < k0 ? (c.y >> 16) : (c.x >> 16);
+            const int bin = g * a.rspan + ((a.rmax - R) >> a.rshift);
+            a.bin_of[p] = bin;
+            atomicAdd(&a.hist[bin], 1);
+        }
+    }
+}
+
+// One workgroup: exclusive scan of the bins (bin starts = slot cursors), then
+// per group its first slot, its pair count and its first wave (waves of
+// floor(64 / nb) pairs), and the plan's wave count.
+__global__ __launch_bounds__(1024) void flat_scan_kernel(FlatPlanArgs a)
+{
+    __shared__ int part[1024];
+    const int t = threadIdx.x;
+    const int nbins = a.nbins;
+    const int C = (nbins + 1023) / 1024;
+    const int b0 = min(nbins, t * C), b1 = min(nbins, b0 + C);
+    int s = 0;
+    for (int i = b0; i < b1; ++i) s += a.hist[i];
+    part[t] = s;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    const int total = part[1023];
+    int run = part[t] - s;
+    for (int i = b0; i < b1; ++i) {
+        const int c = a.hist[i];
+        a.hist[i] = run;
+        run += c;
+    }
+    __syncthreads();
+    // groups (at most 1024: the host planner takes batches with more)
+    int wc = 0, first = 0, cnt = 0;
+    if (t < a.ngroups) {
+        first = a.hist[t * a.rspan];
+        const int end = t + 1 < a.ngroups ? a.hist[(t + 1) * a.rspan] : total;
+        cnt = end - first;
+        const int per = 64 / a.groups[t].y;
+        wc = (cnt + per - 1) / per;
+    }
+    __syncthreads();
+    part[t] = wc;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    if (t < a.ngroups) {
+        a.gtab[3 * t] = first;
+        a.gtab[3 * t + 1] = cnt;
+        a.gtab[3 * t + 2] = part[t] - wc;
+    }
+    if (t == 0) *a.nwaves = part[1023];
+}
+
+// Thread per pair: its slot (order inside a bin is arbitrary: a pair's result
+// does not depend on where it runs).
+__global__ __launch_bounds__(256) void flat_scatter_kernel(FlatPlanArgs a)
+{
+    for (int p = blockIdx.x * 256 + threadIdx.x; p < a.n; p += gridDim.x * 256) {
+        const int pos = atomicAdd(&a.hist[a.bin_of[p]], 1);
+        a.order[pos] = p;
+    }
+}
+
+// Thread per wave: its group by binary search over the groups' first waves,
+// its slots, and its row bounds from its pairs.
+__global__ __launch_bounds__(256) void flat_waves_kernel(FlatPlanArgs a)
+{
+    const int nw = *a.nwaves;
+    for (int w = blockIdx.x * 256 + threadIdx.x; w < nw; w += gridDim.x * 256) {
+        int lo = 0, hi = a.ngroups;   // the last group whose first wave is <= w
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (a.gtab[3 * mid + 2] <= w) lo = mid;
+            else hi = mid;
+        }
+        const int2 g = a.groups[lo];
+        const int per = 64 / g.y;
+        const int s0 = a.gtab[3 * lo] + (w - a.gtab[3 * lo + 2]) * per;
+        const int s1 = min(a.gtab[3 * lo] + a.gtab[3 * lo + 1], s0 + per);
+        int rmax = 0, rmin = 0x7fffffff;
+        for (int s = s0; s < s1; ++s) {
+            const int R = a.pairs[a.order[s]].y;
+            rmax = max(rmax, R);
+            rmin = min(rmin, R);
+        }
+        LaneWave v;
+        v.slot0 = s0;
+        v.rmax = rmax;
+        v.rmin = rmin;
+        v.ncols = g.x;
+        v.npairs = s1 - s0;
+        v.nsteps = rmax + g.y - 1;
+        v.carry_row = 0;
+        a.waves[w] = v;
+    }
 }
 
 int grid_for(long long waves)
@@ -244,6 +399,20 @@ hipError_t launch_prepare_grid(const GridPrepArgs& a, hipStream_t s)
     const long long items = std::max<long long>({(long long)a.nreads, (long long)a.nhaps, a.npairs / 64, a.nslots / 64, 1});
     const int grid = grid_for(items);
     hipLaunchKernelGGL(prepare_grid_kernel, dim3(grid), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_flat_plan(const FlatPlanArgs& a, hipStream_t s)
+{
+    if (a.n <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(a.hist, 0, sizeof(int) * size_t(a.nbins), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(flat_prep_kernel, dim3(grid_for(a.n)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(flat_scan_kernel, dim3(1), dim3(1024), 0, s, a);
+    const int gs = std::min(8192, (a.n + 255) / 256);
+    hipLaunchKernelGGL(flat_scatter_kernel, dim3(gs), dim3(256), 0, s, a);
+    const int gw = std::max(1, std::min(8192, (a.max_waves + 255) / 256));
+    hipLaunchKernelGGL(flat_waves_kernel, dim3(gw), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

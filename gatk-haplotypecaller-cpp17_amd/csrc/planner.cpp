@@ -12,6 +12,7 @@
 
 #include "engine_core.hpp"
 #include "luts.hpp"
+#include "plan_model.hpp"
 #include "pool.hpp"
 
 namespace hcphmm {
@@ -189,13 +190,6 @@ struct Local {
     }
 };
 
-// A hap's two segmented-wave candidates: nb0 = ceil(H / cap) lanes or one more,
-// each with the narrowest compiled width covering H.
-struct Cand {
-    uint8_t bc[2], nb[2];
-};
-static_assert(sizeof(Cand) == sizeof(uint32_t), "Cand packs into a word");
-
 // A structured plan's segment tables for the device (launch_grid_waves).
 struct GridDev {
     std::vector<GridSeg> segs;
@@ -228,13 +222,6 @@ void grow(std::vector<T>& v, size_t n)
     if (v.size() < n) v.resize(n);
 }
 
-
-// Modelled wave instructions of nb lanes of bc columns over R rows: 13 per
-// column + 26 per step, R + nb - 1 steps, times the lane-waste weight.
-inline float seg_cost(int nb, int bc, int R, const float* waste)
-{
-    return float(nb * (13 * bc + 26) * (R + nb - 1)) * waste[nb];
-}
 
 // Cross-product fast path of the planner (regions: hc_phmm_cross,
 // cross_regions, submit_regions) when every hap takes segmented waves. The
@@ -501,25 +488,15 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const int pol = kernel_policy();
     const bool use_lane = pol != 2;
     const int seg_max_h = lane_seg_policy() == 0 ? 0 : 64 * kSegMaxBC;
-    constexpr int kNCaps = 7;
-    constexpr int kCaps[kNCaps] = {64, 48, 32, 24, 16, 12, 8};
     // class: 0 seg, 1 one-lane, 2 diag W16, 3 diag W64
     grow(S.hcls, size_t(nh));
     uint8_t* hcls = S.hcls.data();
-    std::array<std::atomic<int64_t>, kNCaps> lanes_at{};
-    for (auto& x : lanes_at) x = 0;
     std::atomic<int64_t> wide_a{0};
     std::atomic<int> hmax_a{0};
-    // seg_width_ceil as a table (the planner calls it per hap and cap).
-    static const std::array<int8_t, kSegMaxBC + 1> kWidthCeil = [] {
-        std::array<int8_t, kSegMaxBC + 1> t{};
-        for (int x = 0; x <= kSegMaxBC; ++x) t[size_t(x)] = int8_t(seg_width_ceil(x));
-        return t;
-    }();
-    // Modelled wave instructions at each cap (13 per column + ~30 per step,
-    // R + nb - 1 steps at the batch's mean read length), for the cap choice.
+    // Modelled wave instructions at each cap (plan_model.hpp), for the cap choice.
     const double ravg = double(nrows) / double(std::max<int64_t>(nr, 1));
     std::mutex work_mu;
+    std::array<int64_t, kNCaps> lanes_at{};
     std::array<double, kNCaps> work_at{};
     // The cap model needs only totals: past 8k haps it prices every stride-th
     // hap (weighted by the stride), which is all the cap choice can resolve.
@@ -551,80 +528,27 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         for (int64_t i = lo; i < hi; ++i) {
             const int64_t h = i * cap_stride;
             if (hcls[size_t(h)] != 0) continue;
-            const int H = hlen[size_t(h)];
-            const int64_t m = cap_stride * loc.hap_mult(h);
-            for (int q = 0; q < kNCaps; ++q) {
-                const int nbq = std::min(64, (H + kCaps[q] - 1) / kCaps[q]);
-                const int bc = kWidthCeil[size_t(std::min(kSegMaxBC, (H + nbq - 1) / nbq))];
-                const int nb = (H + bc - 1) / bc;
-                lanes[q] += m * nb;
-                work[q] += double(m) * nb * (ravg + nb - 1) * (13.0 * bc + 30.0);
-            }
+            cap_sample(hlen[size_t(h)], ravg, cap_stride * loc.hap_mult(h), lanes, work);
         }
-        for (int q = 0; q < kNCaps; ++q) lanes_at[q] += lanes[q];
         std::lock_guard<std::mutex> lk(work_mu);
-        for (int q = 0; q < kNCaps; ++q) work_at[size_t(q)] += work[q];
+        for (int q = 0; q < kNCaps; ++q) {
+            lanes_at[size_t(q)] += lanes[q];
+            work_at[size_t(q)] += work[q];
+        }
     }, 4096);
     tm.mark("hap classes: cost");
-    int cap = kSegMaxBC;
-    bool few_waves = false;   // the pass gives each SIMD at most ~3 waves: latency-bound, prefer more lanes
+    CapChoice cc = choose_cap(lanes_at.data(), work_at.data(), dv.n_cu);
     {
         const int64_t forced = env_i64("HC_PHMM_SEG_CAP", 0);
-        if (forced > 0) {
-            cap = int(std::max<int64_t>(kSegMinBC, std::min<int64_t>(kSegMaxBC, forced)));
-        } else if (lanes_at[0].load() > 0) {
-            const double simds = 4.0 * dv.n_cu;
-            double best = 0;
-            for (int c = 0; c < kNCaps; ++c) {
-                const double waves = double(lanes_at[c].load()) / 60.0;   // ~60 of 64 lanes filled
-                // Up to two rounds of resident waves (3 per SIMD): the SIMD with
-                // the most waves sets the time, its last round issuing at half
-                // rate if it holds one wave (n waves: 3 floor(n/3) + {0, 2, 2}).
-                // More rounds: waves start as slots free up, so the pass time
-                // follows the total work (a ceil() there once picked cap 48 for
-                // a 415 x 128 region: 1.05 ms vs 0.94 at cap 64).
-                const double per_simd = waves / simds;
-                double rounds = per_simd;
-                if (per_simd <= 6.0) {
-                    const int n = std::max(1, int(std::ceil(per_simd - 1e-9)));
-                    rounds = 3.0 * (n / 3) + (n % 3 ? 2.0 : 0.0);
-                }
-                const double est = rounds * work_at[size_t(c)] / 60.0 / waves;
-                if (c == 0 || est < best * 0.98) {
-                    best = est;
-                    cap = kCaps[c];
-                    few_waves = waves <= 3.0 * simds;
-                }
-            }
-        }
+        if (forced > 0) cc = CapChoice{int(std::max<int64_t>(kSegMinBC, std::min<int64_t>(kSegMaxBC, forced))), false};
     }
-    static const std::array<float, 65> kHalfWaste = [] {
-        std::array<float, 65> f{};
-        for (int nb = 1; nb <= 64; ++nb) f[size_t(nb)] = std::sqrt(64.f / float((64 / nb) * nb));
-        return f;
-    }();
+    const int cap = cc.cap;
     // A pass with few waves per SIMD is latency-bound: its time is one wave's,
     // so the candidate with the shorter wave wins there (S1: 11 lanes of 14
     // columns beat 10 of 16; S1w: 12 of 22 beat 11 of 24).
-    static const std::array<float, 65> kPerLane = [] {
-        std::array<float, 65> f{};
-        for (int nb = 1; nb <= 64; ++nb) f[size_t(nb)] = 1.f / float(nb);
-        return f;
-    }();
-    const float* waste = few_waves ? kPerLane.data() : kHalfWaste.data();
+    const float* waste = cc.few_waves ? waste_per_lane() : waste_half();
     grow(S.hcand, size_t(nh));
     Cand* hcand = reinterpret_cast<Cand*>(S.hcand.data());
-    auto cand_of = [&](int H) {
-        const int nb0 = std::min(64, (H + cap - 1) / cap);
-        Cand c{};
-        for (int q = 0; q < 2; ++q) {
-            const int nb = std::min(nb0 + q, 64);
-            const int bc = kWidthCeil[size_t(std::min(kSegMaxBC, (H + nb - 1) / nb))];
-            c.bc[q] = uint8_t(bc);
-            c.nb[q] = uint8_t((H + bc - 1) / bc);
-        }
-        return c;
-    };
     // Many haps (flat batches: one per pair): the candidates by H from a table
     // (divisions once per length, not per hap).
     const int hmax_seg = std::min(hmax_a.load(), seg_max_h);
@@ -632,13 +556,13 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const bool by_table = nh > 4 * int64_t(hmax_seg + 1);
     if (by_table) {
         ctab.resize(size_t(hmax_seg) + 1);
-        for (int H = 1; H <= hmax_seg; ++H) ctab[size_t(H)] = cand_of(H);
+        for (int H = 1; H <= hmax_seg; ++H) ctab[size_t(H)] = cand_of(H, cap);
     }
     parallel_for(nh, [&](int64_t lo, int64_t hi) {
         for (int64_t h = lo; h < hi; ++h) {
             if (hcls[size_t(h)] != 0) continue;
             const int H = hlen[size_t(h)];
-            hcand[size_t(h)] = by_table ? ctab[size_t(H)] : cand_of(H);
+            hcand[size_t(h)] = by_table ? ctab[size_t(H)] : cand_of(H, cap);
         }
     }, 1 << 14);
     tm.mark("hap classes");
@@ -709,10 +633,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
                     // wave of such pairs alone (floor(64 / nb) groups): uniform
                     // batches pack like that, mixed ones fill the gaps with others;
                     // with few waves, the wave's own time (per lane)
-                    auto cost = [&](int q) {
-                        const int nb = cd.nb[q];
-                        return float(nb * (13 * cd.bc[q] + 26) * (R + nb - 1)) * waste[nb];
-                    };
+                    auto cost = [&](int q) { return seg_cost(cd.nb[q], cd.bc[q], R, waste); };
                     const int q = qforce >= 0 ? qforce : cost(1) < cost(0) ? 1 : 0;
                     bco[k] = cd.bc[q];
                     nbo[k] = cd.nb[q];
@@ -1028,7 +949,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const size_t o_hapw = L.take(sizeof(uint32_t) * (size_t(hap_w[size_t(nh)]) + 16));
     const size_t o_res = L.take(res_bytes);
     const size_t o_list = L.take(sizeof(int) * n1);
-    const size_t o_count = L.take(4 * sizeof(int));   // rescue list counters, in-wave rescue counters (by run parity)
+    const size_t o_count = L.take(kNumCounters * sizeof(int));   // run counters (kernels.hpp kNumCounters)
     const size_t o_sorted = L.take(sizeof(int) * n1);
     const size_t o_big = L.take(sizeof(int) * n1);
     const size_t o_bigc = L.take(sizeof(int));
@@ -1150,7 +1071,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             HIP_TRY(hipEventRecord(b->pack_ev[1], s));
         } else {
             HIP_TRY(hipMemcpyAsync(dev + up0, host + up0, upload - up0, hipMemcpyHostToDevice, s));
-            HIP_TRY(hipMemsetAsync(b->d_count, 0, 4 * sizeof(int), s));
+            HIP_TRY(hipMemsetAsync(b->d_count, 0, kNumCounters * sizeof(int), s));
             HIP_TRY(hipEventRecord(b->pack_ev[0], s));
             HIP_TRY(launch_pack_reads(reinterpret_cast<const uint8_t*>(dev + o_bases),
                                       reinterpret_cast<const uint8_t*>(dev + o_quals),

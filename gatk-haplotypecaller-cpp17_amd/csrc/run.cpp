@@ -30,6 +30,21 @@ int run_part(Part* b, hipStream_t s)
     const int par = b->parity;
     b->parity ^= 1;
     int* count = b->d_count + par;
+    Seg64Args r{};
+    r.pairs = b->d_pairs;
+    r.rows = b->d_rows;
+    r.hapw = b->d_hapw;
+    r.lut = dv.lut_d;
+    r.list = b->d_list;
+    r.count = count;
+    r.count_reset = b->d_count + (par ^ 1);
+    r.inker_reset = b->d_count + 2 + (par ^ 1);
+    r.sorted = b->d_sorted;
+    r.big = b->d_big;
+    r.big_count = b->d_big_count;
+    r.plan = b->d_plan;
+    r.raw_out = b->d_raw64;
+    r.min_lanes = int64_t(2) * 4 * dv.n_cu * 64;
     if (b->n_lane > 0) {
         LaneArgs a{};
         a.pairs = b->d_pairs;
@@ -121,22 +136,9 @@ int run_part(Part* b, hipStream_t s)
         // fp64 rescue (intel_pairhmm.hpp:137-139) over the device-built list, no
         // host round trip for its length: device planning + column-segmented
         // fp64 waves (grid-stride), then the anti-diagonal fp64 kernel for haps
-        // wider than 64 blocks of 32 (only launched if the batch has any).
-        Seg64Args r{};
-        r.pairs = b->d_pairs;
-        r.rows = b->d_rows;
-        r.hapw = b->d_hapw;
-        r.lut = dv.lut_d;
-        r.list = b->d_list;
-        r.count = count;
-        r.count_reset = b->d_count + (par ^ 1);
-        r.inker_reset = b->d_count + 2 + (par ^ 1);
-        r.sorted = b->d_sorted;
-        r.big = b->d_big;
-        r.big_count = b->d_big_count;
-        r.plan = b->d_plan;
-        r.raw_out = b->d_raw64;
-        r.min_lanes = int64_t(2) * 4 * dv.n_cu * 64;
+        // wider than 64 blocks of 32 (only launched if the batch has any). (The
+        // plan folded into the fp32 pass's last workgroup measured slower on S1:
+        // fp32 0.068 -> 0.075 ms for 2 us saved, the per-workgroup fences.)
         const int grid = int(std::min<int64_t>((b->n + 3) / 4, int64_t(2) * dv.n_cu));
         HIP_TRY(launch_rescue_seg64(r, grid, s));
         if (b->n_wide > 0) {

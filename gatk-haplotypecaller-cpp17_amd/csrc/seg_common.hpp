@@ -1,7 +1,7 @@
 // Device building blocks shared by the column-segmented PairHMM kernels
-// (lane_kernel.hip: phmm_seg_kernel, phmm_seg64_kernel, the one-lane kernel;
-// chain_kernel.hip: phmm_chain_kernel): the cell update in the reference's
-// operation order, the per-row constants, DPP hand-offs, prefetch depth.
+// (lane_kernel.hip: phmm_seg_kernel, phmm_seg64_kernel, the one-lane kernel):
+// the cell update in the reference's operation order, the per-row constants,
+// DPP hand-offs, prefetch depth.
 // Same semantics as compute_full_prob_avx{s,d} (avx-pairhmm-template.h:210-346).
 #pragma once
 #include <type_traits>
@@ -178,13 +178,9 @@ struct SegSteps {
 // lone step of a narrow block is too short to cover a global load, so narrow
 // blocks prefetch deeper; the step loop is unrolled by PD so every word lands
 // in its own register and is not touched (no wait) until its step.
-#ifndef HC_SEG_DEEP
-#define HC_SEG_DEEP 1   // 0: one-step prefetch everywhere, prior tables read from global memory (A/B builds)
-#endif
 template <typename T, int BC>
 constexpr int seg_prefetch()
 {
-    if (!HC_SEG_DEEP) return 1;
     return sizeof(T) == 8 ? (BC >= 16 ? 1 : 2) : (BC >= 32 ? 1 : (BC >= 16 ? 2 : 4));
 }
 
@@ -208,18 +204,12 @@ __device__ __forceinline__ void load_slut(T* __restrict__ slut, const T* __restr
     __syncthreads();
 }
 
-// Block widths of fp32 column-segmented waves (LaneWave.ncols of a seg wave).
-#ifndef HC_SEG_WIDTH_STEP2
-#define HC_SEG_WIDTH_STEP2 1   // 0: widths 16..64 in steps of 4 only (A/B builds)
-#endif
-#if HC_SEG_WIDTH_STEP2
+// Block widths of fp32 column-segmented waves (LaneWave.ncols of a seg wave):
+// 8..64 in steps of 2 (steps of 4 measured the same kernel time at a worse
+// column rounding; odd widths model only 0.6 % better).
 #define HC_SEG_WIDTHS(X)                                                                                       \
     X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(22) X(24) X(26) X(28) X(30) X(32) X(34) X(36) X(38) X(40) X(42) \
     X(44) X(46) X(48) X(50) X(52) X(54) X(56) X(58) X(60) X(62) X(64)
-#else
-#define HC_SEG_WIDTHS(X) \
-    X(8) X(10) X(12) X(14) X(16) X(20) X(24) X(28) X(32) X(36) X(40) X(44) X(48) X(52) X(56) X(60) X(64)
-#endif
 
 // A pair's nb column blocks of BC columns sit on nb consecutive lanes (a
 // "group"), lane s of the group owning columns s*BC+1 .. s*BC+BC on every row,
@@ -302,9 +292,8 @@ __device__ __forceinline__ void run_seg(const T* __restrict__ lut, const T* __re
             // Order the load after the last use of wn, so the word can land in
             // wn's register (no register move, hence no wait, at the loop back edge).
             asm volatile("" : "+v"(ridx) : "v"(qo), "v"(mo));
-            const T* __restrict__ pl = HC_SEG_DEEP ? slut : lut;
-            pm_n = pl[kOffPm + qo];
-            px_n = pl[kOffPx + qo];
+            pm_n = slut[kOffPm + qo];
+            px_n = slut[kOffPx + qo];
             m_n = mt[mo];
         } else {
             asm volatile("" : "+v"(ridx) : "v"(wn));

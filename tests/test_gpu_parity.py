@@ -12,14 +12,19 @@ pytestmark = pytest.mark.gpu
 # waves/SIMD, 1 = 64-col 2 waves, 2 = 32-col 4 waves);
 # "seg" = the default lane path: column-segmented waves (run_seg: a pair over
 # ceil(H/BC) lanes, BC per wave) for H <= 1024, one lane per pair above;
-# "segall" = every lane pair column-segmented (up to 64 lanes per pair).
-KERNELS = ["diag", "lane0", "lane1", "lane2", "seg", "segall"]
+# "segall" = every lane pair column-segmented (up to 64 lanes per pair);
+# "auto" = the defaults: flat calls planned on the device (flat_plan.cpp),
+# prepared batches on the host planner.
+KERNELS = ["diag", "lane0", "lane1", "lane2", "seg", "segall", "auto"]
 
 
 @pytest.fixture(params=KERNELS)
 def kernel(request, monkeypatch):
     """Force one fp32 kernel / lane-kernel variant for the test."""
-    if request.param == "diag":
+    if request.param == "auto":
+        for k in ("HC_PHMM_KERNEL", "HC_PHMM_LANE_SEG", "HC_PHMM_LANE_VARIANT", "HC_PHMM_FLAT_PLAN"):
+            monkeypatch.delenv(k, raising=False)
+    elif request.param == "diag":
         monkeypatch.setenv("HC_PHMM_KERNEL", "diag")
     elif request.param == "seg":
         monkeypatch.setenv("HC_PHMM_KERNEL", "lane")
@@ -319,3 +324,34 @@ def test_in_wave_rescue_cap(engine, oracle_lib, monkeypatch):
     assert_same(bt.results(), ref, "cap 1")
     assert bt.stats().n_rescued == int(ref["rescued"].sum()) > 2
     bt.close()
+
+
+@pytest.mark.parametrize("n", [1, 37, 125_000])
+def test_flat_device_planner_matches_host_planner(engine, oracle_lib, monkeypatch, n):
+    """Flat calls are planned on the device (pack, cost model, counting sort,
+    waves: flat_plan.cpp + pack_kernels.hip flat_*); the host planner
+    (HC_PHMM_FLAT_PLAN=0) must give the same bits, and a sample the oracle's."""
+    b = W.config("S2", n)
+    dev = engine.pairs(b)
+    monkeypatch.setenv("HC_PHMM_FLAT_PLAN", "0")
+    host = engine.pairs(b)
+    for k in dev:
+        assert np.array_equal(bits(dev[k]), bits(host[k])), k
+    idx = np.random.default_rng(9).choice(n, min(n, 2000), replace=False)
+    assert_same({k: dev[k][idx] for k in dev}, oracle_lib.pairs(W.subset(b, idx), nthreads=16), f"flat n={n}")
+
+
+def test_flat_device_planner_ragged_and_long(engine, oracle_lib):
+    """Device planning over a ragged mix: reads 1-600, haps 1-4096 (every
+    width and lane count, coarsened R bins), per-base gap qualities on a third
+    of the reads; and a batch with a hap past 4096 that the host planner takes."""
+    b = W.generate(4000, (1, 4096), (1, 600), 0.03, seed=77)
+    rng = np.random.default_rng(8)
+    rows = np.repeat(np.arange(4000) % 3 == 1, b["R"])
+    m = int(rows.sum())
+    b["ins"][rows] = rng.integers(33 + 5, 33 + 60, m, dtype=np.uint8)
+    b["dels"][rows] = rng.integers(33 + 5, 33 + 60, m, dtype=np.uint8)
+    b["gcp"][rows] = rng.integers(33 + 5, 33 + 30, m, dtype=np.uint8)
+    assert_same(engine.pairs(b), oracle_lib.pairs(b, nthreads=16), "ragged")
+    c = W.generate(300, (3000, 6000), (50, 200), 0.02, seed=78)
+    assert_same(engine.pairs(c), oracle_lib.pairs(c, nthreads=16), "long haps")

@@ -1,8 +1,25 @@
-import sys, time, os
-sys.path.insert(0, "gatk-haplotypecaller-cpp17_amd")
-import hcphmm, workloads as W
+"""S2 through the real call path (hc_phmm_pairs_flat: host buffers in, log10
+likelihoods out), a few calls; HC_PHMM_TRACE=1 prints the host phases."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gatk-haplotypecaller-cpp17_amd"))
+import numpy as np  # noqa: E402
+
+import hcphmm  # noqa: E402
+import workloads as W  # noqa: E402
+
+t0 = time.perf_counter()
 hcphmm.init(0)
-b = W.config("S2")
-for k in range(3):
-    t = time.perf_counter(); r = hcphmm.pairs(b); dt = time.perf_counter() - t
-    print(f"call {k}: {dt*1e3:.1f} ms  {W.cells(b)/dt/1e9:.1f} GCUPS", flush=True)
+print(f"init: {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
+b = W.config(sys.argv[1] if len(sys.argv) > 1 else "S2")
+cells = W.cells(b)
+ts = []
+for k in range(int(os.environ.get("REPS", "5"))):
+    t = time.perf_counter()
+    r = hcphmm.pairs(b)
+    dt = time.perf_counter() - t
+    ts.append(dt)
+    print(f"call {k}: {dt * 1e3:.1f} ms  {cells / dt / 1e9:.1f} GCUPS", flush=True)
+print(f"median of calls 1..: {np.median(ts[1:]) * 1e3:.2f} ms  {cells / np.median(ts[1:]) / 1e9:.1f} GCUPS")
