@@ -290,30 +290,36 @@ def end_to_end(hcphmm, W, batch, total_cells):
     kernels + D2H + host log10, the call cut into parts so the planning of part
     k+1 overlaps the device pass of part k). Median of 3 after a first call
     that sizes the workspaces."""
+    n = len(batch["R"])
+    outs = [hcphmm.result_arrays(n) for _ in range(2)]   # the caller's result buffers, reused
+    for o in outs:
+        for v in o.values():
+            v.fill(0)   # touched once, as a caller's long-lived buffers are
     t0 = time.perf_counter()
-    hcphmm.pairs(batch)
+    hcphmm.pairs(batch, outs[0])
     first = time.perf_counter() - t0
     reps = []
-    for _ in range(3):
+    for _ in range(5):
         t0 = time.perf_counter()
-        hcphmm.pairs(batch)
+        hcphmm.pairs(batch, outs[0])
         reps.append(time.perf_counter() - t0)
     e2e = float(np.median(reps))
     # Two calls in flight: submit the second before collecting the first (after
     # one such round that sizes the second set of workspaces).
-    for j in [hcphmm.submit_pairs(batch), hcphmm.submit_pairs(batch)]:
+    for j in [hcphmm.submit_pairs(batch, outs[0]), hcphmm.submit_pairs(batch, outs[1])]:
         j.collect()
     t0 = time.perf_counter()
-    j1 = hcphmm.submit_pairs(batch)
-    j2 = hcphmm.submit_pairs(batch)
+    j1 = hcphmm.submit_pairs(batch, outs[0])
+    j2 = hcphmm.submit_pairs(batch, outs[1])
     j1.collect()
     j2.collect()
     two = time.perf_counter() - t0
     return {"end_to_end_gcups": round(total_cells / e2e / 1e9, 2), "end_to_end_ms": round(e2e * 1e3, 2),
             "end_to_end_first_call_ms": round(first * 1e3, 2),
             "end_to_end_async_2calls_gcups": round(2 * total_cells / two / 1e9, 2),
-            "end_to_end_note": "hc_phmm_pairs_flat on host buffers (host planning, staging, H2D, device packing, "
-                               "kernels, D2H, host log10), median of 3; async: two submit_pairs in flight"}
+            "end_to_end_note": "hc_phmm_pairs_flat on host buffers (host staging of nibble-packed records, H2D, "
+                               "device packing + planning, kernels, D2H, host log10) into reused result "
+                               "buffers, median of 5; async: two submit_pairs in flight"}
 
 
 def region_calls(hcphmm, W, no_cpu):

@@ -286,6 +286,18 @@ void free_part(Part* p)
     --g_live_parts;
 }
 
+// A part that failed before it was handed out: its slot stays with the
+// caller (who returns it) and so does the slot's memory the part borrowed.
+void discard_part(Part* p)
+{
+    if (!p) return;
+    if (p->slot) {
+        p->dev_base = nullptr;
+        p->slot = nullptr;
+    }
+    free_part(p);
+}
+
 // Records of the last traced part (alive: read from the device; freed: the copy
 // saved at free_part).
 int timeline_records(unsigned long long* out, int max_waves)

@@ -235,6 +235,7 @@ struct Part {
     int* d_lane_order = nullptr;
     LaneWave* d_lane_waves = nullptr;
     float2* d_carry = nullptr;
+    void* d_ring = nullptr;        // anti-diagonal rings beyond the LDS (planner.cpp)
     PairDesc* d_pairs = nullptr;
     uint32_t* d_rows = nullptr;
     uint32_t* d_hapw = nullptr;
@@ -249,6 +250,7 @@ struct Part {
     size_t res_o64 = 0, res_ofl = 0;
     int* d_list = nullptr;
     int* d_sorted = nullptr;
+    int* d_worder = nullptr;      // fp64 pass: dispatch position -> wave
     int* d_big = nullptr;
     int* d_big_count = nullptr;
     Seg64Plan* d_plan = nullptr;
@@ -279,6 +281,7 @@ struct Part {
 
 Part* new_part(Device* d);   // counted in g_live_parts
 void free_part(Part* p);
+void discard_part(Part* p);  // failed before hand-out: the slot and its memory stay with the caller
 
 // planner.cpp: plan one part on device d (host planning + staging, then the
 // H2D, device packing and, with_run, the device pass and the D2H of the

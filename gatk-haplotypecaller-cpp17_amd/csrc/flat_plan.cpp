@@ -1,19 +1,26 @@
 // Flat calls (hc_phmm_pairs_flat / hc_phmm_submit_pairs: independent pairs in
 // the caller's host pools) planned on the device. The host does only what
 // needs the caller's memory, in two parallel passes over the pairs:
-//   pass 1  validate, gap-quality constancy (the reference's constant 'I'/'+'
-//           strings, sam.hpp:30-32, travel as three bytes per read), lengths
-//           and record sizes per mini-task, a sample of haplotype lengths for
-//           the width-cap model;
-//   pass 2  copy each pair's record (read bases, base qualities, gap planes
-//           only when they vary, hap bytes) and descriptor into the device's
-//           pinned staging ring, chunk by chunk, each chunk's H2D overlapping
-//           the fill of the next.
+//   pass 1  validate, lengths and record sizes per mini-task, a sample of
+//           haplotype lengths for the width-cap model (lengths only: 8 bytes
+//           per pair);
+//   pass 2  write each pair's record — base qualities, read and hap base codes
+//           as nibbles (1.5 bytes per read base, 0.5 per hap base instead of
+//           2 + 1), gap planes only when they vary — and descriptor into the
+//           device's pinned staging ring, chunk by chunk, each chunk's H2D
+//           overlapping the fill of the next. The gap qualities' constancy
+//           (the reference's constant 'I'/'+' strings, sam.hpp:30-32, travel
+//           as three bytes per read) is checked while filling; a part that
+//           turns out to hold a read with varying gap qualities is planned
+//           again with the check in pass 1, so its records carry the planes.
 // The device then packs rows and hap tables, chooses each pair's
 // column-segmented shape by the planner's cost model (plan_model.hpp), sorts
 // the pairs by (block width, lanes, R) and cuts the sorted runs into waves
 // (pack_kernels.hip flat_*), and runs the pass. No per-call pinned allocation.
+#include <immintrin.h>
+
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cstring>
 
@@ -53,7 +60,7 @@ void grow(std::vector<T>& v, size_t n)
 
 // Gap qualities of a read constant over its rows (blocks of 64 without early
 // exit inside a block, so the compiler vectorises the compare).
-bool constant_gaps(const uint8_t* i, const uint8_t* d, const uint8_t* c, int len)
+bool constant_gaps_scalar(const uint8_t* i, const uint8_t* d, const uint8_t* c, int len)
 {
     const uint8_t i0 = i[0], d0 = d[0], c0 = c[0];
     int k = 0;
@@ -67,6 +74,240 @@ bool constant_gaps(const uint8_t* i, const uint8_t* d, const uint8_t* c, int len
     return a == 0;
 }
 
+// The same, 32 bytes of each plane per step; the last step overlaps the one
+// before instead of a scalar tail.
+__attribute__((target("avx2"))) inline __m256i gap_diff32(const uint8_t* i, const uint8_t* d, const uint8_t* c,
+                                                           __m256i vi, __m256i vd, __m256i vc)
+{
+    const __m256i x = _mm256_xor_si256(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(i)), vi);
+    const __m256i y = _mm256_xor_si256(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(d)), vd);
+    const __m256i z = _mm256_xor_si256(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(c)), vc);
+    return _mm256_or_si256(_mm256_or_si256(x, y), z);
+}
+
+__attribute__((target("avx2"))) bool constant_gaps_avx2(const uint8_t* i, const uint8_t* d, const uint8_t* c,
+                                                        int len)
+{
+    if (len < 32) return constant_gaps_scalar(i, d, c, len);
+    const __m256i vi = _mm256_set1_epi8(char(i[0])), vd = _mm256_set1_epi8(char(d[0])),
+                  vc = _mm256_set1_epi8(char(c[0]));
+    __m256i acc = _mm256_setzero_si256();
+    int k = 0;
+    for (; k + 32 <= len; k += 32) acc = _mm256_or_si256(acc, gap_diff32(i + k, d + k, c + k, vi, vd, vc));
+    if (k < len) {
+        const int t = len - 32;
+        acc = _mm256_or_si256(acc, gap_diff32(i + t, d + t, c + t, vi, vd, vc));
+    }
+    return _mm256_testz_si256(acc, acc) != 0;
+}
+
+bool has_avx2()
+{
+    static const bool v = __builtin_cpu_supports("avx2");
+    return v;
+}
+
+bool constant_gaps(const uint8_t* i, const uint8_t* d, const uint8_t* c, int len)
+{
+    return has_avx2() ? constant_gaps_avx2(i, d, c, len) : constant_gaps_scalar(i, d, c, len);
+}
+
+constexpr int align4(int x) { return (x + 3) & ~3; }
+
+// Record of a pair (pack_kernels.hip flat_prep_kernel): qualities, read code
+// nibbles, [i, d, c planes], hap code nibbles, each field 4-byte aligned.
+inline int64_t record_bytes(int R, int H, bool planes)
+{
+    return align4(R) + align4((R + 1) / 2) + (planes ? 3 * int64_t(align4(R)) : 0) + align4((H + 1) / 2);
+}
+
+// ConvertChar (pairhmm_common.h:26-44): A0 C1 T2 G3 N4, every other byte -> 0.
+const std::array<uint8_t, 256>& code_table()
+{
+    static const std::array<uint8_t, 256> t = [] {
+        std::array<uint8_t, 256> x{};
+        x['C'] = 1;
+        x['T'] = 2;
+        x['G'] = 3;
+        x['N'] = 4;
+        return x;
+    }();
+    return t;
+}
+
+// Base codes of n bytes as nibbles, two per byte (byte k/2: code k in the low
+// nibble when k is even).
+void pack_nibbles_scalar(const uint8_t* __restrict s, int n, uint8_t* __restrict d)
+{
+    const auto& ct = code_table();
+    int k = 0;
+    for (; k + 1 < n; k += 2) d[k >> 1] = uint8_t(ct[s[k]] | ct[s[k + 1]] << 4);
+    if (k < n) d[k >> 1] = ct[s[k]];
+}
+
+__attribute__((target("avx2"))) inline __m256i codes32(__m256i v)
+{
+    const __m256i kC = _mm256_set1_epi8('C'), kT = _mm256_set1_epi8('T'), kG = _mm256_set1_epi8('G'),
+                  kN = _mm256_set1_epi8('N');
+    return _mm256_or_si256(
+        _mm256_or_si256(_mm256_and_si256(_mm256_cmpeq_epi8(v, kC), _mm256_set1_epi8(1)),
+                        _mm256_and_si256(_mm256_cmpeq_epi8(v, kT), _mm256_set1_epi8(2))),
+        _mm256_or_si256(_mm256_and_si256(_mm256_cmpeq_epi8(v, kG), _mm256_set1_epi8(3)),
+                        _mm256_and_si256(_mm256_cmpeq_epi8(v, kN), _mm256_set1_epi8(4))));
+}
+
+// 32 bytes -> 16 nibble bytes.
+__attribute__((target("avx2"))) inline __m128i nibbles32(const uint8_t* s)
+{
+    const __m256i pairmul = _mm256_set1_epi16(0x1001);   // even byte * 1 + odd byte * 16
+    const __m256i p = _mm256_maddubs_epi16(codes32(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(s))), pairmul);
+    const __m256i pk = _mm256_permute4x64_epi64(_mm256_packus_epi16(p, p), 0xD8);
+    return _mm256_castsi256_si128(pk);
+}
+
+__attribute__((target("avx2"))) void pack_nibbles_avx2(const uint8_t* __restrict s, int n, uint8_t* __restrict d)
+{
+    if (n < 32) {
+        pack_nibbles_scalar(s, n, d);
+        return;
+    }
+    int k = 0;
+    for (; k + 32 <= n; k += 32) _mm_storeu_si128(reinterpret_cast<__m128i*>(d + (k >> 1)), nibbles32(s + k));
+    if (k < n) {
+        // the last 32 bytes from an even start, overlapping what is written
+        // (same values); an odd last byte beyond them alone
+        const int t = (n - 32) & ~1;
+        _mm_storeu_si128(reinterpret_cast<__m128i*>(d + (t >> 1)), nibbles32(s + t));
+        if (t + 32 < n) d[(n - 1) >> 1] = code_table()[s[n - 1]];
+    }
+}
+
+// Bytes copied 32 at a time, the last 32 overlapping (n >= 32), else memcpy.
+__attribute__((target("avx2"))) void copy_bytes_avx2(const uint8_t* __restrict s, int n, uint8_t* __restrict d)
+{
+    if (n < 32) {
+        std::memcpy(d, s, size_t(n));
+        return;
+    }
+    int k = 0;
+    for (; k + 32 <= n; k += 32)
+        _mm256_storeu_si256(reinterpret_cast<__m256i*>(d + k), _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + k)));
+    if (k < n)
+        _mm256_storeu_si256(reinterpret_cast<__m256i*>(d + n - 32),
+                            _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + n - 32)));
+}
+
+}  // namespace
+
+void copy_bytes(const uint8_t* s, int n, uint8_t* d)
+{
+    if (has_avx2())
+        copy_bytes_avx2(s, n, d);
+    else
+        std::memcpy(d, s, size_t(n));
+}
+
+void pack_nibbles(const uint8_t* s, int n, uint8_t* d)
+{
+    if (has_avx2())
+        pack_nibbles_avx2(s, n, d);
+    else
+        pack_nibbles_scalar(s, n, d);
+}
+
+namespace {
+
+// Pass 2 over mini-tasks [m0, m1): each pair's record at buf + (its offset
+// - r0) and its descriptor at dd[k - p0]. With scan_gaps false, a read whose
+// gap qualities vary sets `varying` (the part is planned again with planes).
+void fill_chunk(const Src& src, int64_t lo, int64_t n, int64_t m0, int64_t m1, const Mini* mini,
+                const int32_t* gapw, bool scan_gaps, char* buf, int64_t r0, FlatDesc* dd, int64_t p0,
+                std::atomic<bool>& varying)
+{
+    parallel_for(m1 - m0, [&](int64_t a, int64_t e) {
+        for (int64_t m = m0 + a; m < m0 + e; ++m) {
+            int64_t ro = mini[m].rec, rw = mini[m].rows, hw = mini[m].hapw;
+            const int64_t k1 = std::min(n, (m + 1) * kMini);
+            for (int64_t k = m * kMini; k < k1; ++k) {
+                const int64_t p = lo + k;
+                const int R = src.R[p], H = src.H[p];
+                const int64_t o = src.read_off[p];
+                int32_t g;
+                if (scan_gaps) {
+                    g = gapw[k];
+                } else {
+                    const uint8_t *ip = src.ins + o, *dp = src.del + o, *cp = src.gcp + o;
+                    if (!constant_gaps(ip, dp, cp, R)) {
+                        varying.store(true, std::memory_order_relaxed);
+                        return;
+                    }
+                    g = int32_t((ip[0] & 127) | ((dp[0] & 127) << 7) | ((cp[0] & 127) << 14));
+                }
+                const int qa = align4(R);
+                uint8_t* d = reinterpret_cast<uint8_t*>(buf + (ro - r0));
+                copy_bytes(src.q + o, R, d);
+                pack_nibbles(src.rs + o, R, d + qa);
+                size_t at = size_t(qa) + size_t(align4((R + 1) / 2));
+                if (g < 0) {
+                    std::memcpy(d + at, src.ins + o, size_t(R));
+                    std::memcpy(d + at + qa, src.del + o, size_t(R));
+                    std::memcpy(d + at + 2 * qa, src.gcp + o, size_t(R));
+                    at += 3 * size_t(qa);
+                }
+                pack_nibbles(src.hap + src.hap_off[p], H, d + at);
+                dd[k - p0] = FlatDesc{ro, int(rw), R, H, int(hw), g, 0};
+                ro += record_bytes(R, H, g < 0);
+                rw += qa;
+                hw += hap_table_words(H);
+            }
+        }
+    }, 1);
+}
+
+// Pass 1 over pairs [lo, lo + n): per mini-task sums and bounds; with
+// scan_gaps, each read's constant gap triple (or -1) in gapw; every stride-th
+// hap length in hsamp.
+void scan_pass(const Src& src, int64_t lo, int64_t n, bool scan_gaps, Mini* mini, int32_t* gapw, int32_t* hsamp,
+               int64_t stride)
+{
+    const int64_t nmini = (n + kMini - 1) / kMini;
+    parallel_for(nmini, [&](int64_t m0, int64_t m1) {
+        for (int64_t m = m0; m < m1; ++m) {
+            Mini& M = mini[m];
+            const int64_t a = m * kMini, e = std::min(n, a + kMini);
+            for (int64_t k = a; k < e; ++k) {
+                const int64_t p = lo + k;
+                const int R = src.R[p], H = src.H[p];
+                if (R <= 0 || R > HC_PHMM_MAX_READ_LEN || H <= 0 || H > HC_PHMM_MAX_HAP_LEN) {
+                    M.bad = true;
+                    gapw[k] = 0;
+                    continue;
+                }
+                int32_t g = 0;
+                if (scan_gaps) {
+                    const int64_t o = src.read_off[p];
+                    const uint8_t *ip = src.ins + o, *dp = src.del + o, *cp = src.gcp + o;
+                    g = constant_gaps(ip, dp, cp, R)
+                            ? int32_t((ip[0] & 127) | ((dp[0] & 127) << 7) | ((cp[0] & 127) << 14))
+                            : -1;
+                    gapw[k] = g;
+                }
+                M.rec += record_bytes(R, H, g < 0);
+                M.rows += align4(R);
+                M.hapw += hap_table_words(H);
+                M.rmax = std::max(M.rmax, R);
+                M.rmin = std::min(M.rmin, R);
+                M.hmax = std::max(M.hmax, H);
+                M.hmin = std::min(M.hmin, H);
+                M.nwide += H > 64 * 32;
+                if (k % stride == 0) hsamp[k / stride] = H;
+            }
+        }
+    }, 8);
+}
+
+constexpr int kRetryWithPlanes = 1;   // plan_flat_try: a read's gap qualities vary
+
 bool default_policies()
 {
     for (const char* e : {"HC_PHMM_KERNEL", "HC_PHMM_LANE_SEG"}) {
@@ -79,10 +320,14 @@ bool default_policies()
 
 }  // namespace
 
-int plan_flat_device(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool with_run, Part** out)
+namespace {
+
+// One attempt: scan_gaps = false assumes constant gap qualities (checked in
+// pass 2; kRetryWithPlanes if one varies), true finds them in pass 1.
+int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool with_run, bool scan_gaps,
+                  Part** out)
 {
     *out = nullptr;
-    if (!spec.flat || !src.R || !slot || !default_policies()) return HC_PHMM_OK;
     PhaseTimer tm;
     const int64_t lo = spec.lo, n = spec.hi - spec.lo;
     if (n <= 0 || n > (int64_t(1) << 31) - 1) return HC_PHMM_OK;
@@ -97,37 +342,7 @@ int plan_flat_device(Device& dv, const Src& src, const PartSpec& spec, Slot* slo
     Mini* mini = S.mini.data();
     int32_t* hsamp = S.hsamp.data();
 
-    // Pass 1.
-    parallel_for(nmini, [&](int64_t m0, int64_t m1) {
-        for (int64_t m = m0; m < m1; ++m) {
-            Mini& M = mini[m];
-            const int64_t a = m * kMini, e = std::min(n, a + kMini);
-            for (int64_t k = a; k < e; ++k) {
-                const int64_t p = lo + k;
-                const int R = src.R[p], H = src.H[p];
-                if (R <= 0 || R > HC_PHMM_MAX_READ_LEN || H <= 0 || H > HC_PHMM_MAX_HAP_LEN) {
-                    M.bad = true;
-                    gapw[k] = 0;
-                    continue;
-                }
-                const int64_t o = src.read_off[p];
-                const uint8_t *ip = src.ins + o, *dp = src.del + o, *cp = src.gcp + o;
-                const int32_t g = constant_gaps(ip, dp, cp, R)
-                                      ? int32_t((ip[0] & 127) | ((dp[0] & 127) << 7) | ((cp[0] & 127) << 14))
-                                      : -1;
-                gapw[k] = g;
-                M.rec += 2 * int64_t(R) + (g < 0 ? 3 * int64_t(R) : 0) + H;
-                M.rows += R;
-                M.hapw += hap_table_words(H);
-                M.rmax = std::max(M.rmax, R);
-                M.rmin = std::min(M.rmin, R);
-                M.hmax = std::max(M.hmax, H);
-                M.hmin = std::min(M.hmin, H);
-                M.nwide += H > 64 * 32;
-                if (k % stride == 0) hsamp[k / stride] = H;
-            }
-        }
-    }, 8);
+    scan_pass(src, lo, n, scan_gaps, mini, gapw, hsamp, stride);
     tm.mark("flat: scan");
 
     int rmax = 0, rmin = INT32_MAX, hmax = 0, hmin = INT32_MAX;
@@ -159,7 +374,12 @@ int plan_flat_device(Device& dv, const Src& src, const PartSpec& spec, Slot* slo
     const double ravg = double(rows) / double(n);
     int64_t lanes_at[kNCaps] = {};
     double work_at[kNCaps] = {};
-    for (int64_t s = 0; s < nsamp; ++s) cap_sample(hsamp[s], ravg, stride, lanes_at, work_at);
+    {   // the model over the sample's distinct lengths, weighted by their counts
+        std::vector<int32_t> hist(size_t(std::min(hmax, 64 * kSegMaxBC)) + 1, 0);
+        for (int64_t s = 0; s < nsamp; ++s) ++hist[size_t(std::min(hsamp[s], 64 * kSegMaxBC))];
+        for (int H = 1; H < int(hist.size()); ++H)
+            if (hist[size_t(H)]) cap_sample(H, ravg, stride * hist[size_t(H)], lanes_at, work_at);
+    }
     const CapChoice cc = choose_cap(lanes_at, work_at, dv.n_cu);
     const float* waste = cc.few_waves ? waste_per_lane() : waste_full();
     std::vector<Cand> cand(size_t(hmax) + 1);
@@ -245,6 +465,7 @@ int plan_flat_device(Device& dv, const Src& src, const PartSpec& spec, Slot* slo
     const size_t o_list = L.take(sizeof(int) * n1);
     const size_t o_count = L.take(kNumCounters * sizeof(int));
     const size_t o_sorted = L.take(sizeof(int) * n1);
+    const size_t o_worder = L.take(sizeof(int) * n1);
     const size_t o_big = L.take(sizeof(int) * n1);
     const size_t o_bigc = L.take(sizeof(int));
     const size_t o_plan = L.take(sizeof(Seg64Plan));
@@ -298,6 +519,7 @@ int plan_flat_device(Device& dv, const Src& src, const PartSpec& spec, Slot* slo
     b->d_list = reinterpret_cast<int*>(dev + o_list);
     b->d_count = reinterpret_cast<int*>(dev + o_count);
     b->d_sorted = reinterpret_cast<int*>(dev + o_sorted);
+    b->d_worder = reinterpret_cast<int*>(dev + o_worder);
     b->d_big = reinterpret_cast<int*>(dev + o_big);
     b->d_big_count = reinterpret_cast<int*>(dev + o_bigc);
     b->d_plan = reinterpret_cast<Seg64Plan*>(dev + o_plan);
@@ -315,6 +537,7 @@ int plan_flat_device(Device& dv, const Src& src, const PartSpec& spec, Slot* slo
     b->upload_bytes = size_t(rec) + sizeof(FlatDesc) * n1 + tab_bytes;
     hipStream_t s = b->stream;
 
+    std::atomic<bool> varying{false};
     auto enqueue = [&]() -> int {
         // Pass 2: chunks through the ring, each H2D'd as soon as it is filled.
         {
@@ -329,33 +552,8 @@ int plan_flat_device(Device& dv, const Src& src, const PartSpec& spec, Slot* slo
                 char* buf = dv.ring.buf[ri];
                 const size_t dbase = (size_t(r1 - r0) + 255) & ~size_t(255);
                 FlatDesc* dd = reinterpret_cast<FlatDesc*>(buf + dbase);
-                parallel_for(m1 - m0, [&](int64_t a, int64_t e) {
-                    for (int64_t m = m0 + a; m < m0 + e; ++m) {
-                        int64_t ro = mini[m].rec, rw = mini[m].rows, hw = mini[m].hapw;
-                        const int64_t k1 = std::min(n, (m + 1) * kMini);
-                        for (int64_t k = m * kMini; k < k1; ++k) {
-                            const int64_t p = lo + k;
-                            const int R = src.R[p], H = src.H[p];
-                            const int32_t g = gapw[k];
-                            const int64_t o = src.read_off[p];
-                            uint8_t* d = reinterpret_cast<uint8_t*>(buf + (ro - r0));
-                            std::memcpy(d, src.rs + o, size_t(R));
-                            std::memcpy(d + R, src.q + o, size_t(R));
-                            size_t at = 2 * size_t(R);
-                            if (g < 0) {
-                                std::memcpy(d + at, src.ins + o, size_t(R));
-                                std::memcpy(d + at + R, src.del + o, size_t(R));
-                                std::memcpy(d + at + 2 * R, src.gcp + o, size_t(R));
-                                at += 3 * size_t(R);
-                            }
-                            std::memcpy(d + at, src.hap + src.hap_off[p], size_t(H));
-                            dd[k - p0] = FlatDesc{ro, int(rw), R, H, int(hw), g, 0};
-                            ro += int64_t(at) + H;
-                            rw += R;
-                            hw += hap_table_words(H);
-                        }
-                    }
-                }, 1);
+                fill_chunk(src, lo, n, m0, m1, mini, gapw, scan_gaps, buf, r0, dd, p0, varying);
+                if (varying.load()) return kRetryWithPlanes;
                 HIP_TRY(hipMemcpyAsync(dev + o_img + r0, buf, size_t(r1 - r0), hipMemcpyHostToDevice, s));
                 HIP_TRY(hipMemcpyAsync(dev + o_desc + sizeof(FlatDesc) * size_t(p0), dd,
                                        sizeof(FlatDesc) * size_t(p1 - p0), hipMemcpyHostToDevice, s));
@@ -402,13 +600,73 @@ int plan_flat_device(Device& dv, const Src& src, const PartSpec& spec, Slot* slo
     tm.mark("flat: enqueue");
     if (rc) {
         (void)hipStreamSynchronize(s);
-        b->slot = nullptr;   // the caller returns the slot
-        free_part(b);
+        discard_part(b);   // the caller returns the slot (and keeps its memory)
         return rc;
     }
     *out = b;
     return HC_PHMM_OK;
 }
 
+}  // namespace
+
+int plan_flat_device(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool with_run, Part** out)
+{
+    *out = nullptr;
+    if (!spec.flat || !src.R || !slot || !default_policies()) return HC_PHMM_OK;
+    int rc = plan_flat_try(dv, src, spec, slot, with_run, false, out);
+    if (rc == kRetryWithPlanes) rc = plan_flat_try(dv, src, spec, slot, with_run, true, out);
+    return rc;
+}
+
 }  // namespace eng
 }  // namespace hcphmm
+
+// Host-logic test hook (not part of the ABI): the record's nibble packing.
+extern "C" void hcx_pack_nibbles(const uint8_t* s, int n, uint8_t* d) { hcphmm::eng::pack_nibbles(s, n, d); }
+
+// Host-pass timing without a GPU (not part of the ABI: tools/flat_host_bench.py):
+// pass 1 and pass 2 of a flat call over pairs [0, n) into host memory, `reps`
+// times; ms[0] = pass 1, ms[1] = pass 2 (mean per call).
+extern "C" void hcx_flat_host_passes(int64_t n, const int64_t* read_off, const int32_t* R, const int64_t* hap_off,
+                                     const int32_t* H, const uint8_t* rs, const uint8_t* q, const uint8_t* ins,
+                                     const uint8_t* del, const uint8_t* gcp, const uint8_t* hap, int reps, double* ms)
+{
+    using namespace hcphmm;
+    using namespace hcphmm::eng;
+    Src src;
+    src.read_off = read_off;
+    src.R = R;
+    src.hap_off = hap_off;
+    src.H = H;
+    src.rs = rs;
+    src.q = q;
+    src.ins = ins;
+    src.del = del;
+    src.gcp = gcp;
+    src.hap = hap;
+    const int64_t nmini = (n + kMini - 1) / kMini;
+    std::vector<Mini> mini;
+    std::vector<int32_t> gapw(static_cast<size_t>(n)), hsamp(static_cast<size_t>(n));
+    std::vector<char> buf;
+    std::vector<FlatDesc> dd(static_cast<size_t>(n));
+    ms[0] = ms[1] = 0;
+    for (int r = 0; r <= reps; ++r) {   // rep 0 sizes the buffers (untimed)
+        auto t0 = std::chrono::steady_clock::now();
+        mini.assign(size_t(nmini), Mini{});
+        scan_pass(src, 0, n, false, mini.data(), gapw.data(), hsamp.data(), std::max<int64_t>(1, n / 8192));
+        int64_t rec = 0;
+        for (auto& M : mini) {
+            const int64_t x = M.rec;
+            M.rec = rec;
+            rec += x;
+        }
+        if (buf.size() < size_t(rec)) buf.resize(size_t(rec));
+        auto t1 = std::chrono::steady_clock::now();
+        std::atomic<bool> varying{false};
+        fill_chunk(src, 0, n, 0, nmini, mini.data(), gapw.data(), false, buf.data(), 0, dd.data(), 0, varying);
+        auto t2 = std::chrono::steady_clock::now();
+        if (r == 0) continue;
+        ms[0] += std::chrono::duration<double, std::milli>(t1 - t0).count() / reps;
+        ms[1] += std::chrono::duration<double, std::milli>(t2 - t1).count() / reps;
+    }
+}

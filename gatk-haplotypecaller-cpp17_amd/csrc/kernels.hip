@@ -160,7 +160,10 @@ __device__ __forceinline__ void run_stripe(
     }
 }
 
-template <typename T, int W>
+// GRING: the ring in global memory (a.ring_global, this workgroup's slice),
+// for haps too long for the LDS; a wave reads back only what it wrote itself,
+// in program order.
+template <typename T, int W, bool GRING>
 __global__ __launch_bounds__(64) void phmm_diag_kernel(DiagArgs a)
 {
     constexpr int G = 64 / W;
@@ -169,7 +172,8 @@ __global__ __launch_bounds__(64) void phmm_diag_kernel(DiagArgs a)
     const int g = lane / W, l = lane % W;
     const T* __restrict__ lut = static_cast<const T*>(a.lut);
     const T* __restrict__ ph2pr = lut + kOffPh2pr;
-    Pair2<T>* ring = reinterpret_cast<Pair2<T>*>(smem) + g * a.ring_len;
+    Pair2<T>* ring = GRING ? static_cast<Pair2<T>*>(a.ring_global) + (size_t(blockIdx.x) * G + g) * size_t(a.ring_len)
+                           : reinterpret_cast<Pair2<T>*>(smem) + g * a.ring_len;
     const int n = a.n_slots_dev ? *a.n_slots_dev : a.n_slots;
     if (a.count_reset && blockIdx.x == 0 && threadIdx.x == 0) *a.count_reset = 0;
 
@@ -245,10 +249,21 @@ template <typename T>
 hipError_t launch_diag(int W, const DiagArgs& a, int grid, hipStream_t s)
 {
     const size_t lds = diag_lds_bytes(W, a.ring_len, sizeof(T) == 8);
+    if (a.ring_global) {
+        grid = grid < kDiagRingBlocks ? grid : kDiagRingBlocks;
+        switch (W) {
+        case 16: hipLaunchKernelGGL((phmm_diag_kernel<T, 16, true>), dim3(grid), dim3(64), 0, s, a); break;
+        case 32: hipLaunchKernelGGL((phmm_diag_kernel<T, 32, true>), dim3(grid), dim3(64), 0, s, a); break;
+        case 64: hipLaunchKernelGGL((phmm_diag_kernel<T, 64, true>), dim3(grid), dim3(64), 0, s, a); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
+    if (lds > kDiagLdsMax) return hipErrorInvalidValue;
     switch (W) {
-    case 16: hipLaunchKernelGGL((phmm_diag_kernel<T, 16>), dim3(grid), dim3(64), lds, s, a); break;
-    case 32: hipLaunchKernelGGL((phmm_diag_kernel<T, 32>), dim3(grid), dim3(64), lds, s, a); break;
-    case 64: hipLaunchKernelGGL((phmm_diag_kernel<T, 64>), dim3(grid), dim3(64), lds, s, a); break;
+    case 16: hipLaunchKernelGGL((phmm_diag_kernel<T, 16, false>), dim3(grid), dim3(64), lds, s, a); break;
+    case 32: hipLaunchKernelGGL((phmm_diag_kernel<T, 32, false>), dim3(grid), dim3(64), lds, s, a); break;
+    case 64: hipLaunchKernelGGL((phmm_diag_kernel<T, 64, false>), dim3(grid), dim3(64), lds, s, a); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -277,7 +292,7 @@ hipError_t configure_kernels()
     hipError_t e = hipSuccess;
 #define HC_SET(T, W)                                                                        \
     if (e == hipSuccess)                                                                    \
-        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&phmm_diag_kernel<T, W>),     \
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&phmm_diag_kernel<T, W, false>), \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     HC_SET(float, 16) HC_SET(float, 32) HC_SET(float, 64)
     HC_SET(double, 16) HC_SET(double, 32) HC_SET(double, 64)

@@ -35,8 +35,10 @@ using PairDesc = int4;
 
 // Run counters of a part (zeroed when the part is prepared): [0, 1] rescue
 // list lengths and [2, 3] in-wave rescue counts, by run parity (a run zeroes
-// the other parity's for the next run: no memset per run).
-constexpr int kNumCounters = 4;
+// the other parity's for the next run: no memset per run); [4] the fp64
+// pass's wave counter (zeroed by its plan each run).
+constexpr int kNumCounters = 8;
+constexpr int kNextWave = 4;
 
 struct DiagArgs {
     const PairDesc* pairs;
@@ -55,6 +57,8 @@ struct DiagArgs {
                               // (the rescue pass overwrites the rescued ones)
     int* count_reset;         // fp64 pass: the other run parity's rescue counter,
                               // zeroed for the next run (no memset per run)
+    void* ring_global;        // stripe hand-off ring in global memory (block b: entries
+                              // [b * G * ring_len, ...)) when it exceeds the LDS; null = LDS
 };
 
 // fp64 rescue pass in column-segmented form, planned on the device
@@ -69,6 +73,7 @@ constexpr int kSeg64Classes = 7 * kSeg64Widths + 1;
 __host__ __device__ constexpr int seg64_width(int wi) { return 8 + 4 * wi; }
 struct Seg64Plan {
     int bc0;                        // block width bound of the pass (32, or 16 / 8 for short lists)
+    int dynamic;                    // waves fetched from a counter (more than two per SIMD)
     int n_class[kSeg64Classes];
     int off_class[kSeg64Classes];   // class c's entries in `sorted` start here
     int wave_base[kSeg64Classes];   // first wave of class c; [last] = total waves
@@ -88,6 +93,9 @@ struct Seg64Args {
     Seg64Plan* plan;
     double* raw_out;          // raw f64 sums by pair id
     long long min_lanes;      // narrower blocks below this many lanes at bc = 32
+    int* wave_order;          // dispatch position -> wave (n entries), see rescue_plan_kernel
+    int* next_wave;           // dynamic wave counter (zeroed by the plan)
+    int n_simd;               // SIMDs of the device (4 per CU)
 };
 // Lane-per-pair kernel (large batches): one lane owns one pair and sweeps it
 // row by row over register-resident blocks of kLaneBlock columns. A wave holds
@@ -155,6 +163,13 @@ hipError_t launch_rescue_seg64(const Seg64Args& a, int grid, hipStream_t s);
 hipError_t launch_diag_f32(int W, const DiagArgs& a, int grid, hipStream_t s);
 hipError_t launch_diag_f64(int W, const DiagArgs& a, int grid, hipStream_t s);
 size_t diag_lds_bytes(int W, int ring_len, bool f64);
+// The anti-diagonal kernel keeps a wave's stripe hand-off ring (H + 2W + 16
+// entries per pair) in LDS up to this size, in global memory beyond (haps
+// longer than ~9.9k bases in fp32, ~4.9k in fp64 at W = 64), with at most
+// kDiagRingBlocks workgroups, each looping over its share of the pairs.
+constexpr size_t kDiagLdsMax = size_t(152) * 1024;
+constexpr int kDiagRingBlocks = 1024;
+inline bool diag_ring_in_lds(int W, int ring_len, bool f64) { return diag_lds_bytes(W, ring_len, f64) <= kDiagLdsMax; }
 hipError_t configure_kernels();   // raise the dynamic-LDS limit once
 
 // Device packing (pack_kernels.hip). Reads: `bases` / `quals` one byte per
@@ -216,15 +231,16 @@ struct GridPrepArgs {
 hipError_t launch_prepare_grid(const GridPrepArgs& a, hipStream_t s);
 
 // Flat batches planned on the device (flat_plan.cpp, pack_kernels.hip): the
-// host uploads one record per pair — its read bases, base qualities, gap
-// qualities only when they vary, then its hap bytes — and a descriptor; the
-// device packs rows and hap tables, picks each pair's column-segmented shape
-// (the host planner's cost model, from per-length candidate tables), sorts the
-// pairs by (block width, lanes, R) with a counting sort and cuts the sorted
-// runs into waves of floor(64 / nb) pairs.
+// host uploads one record per pair — its base qualities, its base codes as
+// nibbles, its gap planes only when they vary, its hap codes as nibbles, each
+// field 4-byte aligned — and a descriptor; the device packs rows (4 per
+// lane) and hap tables (8 columns per lane), picks each pair's
+// column-segmented shape (the host planner's cost model, from per-length
+// candidate tables), sorts the pairs by (block width, lanes, R) with a
+// counting sort and cuts the sorted runs into waves of floor(64 / nb) pairs.
 struct FlatDesc {
-    long long rec;   // byte offset of the pair's record in the upload image
-    int row_off;     // first packed row of the read
+    long long rec;   // byte offset of the pair's record in the upload image (4-aligned)
+    int row_off;     // first packed row of the read (a multiple of 4)
     int R, H;
     int hapw_off;    // first word of the hap's match table
     int gapw;        // constant gap qualities i | d << 7 | c << 14, or -1 (planes in the record)

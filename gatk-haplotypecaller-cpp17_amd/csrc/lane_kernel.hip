@@ -209,11 +209,22 @@ __device__ __forceinline__ int rescue_class(int H, int bc0)
     return (6 - k) * kSeg64Widths + (kSeg64Widths - 1 - wi);
 }
 
+// Wave order of the pass. With at most two waves per SIMD (fp64 occupancy)
+// every wave is resident at once and the pass lasts as long as its busiest
+// SIMD: position p and p + n_simd share a SIMD (workgroups of four waves, the
+// first n_simd positions filling one slot per SIMD), so the heaviest waves go
+// first, in descending cost, and the rest after them in ascending cost — the
+// heaviest wave shares its SIMD with the lightest. With more, waves are
+// fetched from a counter in descending cost (greedy longest-first). Wave
+// cost: (rows + skew) steps x (14 ops per column + ~40 per step).
+constexpr int kMaxSortWaves = 8192;
+
 __global__ __launch_bounds__(1024) void rescue_plan_kernel(Seg64Args a)
 {
     constexpr int NC = kSeg64Classes;
-    __shared__ int cnt[NC], fill[NC];
+    __shared__ int cnt[NC], fill[NC], wbase[NC];
     __shared__ unsigned long long lanes_sh;
+    __shared__ unsigned long long key[kMaxSortWaves];
     const int n = *a.count;
     const int t = threadIdx.x;
     if (t < NC) cnt[t] = 0;
@@ -221,6 +232,7 @@ __global__ __launch_bounds__(1024) void rescue_plan_kernel(Seg64Args a)
         lanes_sh = 0;
         *a.count_reset = 0;
         *a.inker_reset = 0;
+        *a.next_wave = 0;
     }
     __syncthreads();
     // Width bound: 32 unless the lanes at width 32 give fewer than min_lanes
@@ -243,11 +255,13 @@ __global__ __launch_bounds__(1024) void rescue_plan_kernel(Seg64Args a)
             fill[c] = off;
             off += cnt[c];
             p.wave_base[c] = wb;
+            wbase[c] = wb;
             if (c < NC - 1) {
                 const int per = 64 >> (6 - c / kSeg64Widths);
                 wb += (cnt[c] + per - 1) / per;
             }
         }
+        p.dynamic = a.wave_order != nullptr && wb > 2 * a.n_simd;
         *a.plan = p;
         *a.big_count = cnt[NC - 1];
     }
@@ -260,6 +274,53 @@ __global__ __launch_bounds__(1024) void rescue_plan_kernel(Seg64Args a)
             a.sorted[pos] = pid;
         else
             a.big[pos - (n - cnt[NC - 1])] = pid;
+    }
+    __syncthreads();
+    const int W = wbase[NC - 1];   // segmented waves
+    if (W <= 1 || !a.wave_order) return;
+    if (W > kMaxSortWaves) {   // classes longest first, fetched in that order
+        for (int w = t; w < W; w += blockDim.x) a.wave_order[w] = w;
+        return;
+    }
+    // Cost of every wave, then a bitonic sort (descending) in LDS.
+    int N = 1;
+    while (N < W) N <<= 1;
+    for (int w = t; w < N; w += blockDim.x) {
+        unsigned long long k = 0;
+        if (w < W) {
+            int c = 0;
+            while (c + 1 < NC - 1 && wbase[c + 1] <= w) ++c;
+            const int kk = 6 - c / kSeg64Widths, per = 64 >> kk;
+            const int bc = seg64_width(kSeg64Widths - 1 - c % kSeg64Widths);
+            const int off = fill[c] - cnt[c];   // the class's first entry (fill ran past it)
+            const int e0 = off + (w - wbase[c]) * per;
+            const int e1 = min(off + cnt[c], e0 + per);
+            int rmax = 0;
+            for (int e = e0; e < e1; ++e) rmax = max(rmax, a.pairs[a.sorted[e]].y);
+            const unsigned cost = unsigned(rmax + (1 << kk) - 1) * unsigned(bc * 14 + 40);
+            k = ((unsigned long long)cost << 32) | unsigned(w);
+        }
+        key[w] = k;
+    }
+    __syncthreads();
+    for (int size = 2; size <= N; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = t; i < N / 2; i += blockDim.x) {
+                const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
+                const bool desc = (lo & size) == 0;
+                const unsigned long long x = key[lo], y = key[hi];
+                if ((x < y) == desc) {
+                    key[lo] = y;
+                    key[hi] = x;
+                }
+            }
+            __syncthreads();
+        }
+    const int S = a.n_simd;
+    for (int p = t; p < W; p += blockDim.x) {
+        // two waves per SIMD at most: positions S.. pair the heaviest with the lightest
+        const int r = (W <= 2 * S && p >= S) ? S + (W - 1 - p) : p;
+        a.wave_order[p] = int(key[r] & 0xffffffffu);
     }
 }
 
@@ -374,7 +435,15 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
     // Lane l holds the first wave of class l + 1: a wave's class is the number
     // of class starts at or below it (wave_base is non-decreasing).
     const int next_base = lane < kSeg64Classes - 1 ? p->wave_base[lane + 1] : INT32_MAX;
-    for (int w = blockIdx.x * 4 + (threadIdx.x >> 6); w < total; w += gridDim.x * 4) {
+    const bool dyn = __builtin_amdgcn_readfirstlane(p->dynamic) != 0;
+    for (int pos = blockIdx.x * 4 + (threadIdx.x >> 6);;) {
+        if (dyn) {   // greedy: the next wave in descending cost
+            int v = 0;
+            if (lane == 0) v = atomicAdd(a.next_wave, 1);
+            pos = __builtin_amdgcn_readfirstlane(v);
+        }
+        if (pos >= total) break;
+        const int w = (total > 1 && a.wave_order) ? __builtin_amdgcn_readfirstlane(a.wave_order[pos]) : pos;
         const int c = __popcll(__builtin_amdgcn_ballot_w64(next_base <= w));
         const int k = 6 - c / kSeg64Widths;
         const int bc = seg64_width(kSeg64Widths - 1 - c % kSeg64Widths);
@@ -405,6 +474,7 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
         }
         if (owner) a.raw_out[pid] = sumM + sumX;
         __builtin_amdgcn_wave_barrier();   // the next wave's match table reuses mt
+        if (!dyn) pos += gridDim.x * 4;
     }
 }
 

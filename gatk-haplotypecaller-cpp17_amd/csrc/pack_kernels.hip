@@ -217,6 +217,81 @@ __global__ __launch_bounds__(256) void prepare_grid_kernel(GridPrepArgs a)
 // ---------------------------------------------------------------------------
 // Flat batches planned on the device (kernels.hpp FlatPlanArgs).
 
+// Flat records (flat_plan.cpp, kernels.hpp FlatDesc): the read's base
+// qualities, its base codes as nibbles (ConvertChar, two per byte, row k in
+// the low nibble of byte k/2 when k is even), its i / d / c planes when they
+// vary, then the hap's base codes as nibbles; every field 4-byte aligned.
+__host__ __device__ constexpr int align4(int x) { return (x + 3) & ~3; }
+
+// Rows of one read from its record, four rows per lane (one 32-bit load of
+// qualities, one 16-bit load of codes, one 128-bit store).
+__device__ __forceinline__ void pack_read_rec(const uint8_t* __restrict__ quals, const uint8_t* __restrict__ codes,
+                                              const uint8_t* __restrict__ gaps, int R, int gw,
+                                              uint32_t* __restrict__ rows, int lane)
+{
+    const int qa = align4(R);
+    for (int t = lane; 4 * t < R; t += 64) {
+        const uint32_t q4 = reinterpret_cast<const uint32_t*>(quals)[t];
+        const uint32_t c4 = reinterpret_cast<const uint16_t*>(codes)[t];
+        uint32_t w[4];
+        if (gw >= 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                w[j] = ((q4 >> (8 * j)) & 127u) | (uint32_t(gw) << 7) | (((c4 >> (4 * j)) & 15u) << 28);
+            if (t == 0) w[0] |= 0x80000000u;   // constant-gap tag on the read's first row
+        } else {
+            const uint32_t i4 = reinterpret_cast<const uint32_t*>(gaps)[t];
+            const uint32_t d4 = reinterpret_cast<const uint32_t*>(gaps + qa)[t];
+            const uint32_t g4 = reinterpret_cast<const uint32_t*>(gaps + 2 * qa)[t];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                w[j] = ((q4 >> (8 * j)) & 127u) | (((i4 >> (8 * j)) & 127u) << 7) | (((d4 >> (8 * j)) & 127u) << 14) |
+                       (((g4 >> (8 * j)) & 127u) << 21) | (((c4 >> (4 * j)) & 15u) << 28);
+        }
+        reinterpret_cast<uint4*>(rows)[t] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+// Nibbles equal to zero (values <= 7): bit 0 of each such nibble.
+__device__ __forceinline__ uint32_t zero_nibbles(uint32_t t) { return ~(t | (t >> 1) | (t >> 2)) & 0x11111111u; }
+
+// Match table of one hap from its code nibbles: a lane takes 8 columns (one
+// 32-bit load), forms for each read code the 8 match bits (MSB first), and
+// each quad of lanes joins its four bytes into one table word (DPP
+// quad_perm): 512 columns per wave step.
+__device__ __forceinline__ void hap_table_rec(const uint8_t* __restrict__ hc, int H, uint32_t* __restrict__ o, int lane)
+{
+    const int nw = (H + 31) / 32;
+    if (lane < 5 * kHapLead) o[lane] = 0u;
+    if (lane < 5) o[(kHapLead + nw) * 5 + lane] = 0u;
+    const uint32_t* __restrict__ h32 = reinterpret_cast<const uint32_t*>(hc);
+    for (int base = 0; base < H; base += 512) {
+        const int col0 = base + 8 * lane;
+        const int nv = H - col0;   // valid columns of this lane (<= 0: none)
+        const uint32_t x = nv > 0 ? h32[base / 8 + lane] : 0u;
+        const uint32_t vmask = nv >= 8 ? 0x11111111u : (nv > 0 ? 0x11111111u & ((1u << (4 * nv)) - 1u) : 0u);
+        const uint32_t isN = zero_nibbles(x ^ 0x44444444u);
+        uint32_t word[5];
+#pragma unroll
+        for (int rc = 0; rc < 5; ++rc) {
+            // read code rc matches: equal code, hap 'N' (matches every rc), or read 'N'
+            const uint32_t eq = (rc == 4 ? 0x11111111u : (zero_nibbles(x ^ (uint32_t(rc) * 0x11111111u)) | isN)) & vmask;
+            uint32_t m = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) m |= ((eq >> (4 * j)) & 1u) << (7 - j);
+            const uint32_t m1 = __builtin_amdgcn_mov_dpp(int(m), 0x55, 0xf, 0xf, false);   // quad_perm [1,1,1,1]
+            const uint32_t m2 = __builtin_amdgcn_mov_dpp(int(m), 0xaa, 0xf, 0xf, false);   // quad_perm [2,2,2,2]
+            const uint32_t m3 = __builtin_amdgcn_mov_dpp(int(m), 0xff, 0xf, 0xf, false);   // quad_perm [3,3,3,3]
+            word[rc] = (m << 24) | (m1 << 16) | (m2 << 8) | m3;
+        }
+        const int w = base / 32 + (lane >> 2);
+        if ((lane & 3) == 0 && w < nw) {
+#pragma unroll
+            for (int rc = 0; rc < 5; ++rc) o[(kHapLead + w) * 5 + rc] = word[rc];
+        }
+    }
+}
+
 // One wave per pair (grid-stride): its rows, its hap table, its pair
 // descriptor, and its plan key — the cheaper of its two (block width, lanes)
 // candidates by the host planner's cost model, and the counting-sort bin of
@@ -229,18 +304,18 @@ __global__ __launch_bounds__(256) void flat_prep_kernel(FlatPlanArgs a)
         const FlatDesc d = a.desc[p];
         const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(d.rec & 0xffffffffll));
         const unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(d.rec >> 32));
-        const uint8_t* bases = a.img + (long long)(((unsigned long long)hi << 32) | lo);
+        const uint8_t* quals = a.img + (long long)(((unsigned long long)hi << 32) | lo);
         const int R = __builtin_amdgcn_readfirstlane(d.R), H = __builtin_amdgcn_readfirstlane(d.H);
         const int ro = __builtin_amdgcn_readfirstlane(d.row_off), ho = __builtin_amdgcn_readfirstlane(d.hapw_off);
         const int gw = __builtin_amdgcn_readfirstlane(d.gapw);
-        const uint8_t* quals = bases + R;
-        const uint8_t* gaps = quals + R;
-        pack_read(bases, quals, gaps, gaps + R, gaps + 2 * R, R, gw, a.rows + ro, lane);
-        hap_table(gaps + (gw < 0 ? 3 * R : 0), H, a.hapw + ho, lane);
+        const uint8_t* codes = quals + align4(R);
+        const uint8_t* gaps = codes + align4((R + 1) / 2);
+        pack_read_rec(quals, codes, gaps, R, gw, a.rows + ro, lane);
+        hap_table_rec(gaps + (gw < 0 ? 3 * align4(R) : 0), H, a.hapw + ho, lane);
         if (lane == 0) {
             a.pairs[p] = make_int4(ro, R, ho, H);
             const int2 c = a.ctab[H];
-            // modelled wave instructions of each candidate (planner.cpp seg_cost)
+            // modelled wave instructions of each candidate (plan_model.hpp seg_cost)
             const int bc0 = c.x & 0xff, nb0 = (c.x >> 8) & 0xff, bc1 = c.y & 0xff, nb1 = (c.y >> 8) & 0xff;
             const float k0 = float((long long)nb0 * (13 * bc0 + 26) * (R + nb0 - 1)) * a.waste[nb0];
             const float k1 = float((long long)nb1 * (13 * bc1 + 26) * (R + nb1 - 1)) * a.waste[nb1];

@@ -859,7 +859,6 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             sort_desc(ord2[c], key);
         }
     }
-    const int Hmax = hmax_a.load();
     tm.mark("one-lane/diag bins");
 
     // Staging fill: order, wave list, read descriptors + bytes, hap bytes.
@@ -951,10 +950,33 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const size_t o_list = L.take(sizeof(int) * n1);
     const size_t o_count = L.take(kNumCounters * sizeof(int));   // run counters (kernels.hpp kNumCounters)
     const size_t o_sorted = L.take(sizeof(int) * n1);
+    const size_t o_worder = L.take(sizeof(int) * n1);
     const size_t o_big = L.take(sizeof(int) * n1);
     const size_t o_bigc = L.take(sizeof(int));
     const size_t o_plan = L.take(sizeof(Seg64Plan));
     const size_t o_carry = L.take(sizeof(float2) * size_t(carry_rows) * 64 * LV.P);
+    // Anti-diagonal stripe rings too long for the LDS (kernels.hpp
+    // diag_ring_in_lds) live in global memory, one slice per workgroup; the
+    // fp32 classes and the fp64 wide-hap pass run one after another and share it.
+    const int Wc[2] = {16, 64};
+    int cls_ring[2] = {0, 0};
+    size_t ring_bytes = 0;
+    for (int c = 0; c < 2; ++c) {
+        int hm = 0;
+        for (int p : ord2[c]) hm = std::max(hm, pd[p].w);
+        cls_ring[c] = hm + 2 * Wc[c] + 16;
+        if (!ord2[c].empty() && !diag_ring_in_lds(Wc[c], cls_ring[c], false)) {
+            const size_t G = size_t(64 / Wc[c]);
+            const size_t blocks = std::min<size_t>((ord2[c].size() + G - 1) / G, kDiagRingBlocks);
+            ring_bytes = std::max(ring_bytes, blocks * G * size_t(cls_ring[c]) * sizeof(float2));
+        }
+    }
+    const int Hmax = hmax_a.load();
+    if (wide_a.load() > 0 && !diag_ring_in_lds(64, Hmax + 2 * 64 + 16, true)) {
+        const size_t blocks = std::min<size_t>(size_t(wide_a.load()), kDiagRingBlocks);
+        ring_bytes = std::max(ring_bytes, blocks * size_t(Hmax + 2 * 64 + 16) * 2 * sizeof(double));
+    }
+    const size_t o_ring = L.take(ring_bytes);
     const size_t total = L.off;
 
     auto* b = new_part(&dv);
@@ -969,8 +991,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         rc = fail(HC_PHMM_ENOMEM, "device allocation failed (" + std::to_string(total >> 20) + " MiB)");
     }
     if (rc) {
-        b->slot = nullptr;   // the caller returns the slot
-        free_part(b);
+        discard_part(b);   // the caller returns the slot
         return rc;
     }
     b->dev_base = dev;
@@ -985,7 +1006,6 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     b->d_pairs = reinterpret_cast<PairDesc*>(dev + o_pairs);
     b->d_rows = reinterpret_cast<uint32_t*>(dev + o_rows) + kRowPadBefore;
     b->d_hapw = reinterpret_cast<uint32_t*>(dev + o_hapw);
-    const int Wc[2] = {16, 64};
     int* d_ord = reinterpret_cast<int*>(dev + o_ord);
     b->d_lane_order = d_ord;
     b->cls[0].d_order = d_ord + o_ord0;
@@ -993,10 +1013,9 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     for (int c = 0; c < 2; ++c) {
         b->cls[c].W = Wc[c];
         b->cls[c].n = int(ord2[c].size());
-        int hm = 0;
-        for (int p : ord2[c]) hm = std::max(hm, pd[p].w);
-        b->cls[c].ring_len = hm + 2 * Wc[c] + 16;
+        b->cls[c].ring_len = cls_ring[c];
     }
+    b->d_ring = ring_bytes ? dev + o_ring : nullptr;
     b->d_lane_waves = reinterpret_cast<LaneWave*>(dev + o_lw);
     b->res_bytes = res_bytes;
     b->res_o64 = res_o64;
@@ -1007,6 +1026,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     b->d_list = reinterpret_cast<int*>(dev + o_list);
     b->d_count = reinterpret_cast<int*>(dev + o_count);
     b->d_sorted = reinterpret_cast<int*>(dev + o_sorted);
+    b->d_worder = reinterpret_cast<int*>(dev + o_worder);
     b->d_big = reinterpret_cast<int*>(dev + o_big);
     b->d_big_count = reinterpret_cast<int*>(dev + o_bigc);
     b->d_plan = reinterpret_cast<Seg64Plan*>(dev + o_plan);
@@ -1095,8 +1115,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     tm.mark("enqueue");
     if (rc) {
         (void)hipStreamSynchronize(s);
-        b->slot = nullptr;
-        free_part(b);
+        discard_part(b);   // the caller returns the slot
         return rc;
     }
     *out = b;

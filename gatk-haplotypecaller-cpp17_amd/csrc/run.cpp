@@ -45,6 +45,9 @@ int run_part(Part* b, hipStream_t s)
     r.plan = b->d_plan;
     r.raw_out = b->d_raw64;
     r.min_lanes = int64_t(2) * 4 * dv.n_cu * 64;
+    r.wave_order = env_i64("HC_PHMM_RESCUE_ORDER", 1) != 0 ? b->d_worder : nullptr;   // 0: class order (A/B)
+    r.next_wave = b->d_count + kNextWave;
+    r.n_simd = 4 * dv.n_cu;
     if (b->n_lane > 0) {
         LaneArgs a{};
         a.pairs = b->d_pairs;
@@ -121,6 +124,7 @@ int run_part(Part* b, hipStream_t s)
         a.hapw = b->d_hapw;
         a.lut = dv.lut_f;
         a.ring_len = c.ring_len;
+        a.ring_global = diag_ring_in_lds(c.W, c.ring_len, false) ? nullptr : b->d_ring;
         a.raw_out = b->d_raw32;
         a.rescue_flag = b->d_flag;
         a.rescue_list = b->d_list;
@@ -150,6 +154,7 @@ int run_part(Part* b, hipStream_t s)
             a.hapw = b->d_hapw;
             a.lut = dv.lut_d;
             a.ring_len = b->Hmax + 2 * 64 + 16;
+            a.ring_global = diag_ring_in_lds(64, a.ring_len, true) ? nullptr : b->d_ring;
             a.raw_out = b->d_raw64;
             HIP_TRY(launch_diag_f64(64, a, int(std::min<int64_t>(b->n_wide, 2048)), s));
         }

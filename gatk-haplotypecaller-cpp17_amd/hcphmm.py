@@ -173,12 +173,20 @@ def _flat_args(b):
     return args, arrs
 
 
-def pairs(b):
-    """Independent pairs (flat batch dict, see workloads.py) -> dict of results."""
+def result_arrays(n: int):
+    """Output arrays of a flat call of n pairs (reusable across calls, as a C++
+    caller reuses its result buffers)."""
+    return dict(loglik=np.zeros(n, np.float64), raw_f32=np.zeros(n, np.float32),
+                raw_f64=np.zeros(n, np.float64), rescued=np.zeros(n, np.uint8))
+
+
+def pairs(b, out=None):
+    """Independent pairs (flat batch dict, see workloads.py) -> dict of results
+    (written into `out` from :func:`result_arrays` when given)."""
     args, keep = _flat_args(b)
     n = len(keep["R"])
-    out = dict(loglik=np.zeros(n, np.float64), raw_f32=np.zeros(n, np.float32),
-               raw_f64=np.zeros(n, np.float64), rescued=np.zeros(n, np.uint8))
+    if out is None:
+        out = result_arrays(n)
     _check(lib().hc_phmm_pairs_flat(*args, _p(out["loglik"], _f64p), _p(out["raw_f32"], _f32p),
                                     _p(out["raw_f64"], _f64p), _p(out["rescued"], _u8p)))
     return out
@@ -290,13 +298,13 @@ class Job:
                 pass
 
 
-def submit_pairs(b) -> Job:
+def submit_pairs(b, out=None) -> Job:
     """Asynchronous :func:`pairs`: returns a :class:`Job` whose collect()
     gives the same dict."""
     args, _arrs = _flat_args(b)
     n = len(_arrs["R"])
-    out = dict(loglik=np.zeros(n, np.float64), raw_f32=np.zeros(n, np.float32),
-               raw_f64=np.zeros(n, np.float64), rescued=np.zeros(n, np.uint8))
+    if out is None:
+        out = result_arrays(n)
     h = C.c_void_p()
     _check(lib().hc_phmm_submit_pairs(*args, _p(out["loglik"], _f64p), _p(out["raw_f32"], _f32p),
                                       _p(out["raw_f64"], _f64p), _p(out["rescued"], _u8p), C.byref(h)))

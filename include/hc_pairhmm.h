@@ -59,7 +59,7 @@ extern "C" {
 #define HC_PHMM_EHIP (-3)     /* HIP runtime error                                  */
 #define HC_PHMM_ENOMEM (-4)   /* host or device allocation failed                   */
 
-#define HC_PHMM_MAX_HAP_LEN 8192   /* LDS ring bound of the anti-diagonal kernel */
+#define HC_PHMM_MAX_HAP_LEN 262144   /* longer haps: anti-diagonal kernel with its stripe ring in HBM */
 #define HC_PHMM_MAX_READ_LEN 65536
 
 /* shacc_pairhmm::Read (shacc_pairhmm.h:12-19): same fields, same order. */

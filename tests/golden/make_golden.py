@@ -13,8 +13,8 @@ workloads.py) + the reference's outputs for every pair:
     loglik       finished log10 likelihood             (intel_pairhmm.hpp:137-143)
 and the reference LUTs (ph2pr, matchToMatchProb) plus a SHA-256 of the
 Jacobian tables. Sets: SURVEY Appendix-B edge grid (1 596 pairs), a random
-mixed set, S1/S4 samples, and an underflow set that drives fp64 results into
-the denormal / FTZ -> 0 -> -inf region.
+mixed set, S1/S4 samples, an underflow set that drives fp64 results into
+the denormal / FTZ -> 0 -> -inf region, and haps of 8 193 - 20 000 bases.
 """
 from __future__ import annotations
 
@@ -76,6 +76,34 @@ def underflow_set(seed):
     return concat(out)
 
 
+def long_haps(seed):
+    """Haplotypes past the anti-diagonal kernel's LDS ring (H 8 193, 12 000,
+    20 000): reads copied from the hap, random reads (rescued in fp64), one
+    base, 8 % substitutions at R 250, and an N-rich read with per-base gap
+    qualities."""
+    rng = np.random.default_rng(seed)
+    pairs = []
+    for H in (8193, 12000, 20000):
+        hap = W.ACGT[rng.integers(0, 4, H)]
+        o = int(rng.integers(0, H - 250))
+        kinds = []
+        rs = hap[o:o + 150].copy()
+        kinds.append((rs, rng.integers(43, 74, 150), np.full(150, W.GOP), np.full(150, W.GOP), np.full(150, W.GCP)))
+        rs = W.ACGT[rng.integers(0, 4, 101)]
+        kinds.append((rs, rng.integers(60, 74, 101), np.full(101, W.GOP), np.full(101, W.GOP), np.full(101, W.GCP)))
+        kinds.append((hap[o:o + 1].copy(), np.array([60]), np.array([W.GOP]), np.array([W.GOP]), np.array([W.GCP])))
+        rs = hap[o:o + 250].copy()
+        sub = rng.random(250) < 0.08
+        rs[sub] = W.ACGT[rng.integers(0, 4, int(sub.sum()))]
+        kinds.append((rs, rng.integers(43, 74, 250), np.full(250, W.GOP), np.full(250, W.GOP), np.full(250, W.GCP)))
+        rs = np.frombuffer(b"ACGTN", np.uint8)[rng.integers(0, 5, 64)]
+        kinds.append((rs, rng.integers(33, 127, 64), rng.integers(20, 90, 64), rng.integers(20, 90, 64),
+                      rng.integers(10, 60, 64)))
+        for rs, q, i, d, c in kinds:
+            pairs.append(tuple(np.asarray(x, np.uint8).tobytes() for x in (rs, q, i, d, c)) + (hap.tobytes(),))
+    return W.from_pairs(pairs)
+
+
 def main():
     ref = oracle.Reference()
     sets = {
@@ -85,6 +113,7 @@ def main():
         "s2": W.subset(W.config("S2", 20_000), np.arange(400)),
         "s4": W.subset(W.config("S4"), np.arange(40)),
         "underflow": underflow_set(seed=101),
+        "long_haps": long_haps(seed=131),
     }
     names = list(sets)
     batch = concat([sets[k] for k in names])

@@ -97,3 +97,31 @@ int main() {
                     "-L", os.path.dirname(hcphmm.LIB_PATH), "-lhcpairhmm",
                     "-Wl,-rpath," + os.path.dirname(hcphmm.LIB_PATH), "-o", str(exe)], check=True)
     assert exe.exists()
+
+
+def test_flat_record_nibble_packing():
+    """Flat calls upload base codes as nibbles (flat_plan.cpp pack_nibbles,
+    AVX2 with a scalar tail): ConvertChar codes (pairhmm_common.h:26-44: A0 C1
+    T2 G3 N4, every other byte 0), two per byte, even index in the low nibble;
+    every byte value and every length around the 64-byte vector step."""
+    import ctypes as C
+    import hcphmm
+    L = hcphmm.lib()
+    L.hcx_pack_nibbles.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+    L.hcx_pack_nibbles.restype = None
+    code = np.zeros(256, np.uint8)
+    for ch, v in ((b"C", 1), (b"T", 2), (b"G", 3), (b"N", 4)):
+        code[ch[0]] = v
+    rng = np.random.default_rng(0)
+    for n in list(range(0, 140)) + [255, 256, 257, 1000, 4096]:
+        s = rng.integers(0, 256, n, dtype=np.uint8)
+        if n >= 256:
+            s[:256] = np.arange(256, dtype=np.uint8)
+        c = code[s]
+        exp = np.zeros((n + 1) // 2, np.uint8)
+        exp[:] = c[0::2]
+        exp[: n // 2] |= c[1::2] << 4
+        got = np.full((n + 1) // 2 + 8, 0xEE, np.uint8)
+        L.hcx_pack_nibbles(s.ctypes.data, n, got.ctypes.data)
+        assert np.array_equal(got[: (n + 1) // 2], exp), n
+        assert (got[(n + 1) // 2:] == 0xEE).all(), n   # nothing written past the record field

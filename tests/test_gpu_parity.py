@@ -150,14 +150,24 @@ def test_cross_and_compute_likelihoods(engine, kernel, oracle_lib):
     assert np.array_equal(bits(Ln), bits(refn[keep]))
 
 
-def test_edge_contract(engine):
+def test_edge_contract(engine, oracle_lib):
     empty = engine.cross([], [b"ACGT"])
     assert empty.shape == (0, 1)
     with pytest.raises(engine.PairHMMError) as e:
         engine.cross([(b"", b"", b"", b"", b"")], [b"ACGT"])
     assert e.value.code == engine.EINVAL
-    with pytest.raises(engine.PairHMMError):
-        engine.cross([(b"A", b"I", b"I", b"I", b"+")], [b"A" * 9000])
+    # Haps past the anti-diagonal kernel's LDS ring (the reference has no hap
+    # length limit: its stripe carries are VLAs, avx-pairhmm-template.h:224)
+    # run with the ring in HBM.
+    reads = [(b"A", b"I", b"I", b"I", b"+"), (b"ACGTN" * 30, b"5" * 150, b"I" * 150, b"I" * 150, b"+" * 150)]
+    haps = [b"A" * 9000, (b"ACGT" * 3000)[:12000]]
+    got = engine.cross(reads, haps)
+    flat = W.from_pairs([(r[0], r[1], r[2], r[3], r[4], h) for r in reads for h in haps])
+    ref = oracle_lib.pairs(flat, nthreads=16)["loglik"].reshape(2, 2)
+    assert np.array_equal(bits(got), bits(ref))
+    with pytest.raises(engine.PairHMMError) as e:
+        engine.cross([(b"A", b"I", b"I", b"I", b"+")], [b"A" * 262145])
+    assert e.value.code == engine.EINVAL
 
 
 def test_s2_full_size_properties(engine):

@@ -15,10 +15,13 @@ hcphmm.init(0)
 print(f"init: {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
 b = W.config(sys.argv[1] if len(sys.argv) > 1 else "S2")
 cells = W.cells(b)
+out = hcphmm.result_arrays(len(b["R"]))
+for v in out.values():
+    v.fill(0)
 ts = []
 for k in range(int(os.environ.get("REPS", "5"))):
     t = time.perf_counter()
-    r = hcphmm.pairs(b)
+    r = hcphmm.pairs(b, out)
     dt = time.perf_counter() - t
     ts.append(dt)
     print(f"call {k}: {dt * 1e3:.1f} ms  {cells / dt / 1e9:.1f} GCUPS", flush=True)
