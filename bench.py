@@ -74,30 +74,38 @@ def cpu_baseline(batch, threads, reps, sample_desc):
                 sample=sample_desc, seconds=round(best, 3)), res
 
 
-def pmc_from_profiles(workload, cells, kernel_ms):
-    """Counters of the dominant kernel from the newest committed PMC summary of
-    this workload (profiles/r*_pmc_<workload>.json, tools/pmc_summary.py),
-    scaled by cells when this launch is a shard of the profiled one: HBM bytes
-    per launch (2*FETCH_SIZE + WRITE_SIZE, gfx950 rule), LDS bank-conflict
-    cycles per launch, VALU lane-instructions per cell, and the measured HBM
-    rate traffic / kernel time."""
+def pmc_from_profiles(workload, cells, kernel_ms, world):
+    """Counters of the dominant kernel from the committed PMC summary of this
+    exact configuration (profiles/r*_pmc_<workload>.json, written by
+    tools/profile_r03.sh + tools/profile_summary.py): used only when its kernel
+    source hash (tools/kernel_src_hash.py) equals the tree's and it profiled the
+    same cell count on one GPU; otherwise traffic is null. Reports HBM bytes per
+    launch (2*FETCH_SIZE + WRITE_SIZE, gfx950 rule), LDS bank-conflict cycles,
+    VALU lane-instructions per cell, the measured HBM rate traffic / kernel
+    time, and the profile's own warm-average frac beside this run's."""
+    if world != 1:
+        return dict(traffic_note="PMC profiles are single-GPU; N>1 reports traffic null")
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from kernel_src_hash import kernel_src_hash
+    want = kernel_src_hash()
     cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}.json")))
-    if not cands:
-        return {}
-    try:
-        d = json.load(open(cands[-1]))
-        k = d["kernels"][d["dominant_kernel"]]
-        prof_cells = d.get("cells") or (d["hbm_bytes_per_launch"] / d["hbm_bytes_per_cell"])
-        scale = cells / prof_cells
-        traffic = int(d["hbm_bytes_per_launch"] * scale)
-        out = dict(traffic=traffic, traffic_source=os.path.relpath(cands[-1], ROOT),
-                   lds_bank_conflict_cycles=int(k.get("SQ_LDS_BANK_CONFLICT", 0) * scale),
-                   valu_lane_instr_per_cell=round(k["SQ_INSTS_VALU"] * 64 / prof_cells, 3))
-        if kernel_ms > 0:
-            out["hbm_measured_GBs"] = round(traffic / (kernel_ms * 1e-3) / 1e9, 2)
-        return out
-    except Exception:
-        return {}
+    for path in reversed(cands):
+        try:
+            d = json.load(open(path))
+            if d.get("kernel_src_hash") != want or int(d.get("cells", -1)) != int(cells):
+                continue
+            k = d["kernels"][d["dominant_kernel"]]
+            out = dict(traffic=int(d["hbm_bytes_per_launch"]), traffic_source=os.path.relpath(path, ROOT),
+                       kernel_src_hash=want, profile_kernel_ms_warm=k.get("avg_ms_warm"),
+                       profile_frac=d.get("frac_from_warm_avg"),
+                       lds_bank_conflict_cycles=int(k.get("SQ_LDS_BANK_CONFLICT", 0)),
+                       valu_lane_instr_per_cell=d.get("valu_lane_instr_per_cell"))
+            if kernel_ms > 0:
+                out["hbm_measured_GBs"] = round(out["traffic"] / (kernel_ms * 1e-3) / 1e9, 2)
+            return out
+        except (OSError, KeyError, ValueError, TypeError):
+            continue
+    return dict(traffic_note=f"no committed PMC profile of this config with kernel source hash {want}")
 
 
 def host_cpu():
@@ -249,7 +257,7 @@ def gt_secondary(no_cpu: bool):
 FP64_PEAK_TOPS = 39.3   # AMD MI355X FP64 vector 78.6 TFLOPS (FMA = 2) -> 39.3 T non-FMA op/s; the guide has no FP64 row
 
 
-def resident_pass(hcphmm, W, name, npairs):
+def resident_pass(hcphmm, W, name, npairs, prof):
     """One BASELINE config as a device-resident batch: 5 timed device passes
     (HIP events). S4 also prices its fp64 rescue pass (intel_pairhmm.hpp:
     137-139): 12 f64 ops per rescued cell / fp64 pass time vs the fp64 peak."""
@@ -269,6 +277,10 @@ def resident_pass(hcphmm, W, name, npairs):
                if s2.kernel_ms_f32 > 0 else None,
                kernel_ms_f64=round(s2.kernel_ms_f64, 4), rescued=int(s2.n_rescued),
                new_batch_device_ms=round(s2.run_ms + s2.pack_ms, 4))
+    pmc = pmc_from_profiles(prof, cells, s2.kernel_ms_f32, 1)
+    if "traffic" in pmc:
+        ent["pmc"] = {k: pmc[k] for k in ("traffic", "traffic_source", "profile_kernel_ms_warm", "profile_frac",
+                                          "hbm_measured_GBs", "valu_lane_instr_per_cell")}
     if s2.n_rescued and s2.kernel_ms_f64 > 0:
         r = bb.results()
         m = r["rescued"].astype(bool)
@@ -503,7 +515,8 @@ def main():
     # Dominant kernel: the fp32 PairHMM pass. Algorithmic work 12 ops/cell.
     k_ms = st.kernel_ms_f32
     achieved = FLOPS_PER_CELL * my_cells / (k_ms * 1e-3) / 1e12 if k_ms > 0 else 0.0
-    pmc = pmc_from_profiles(args.workload, my_cells, k_ms)
+    pmc = pmc_from_profiles(args.workload if args.pairs is None else f"{args.workload}_{args.pairs}",
+                            my_cells, k_ms, world)
     roofline = dict(bound="valu", achieved=round(achieved, 3), peak=VALU_PEAK_TOPS, unit="TFLOP/s",
                     frac=round(achieved / VALU_PEAK_TOPS, 4), traffic=pmc.get("traffic"),
                     kernel=(("phmm_seg_kernel" if st.n_seg_waves > 0 else "phmm_lane_kernel")
@@ -514,7 +527,9 @@ def main():
                     hbm_measured_GBs=pmc.get("hbm_measured_GBs"), hbm_peak_GBs=HBM_PEAK_GBS,
                     lds_bank_conflict_cycles=pmc.get("lds_bank_conflict_cycles"),
                     valu_lane_instr_per_cell=pmc.get("valu_lane_instr_per_cell"),
-                    traffic_source=pmc.get("traffic_source"))
+                    traffic_source=pmc.get("traffic_source"), traffic_note=pmc.get("traffic_note"),
+                    kernel_src_hash=pmc.get("kernel_src_hash"),
+                    profile_kernel_ms_warm=pmc.get("profile_kernel_ms_warm"), profile_frac=pmc.get("profile_frac"))
 
     out = {
         "metric": "PairHMM GCUPS (cell updates/s), fp32 pass + fp64 rescue",
@@ -564,8 +579,11 @@ def main():
         sec = {}
         # S1w1M: the north star's 101x250 shape at a size that fills the chip
         # (S1/S1w are 10k-pair, latency-bound passes of < 0.15 ms).
-        for name, npairs in (("S1", None), ("S1w", None), ("S1w1M", 1_000_000), ("S4", None)):
-            sec[name] = resident_pass(hcphmm, W, name.replace("1M", ""), npairs)
+        # S4_20k: the S4 shape at 20 000 pairs, a rescue pass large enough to
+        # fill the chip with fp64 waves (S4 itself rescues ~2k pairs).
+        for label, name, npairs in (("S1", "S1", None), ("S1w", "S1w", None), ("S1w1M", "S1w", 1_000_000),
+                                    ("S4", "S4", None), ("S4_20k", "S4", 20_000)):
+            sec[label] = resident_pass(hcphmm, W, name, npairs, name if npairs is None else f"{name}_{npairs}")
         sec.update(region_calls(hcphmm, W, args.no_cpu))
         sec["smith_waterman"] = sw_secondary(args.no_cpu)
         sec["genotyper"] = gt_secondary(args.no_cpu)

@@ -88,10 +88,17 @@ int plan_call_part(Device& d, const Src& src, const PartSpec& spec, Slot* sl, bo
     return plan_part(d, src, spec, sl, with_run, PlanMode::Real, p);
 }
 
-// Prepared batches keep the host planner: the plan is made once and run
-// many times, and its mixed-width greedy packing fills the waves best.
+// Prepared batches keep the host planner unless HC_PHMM_BATCH_PLAN=device:
+// the plan is made once and run many times, and its mixed-width greedy
+// packing fills the waves best.
 int plan_batch_part(Device& d, const Src& src, const PartSpec& spec, Part** p)
 {
+    *p = nullptr;
+    const char* e = std::getenv("HC_PHMM_BATCH_PLAN");
+    if (e && !std::strcmp(e, "device")) {
+        const int rc = plan_flat_device(d, src, spec, nullptr, false, p);
+        if (rc || *p) return rc;
+    }
     return plan_part(d, src, spec, nullptr, false, PlanMode::Real, p);
 }
 
@@ -603,7 +610,14 @@ int hc_phmm_batch_stats(hc_phmm_batch* b, hc_phmm_stats* st)
         st->cells += p->cells;
         st->n_launch_waves += p->launch_waves;
         st->n_lane_pairs += p->n_lane;
-        st->n_seg_waves += p->n_seg_waves;
+        if (p->d_nwaves && p->pack_ev[1]) {   // device-planned: the plan's own wave count
+            int nw = 0;
+            HIP_TRY(hipEventSynchronize(p->pack_ev[1]));
+            HIP_TRY(hipMemcpy(&nw, p->d_nwaves, sizeof(int), hipMemcpyDeviceToHost));
+            st->n_seg_waves += nw;
+        } else {
+            st->n_seg_waves += p->n_seg_waves;
+        }
         st->upload_bytes += int64_t(p->upload_bytes);
         if (p->pack_ev[0]) {
             float pk = 0;

@@ -295,7 +295,15 @@ int plan_flat_device(Device& d, const Src& src, const PartSpec& spec, Slot* slot
 // run.cpp
 int run_part(Part* b, hipStream_t s);
 void finish_part(const Part& P, const float* f, const double* d, const uint8_t* fl, const Outputs& o);
-// Enqueue the D2H of a part's results and its done event (with_run parts).
+// Enqueue the results' return to the pinned host image and the part's done
+// event (with_run parts). A kernel stores them into the mapped host memory
+// rather than a DMA copy: DMA copies run in enqueue order, so a D2H enqueued
+// behind its part's kernels held the next part's uploads until those kernels
+// finished (the parts of a call ran one after another: S2 end to end 22 ms).
+// ConvertChar codes (pairhmm_common.h:26-44: A0 C1 T2 G3 N4, other bytes 0) of n bases, two per byte,
+// base k in the low nibble of byte k / 2 when k is even (AVX2 when the CPU
+// has it; flat_plan.cpp).
+void pack_nibbles(const uint8_t* s, int n, uint8_t* d);
 int enqueue_results(Part* b, hipStream_t s);
 
 // The last dry-run plan (hcx_dump_sizes / hcx_dump_plan).

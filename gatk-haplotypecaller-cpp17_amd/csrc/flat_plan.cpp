@@ -437,7 +437,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     const size_t n1 = size_t(n);
     const size_t res_o64 = (sizeof(float) * n1 + 255) & ~size_t(255);
     const size_t res_ofl = res_o64 + ((sizeof(double) * n1 + 255) & ~size_t(255));
-    const size_t res_bytes = res_ofl + n1;
+    const size_t res_bytes = (res_ofl + n1 + 15) & ~size_t(15);   // whole 16-byte stores (launch_store_to_host)
     struct Lay {
         size_t off = 0;
         size_t take(size_t b)
@@ -460,6 +460,10 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     const size_t o_gtab = L.take(sizeof(int) * 3 * size_t(ngroups));
     const size_t o_order = L.take(sizeof(int) * n1);
     const size_t o_waves = L.take(sizeof(LaneWave) * size_t(max_waves));
+    // The last two rounds of wave slots (3 per SIMD) dispatched longest first
+    // (planner.cpp: 125k-pair shard 1.39 -> 1.25 ms with it on the host plan).
+    const int tail = int(std::max<int64_t>(0, env_i64("HC_PHMM_TAIL_ROUNDS", 2))) * 4 * dv.n_cu * 3;
+    const size_t o_wtmp = L.take(tail > 0 ? sizeof(LaneWave) * size_t(max_waves) : 0);
     const size_t o_nw = L.take(sizeof(int));
     const size_t o_res = L.take(res_bytes);
     const size_t o_list = L.take(sizeof(int) * n1);
@@ -471,10 +475,23 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     const size_t o_plan = L.take(sizeof(Seg64Plan));
     const size_t total = L.off;
     const size_t host_res_off = (tab_bytes + 255) & ~size_t(255);
-    int rc = slot_reserve(*slot, total, host_res_off + res_bytes);
-    if (rc) return rc;
-    char* dev = slot->dev;
-    char* host = slot->host;
+    // Jobs borrow their slot's workspace; batches (slot == nullptr) own their
+    // device memory, and their tables go up from plain host memory.
+    std::vector<char> own_tab;
+    char* dev = nullptr;
+    char* host = nullptr;
+    int rc = HC_PHMM_OK;
+    if (slot) {
+        rc = slot_reserve(*slot, total, host_res_off + res_bytes);
+        if (rc) return rc;
+        dev = slot->dev;
+        host = slot->host;
+    } else {
+        if (hipMalloc(&dev, total) != hipSuccess)
+            return fail(HC_PHMM_ENOMEM, "device allocation failed (" + std::to_string(total >> 20) + " MiB)");
+        own_tab.resize(tab_bytes);
+        host = own_tab.data();
+    }
     tm.mark("flat: layout");
 
     // Tables (the slot's pinned area; its results image follows).
@@ -498,7 +515,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     auto* b = new_part(&dv);
     b->spec = spec;
     b->slot = slot;
-    b->dev_base = dev;
+    b->dev_base = dev;   // a batch's own allocation (freed with it), or the slot's
     b->n = n;
     b->Hmax = hmax;
     b->n_lane = int(n);
@@ -524,16 +541,23 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     b->d_big_count = reinterpret_cast<int*>(dev + o_bigc);
     b->d_plan = reinterpret_cast<Seg64Plan*>(dev + o_plan);
     b->n_wide = nwide;
-    b->host_res = host + host_res_off;
-    b->stream = slot->stream;
-    b->side = slot->side;
-    b->fork = slot->fork;
-    b->join = slot->join;
-    b->slot_ev = true;
-    b->pack_ev[0] = slot->ev[0];
-    b->pack_ev[1] = slot->ev[1];
-    b->ev_pool.push_back({slot->ev[2], slot->ev[3], slot->ev[4]});
-    b->done = slot->ev[5];
+    if (slot) {
+        b->host_res = host + host_res_off;
+        b->stream = slot->stream;
+        b->side = slot->side;
+        b->fork = slot->fork;
+        b->join = slot->join;
+        b->slot_ev = true;
+        b->pack_ev[0] = slot->ev[0];
+        b->pack_ev[1] = slot->ev[1];
+        b->ev_pool.push_back({slot->ev[2], slot->ev[3], slot->ev[4]});
+        b->done = slot->ev[5];
+    } else {
+        b->stream = dv.stream;
+        b->side = dv.side;
+        b->fork = dv.fork;
+        b->join = dv.join;
+    }
     b->upload_bytes = size_t(rec) + sizeof(FlatDesc) * n1 + tab_bytes;
     hipStream_t s = b->stream;
 
@@ -562,6 +586,8 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
             }
         }
         tm.mark("flat: fill + H2D");
+        if (!b->slot_ev)
+            for (auto& e : b->pack_ev) HIP_TRY(hipEventCreate(&e));
         HIP_TRY(hipMemcpyAsync(dev + o_tab, host, tab_bytes, hipMemcpyHostToDevice, s));
         HIP_TRY(hipEventRecord(b->pack_ev[0], s));
         FlatPlanArgs a{};
@@ -584,6 +610,8 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
         a.gtab = reinterpret_cast<int*>(dev + o_gtab);
         a.order = b->d_lane_order;
         a.waves = b->d_lane_waves;
+        a.waves_tmp = reinterpret_cast<LaneWave*>(dev + o_wtmp);
+        a.tail = tail;
         a.max_waves = int(max_waves);
         a.nwaves = reinterpret_cast<int*>(dev + o_nw);
         a.counters = b->d_count;
@@ -594,6 +622,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
             if (r) return r;
             return enqueue_results(b, s);
         }
+        if (!slot) HIP_TRY(hipStreamSynchronize(s));   // the tables' host memory goes with this call
         return HC_PHMM_OK;
     };
     rc = enqueue();
@@ -612,7 +641,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
 int plan_flat_device(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool with_run, Part** out)
 {
     *out = nullptr;
-    if (!spec.flat || !src.R || !slot || !default_policies()) return HC_PHMM_OK;
+    if (!spec.flat || !src.R || !default_policies() || (!slot && with_run)) return HC_PHMM_OK;
     int rc = plan_flat_try(dv, src, spec, slot, with_run, false, out);
     if (rc == kRetryWithPlanes) rc = plan_flat_try(dv, src, spec, slot, with_run, true, out);
     return rc;

@@ -12,7 +12,7 @@ namespace hcphmm {
 //   bits 21-27  c  (gap continuation byte & 127)
 //   bits 28-30  read base code, ConvertChar (pairhmm_common.h:26-44): A0 C1 T2 G3 N4
 //   bit  31     first row of a read only: the read's gap qualities are constant
-//               (found on the host while staging, set by pack_reads_kernel)
+//               (found on the host while staging, set by the packer)
 __host__ __device__ inline uint32_t pack_row(int q, int i, int d, int c, int code)
 {
     return uint32_t(q & 127) | (uint32_t(i & 127) << 7) | (uint32_t(d & 127) << 14) |
@@ -172,40 +172,16 @@ constexpr int kDiagRingBlocks = 1024;
 inline bool diag_ring_in_lds(int W, int ring_len, bool f64) { return diag_lds_bytes(W, ring_len, f64) <= kDiagLdsMax; }
 hipError_t configure_kernels();   // raise the dynamic-LDS limit once
 
-// Device packing (pack_kernels.hip). Reads: `bases` / `quals` one byte per
-// row (row k of read r at rdesc[r].x + k); rdesc {row offset, length, constant
-// gap triple i | d << 7 | c << 14 or -1, offset into the i/d/c planes `gaps`
-// (3 planes of gap_stride bytes) when the read's gap qualities vary}.
-// Haps: {byte offset, H, table word offset, 0}; tables as hap_table_words.
-hipError_t launch_pack_reads(const uint8_t* bases, const uint8_t* quals, const uint8_t* gaps, long long gap_stride,
-                             const int4* rdesc, int nreads, uint32_t* rows, hipStream_t s);
-hipError_t launch_hap_tables(const uint8_t* hap_bytes, const int4* haps, int nhaps, uint32_t* hapw, hipStream_t s);
-// Pair descriptors of a structured (cross-product) plan, built on the device
-// instead of uploaded: block b's pairs [p0, p0 + nr * nh) are its reads
-// [r0, r0 + nr) x haps [h0, h0 + nh) (part-local ids), read-major; blocks in
-// ascending p0. pairs[k] = {rows offset, R, table offset, H} from the read and
-// hap descriptors (rdesc .x/.y, hdesc .z/.y).
-struct GridBlock {
-    long long p0;
-    int nr, nh, r0, h0;
-};
-hipError_t launch_grid_pairs(const GridBlock* blocks, int nblocks, long long npairs, const int4* rdesc,
-                             const int4* hdesc, PairDesc* pairs, hipStream_t s);
-// Slot order and segmented waves of a structured plan, built on the device
-// from its segments (engine.cpp plan_grid): segment g holds the pairs of block
-// reads rord[r0 .. r0 + nr) (by R descending) x haps hord[g0 .. g0 + G),
-// read-major, in slots [slot0, slot0 + nr * G) and waves [w0, ...) of
-// floor(64 / nb) pairs at block width bc. Segments in ascending slot0 / w0.
-struct GridSeg {
-    long long slot0, p0;   // first slot; the block's first pair
-    int w0, r0, nr, nh, h0, g0, G, bc, nb, pad;
-};
-hipError_t launch_grid_waves(const GridSeg* segs, int nsegs, long long nslots, int nwaves, const int* rord,
-                             const int* hord, const int4* rdesc, int* order, LaneWave* waves, hipStream_t s);
-// The run counters zeroed, launch_pack_reads, launch_hap_tables,
-// launch_grid_pairs and launch_grid_waves of one structured part, fused into
-// one launch.
-struct GridPrepArgs {
+// Device packing of a staged part (pack_kernels.hip), one launch. Reads:
+// `quals` one byte per row, `bases` the ConvertChar codes two per byte (row k
+// of read r: quality byte rdesc[r].x + k, code nibble rdesc[r].x + k, low
+// nibble first; each read's start a multiple of 4); rdesc {row offset,
+// length, constant gap triple i | d << 7 | c << 14 or -1, offset (a multiple
+// of 4) into the i/d/c planes `gaps` (3 planes of gap_stride bytes) when the
+// read's gap qualities vary}. Haps: codes two per byte, hdesc {byte offset (a
+// multiple of 4), H, table word offset, 0}; tables as hap_table_words. Bytes
+// past a read's or hap's end up to its alignment are read and ignored.
+struct PackArgs {
     const uint8_t *bases, *quals, *gaps;
     long long gap_stride;
     const int4* rdesc;
@@ -215,6 +191,31 @@ struct GridPrepArgs {
     const int4* hdesc;
     int nhaps;
     uint32_t* hapw;
+};
+hipError_t launch_pack_batch(const PackArgs& a, hipStream_t s);
+// Pair descriptors of a structured (cross-product) plan, built on the device
+// instead of uploaded: block b's pairs [p0, p0 + nr * nh) are its reads
+// [r0, r0 + nr) x haps [h0, h0 + nh) (part-local ids), read-major; blocks in
+// ascending p0. pairs[k] = {rows offset, R, table offset, H} from the read and
+// hap descriptors (rdesc .x/.y, hdesc .z/.y).
+struct GridBlock {
+    long long p0;
+    int nr, nh, r0, h0;
+};
+// Slot order and segmented waves of a structured plan, built on the device
+// from its segments (engine.cpp plan_grid): segment g holds the pairs of block
+// reads rord[r0 .. r0 + nr) (by R descending) x haps hord[g0 .. g0 + G),
+// read-major, in slots [slot0, slot0 + nr * G) and waves [w0, ...) of
+// floor(64 / nb) pairs at block width bc. Segments in ascending slot0 / w0.
+struct GridSeg {
+    long long slot0, p0;   // first slot; the block's first pair
+    int w0, r0, nr, nh, h0, g0, G, bc, nb, pad;
+};
+// A structured part's preparation in one launch: the run counters zeroed,
+// the packing of launch_pack_batch, its pair descriptors (GridBlock) and its
+// slot order and waves (GridSeg).
+struct GridPrepArgs {
+    PackArgs pack;
     const GridBlock* blocks;
     int nblocks;
     long long npairs;
@@ -263,11 +264,16 @@ struct FlatPlanArgs {
     int ngroups;
     int* gtab;             // per group: {first slot, pairs, first wave}
     int* order;            // slot -> pair
-    LaneWave* waves;
+    LaneWave* waves;       // the plan's waves (packing order), then the dispatch order
+    LaneWave* waves_tmp;   // max_waves entries: the packing order while the tail is reordered
     int max_waves;         // waves the launch covers (upper bound of the plan's)
     int* nwaves;           // the plan's wave count
+    int tail;              // waves dispatched last, longest first (0: packing order)
     int* counters;         // kNumCounters run counters, zeroed
 };
 hipError_t launch_flat_plan(const FlatPlanArgs& a, hipStream_t s);
+// bytes (a multiple of 16, both 16-byte aligned) from device memory to mapped
+// pinned host memory, stored by a kernel (no DMA engine).
+hipError_t launch_store_to_host(void* host, const void* dev, size_t bytes, hipStream_t s);
 
 }  // namespace hcphmm

@@ -3,20 +3,22 @@
 // avx-pairhmm-template.h:3-35, done once per read and once per haplotype
 // instead of once per pair).
 //
-//   pack_reads   uploaded read bytes -> one uint32 row word per base
-//                (kernels.hpp pack_row). The upload carries 2 bytes per base
-//                (base, quality); a read whose gap qualities are constant —
-//                every read the reference builds, sam.hpp:30-32,47-49 — sends
-//                them once in its descriptor, the others send 3 more planes.
-//   hap_tables   hap bytes -> per-hap match table, (ceil(H/32) + 3) rows of 5
-//                words: bit (MSB first) per column for read codes 0..4.
+//   pack_batch   staged read bytes -> one uint32 row word per base
+//                (kernels.hpp pack_row), four rows per lane; hap bytes ->
+//                per-hap match table, (ceil(H/32) + 3) rows of 5 words: bit
+//                (MSB first) per column for read codes 0..4, eight columns per
+//                lane. The upload carries 2 bytes per base (base, quality); a
+//                read whose gap qualities are constant — every read the
+//                reference builds, sam.hpp:30-32,47-49 — sends them once in its
+//                descriptor, the others send 3 more planes.
 //   grid_*       descriptors, slot order and waves of a structured
 //                (cross-product) plan from its block and segment tables.
 //   flat_*       a flat batch planned on the device: rows, tables, each pair's
 //                segmented shape, a counting sort and the waves (flat_plan.cpp).
 //
-// The packers are byte-streaming kernels, one wave per read / per haplotype
-// (coalesced byte loads across the wave; the match words come from ballots).
+// The packers are byte-streaming kernels, a wave per read / haplotype / pair,
+// loading 4 or 8 bytes per lane and keeping several requests in flight per
+// wave (the packing is latency-bound, not bandwidth-bound, at one chain each).
 #include <algorithm>
 
 #include "kernels.hpp"
@@ -24,87 +26,128 @@
 namespace hcphmm {
 namespace {
 
-// ConvertChar (pairhmm_common.h:26-44): A0 C1 T2 G3 N4, every other byte -> 0.
-__device__ __forceinline__ uint32_t base_code(uint32_t b)
-{
-    return b == 'C' ? 1u : b == 'T' ? 2u : b == 'G' ? 3u : b == 'N' ? 4u : 0u;
-}
+// Nibbles equal to zero (values <= 7): bit 0 of each such nibble.
+__device__ __forceinline__ uint32_t zero_nibbles(uint32_t t) { return ~(t | (t >> 1) | (t >> 2)) & 0x11111111u; }
 
-// Row words of one read, lanes over rows (a wave). gw: constant gap qualities
-// i | d << 7 | c << 14 (already & 127), or -1 when they vary: then the i, d, c
-// planes are at gi, gd, gc.
-__device__ __forceinline__ void pack_read(const uint8_t* __restrict__ bases, const uint8_t* __restrict__ quals,
-                                          const uint8_t* __restrict__ gi, const uint8_t* __restrict__ gd,
-                                          const uint8_t* __restrict__ gc, int len, int gw, uint32_t* __restrict__ rows,
-                                          int lane)
+// Match-table words of 32 columns from a quad of lanes, each holding the
+// codes of 8 columns as nibbles (column 8 * lane + j in nibble j) of which the
+// first nv are real: per read code, the lane's 8 match bits (MSB first), the
+// quad's four bytes joined by DPP quad_perm. Lane 4q + 0 stores the word of
+// columns 32 * (w) + 1 .. 32 * (w + 1), w = base / 32 + q; all 64 lanes take part.
+__device__ __forceinline__ void hap_words(uint32_t x, int nv, int base, int nw, uint32_t* __restrict__ o, int lane)
 {
-    for (int k = lane; k < len; k += 64) {
-        const uint32_t q = quals[k] & 127u;
-        const uint32_t code = base_code(bases[k]) << 28;
-        uint32_t w;
-        if (gw >= 0) {
-            w = q | (uint32_t(gw) << 7) | code;
-            if (k == 0) w |= 0x80000000u;   // constant-gap tag on the read's first row
-        } else {
-            w = q | ((gi[k] & 127u) << 7) | ((gd[k] & 127u) << 14) | ((gc[k] & 127u) << 21) | code;
-        }
-        rows[k] = w;
+    const uint32_t vmask = nv >= 8 ? 0x11111111u : (nv > 0 ? 0x11111111u & ((1u << (4 * nv)) - 1u) : 0u);
+    const uint32_t isN = zero_nibbles(x ^ 0x44444444u);
+    uint32_t word[5];
+#pragma unroll
+    for (int rc = 0; rc < 5; ++rc) {
+        // read code rc matches: equal code, hap 'N' (matches every rc), or read 'N'
+        const uint32_t eq = (rc == 4 ? 0x11111111u : (zero_nibbles(x ^ (uint32_t(rc) * 0x11111111u)) | isN)) & vmask;
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m |= ((eq >> (4 * j)) & 1u) << (7 - j);
+        const uint32_t m1 = __builtin_amdgcn_mov_dpp(int(m), 0x55, 0xf, 0xf, false);   // quad_perm [1,1,1,1]
+        const uint32_t m2 = __builtin_amdgcn_mov_dpp(int(m), 0xaa, 0xf, 0xf, false);   // quad_perm [2,2,2,2]
+        const uint32_t m3 = __builtin_amdgcn_mov_dpp(int(m), 0xff, 0xf, 0xf, false);   // quad_perm [3,3,3,3]
+        word[rc] = (m << 24) | (m1 << 16) | (m2 << 8) | m3;
+    }
+    const int w = base / 32 + (lane >> 2);
+    if ((lane & 3) == 0 && w < nw) {
+#pragma unroll
+        for (int rc = 0; rc < 5; ++rc) o[(kHapLead + w) * 5 + rc] = word[rc];
     }
 }
 
-// One wave per read (grid-stride). rdesc: {row offset, length, constant gap
-// qualities or -1, offset of the read's rows in the i/d/c planes when they vary}.
-__device__ __forceinline__ void pack_reads(const uint8_t* __restrict__ bases, const uint8_t* __restrict__ quals,
-                                           const uint8_t* __restrict__ gaps, long long gap_stride,
-                                           const int4* __restrict__ rdesc, int nreads, uint32_t* __restrict__ rows)
+// Zero rows of a table: kHapLead before the data, one after.
+__device__ __forceinline__ void hap_zero_rows(int nw, uint32_t* __restrict__ o, int lane)
 {
-    const int lane = threadIdx.x & 63;
-    for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < nreads; r += gridDim.x * 4) {
-        const int4 d = rdesc[r];
-        const int off = __builtin_amdgcn_readfirstlane(d.x), len = __builtin_amdgcn_readfirstlane(d.y);
-        const int gw = __builtin_amdgcn_readfirstlane(d.z), goff = __builtin_amdgcn_readfirstlane(d.w);
-        const uint8_t* g = gaps + goff;
-        pack_read(bases + off, quals + off, g, g + gap_stride, g + 2 * gap_stride, len, gw, rows + off, lane);
-    }
-}
-
-// Match table of one haplotype (a wave): row w + kHapLead holds columns
-// 32w+1 .. 32w+32; lanes 0-31 take the columns of row w, lanes 32-63 those of
-// row w+1, and the wave ballot of "hap base matches read code rc" gives both
-// rows' words for rc at once (bit-reversed: column 1 is the MSB).
-__device__ __forceinline__ void hap_table(const uint8_t* __restrict__ hb, int H, uint32_t* __restrict__ o, int lane)
-{
-    const int nw = (H + 31) / 32;
-    // Zero rows: kHapLead before the data, one after.
     if (lane < 5 * kHapLead) o[lane] = 0u;
     if (lane < 5) o[(kHapLead + nw) * 5 + lane] = 0u;
-    for (int w0 = 0; w0 < nw; w0 += 2) {
-        const int col = w0 * 32 + lane;   // 0-based hap column
-        const uint32_t hc = col < H ? base_code(hb[col]) : 7u;   // 7: past the hap, no match
-        uint32_t word = 0u;
-#pragma unroll
-        for (int rc = 0; rc < 5; ++rc) {
-            // read code rc matches: equal code, hap 'N' (matches every rc), or read 'N'
-            const bool m = hc != 7u && (hc == uint32_t(rc) || hc == 4u || rc == 4);
-            const uint64_t bl = __builtin_amdgcn_ballot_w64(m);
-            const uint32_t lo = __builtin_bitreverse32(uint32_t(bl)), hi = __builtin_bitreverse32(uint32_t(bl >> 32));
-            if (lane == rc) word = lo;
-            if (lane == 5 + rc) word = hi;
-        }
-        if (lane < 5) o[(kHapLead + w0) * 5 + lane] = word;
-        if (lane >= 5 && lane < 10 && w0 + 1 < nw) o[(kHapLead + w0 + 1) * 5 + lane - 5] = word;
-    }
 }
 
-// One wave per haplotype (grid-stride); haps[h] = {byte offset, H, table word offset, 0}.
-__device__ __forceinline__ void hap_tables(const uint8_t* __restrict__ hap_bytes, const int4* __restrict__ haps,
-                                           int nhaps, uint32_t* __restrict__ hapw)
+// Four row words from a record: qualities q4 (byte j = row 4t + j), codes c4
+// (nibble j), and the i / d / c planes' bytes when the gaps vary (gw < 0).
+__device__ __forceinline__ uint4 rows_rec4(uint32_t q4, uint32_t c4, uint32_t i4, uint32_t d4, uint32_t g4, int gw,
+                                           bool first)
+{
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t q = (q4 >> (8 * j)) & 127u, code = ((c4 >> (4 * j)) & 15u) << 28;
+        w[j] = gw >= 0 ? q | (uint32_t(gw) << 7) | code
+                       : q | (((i4 >> (8 * j)) & 127u) << 7) | (((d4 >> (8 * j)) & 127u) << 14) |
+                             (((g4 >> (8 * j)) & 127u) << 21) | code;
+    }
+    if (first && gw >= 0) w[0] |= 0x80000000u;   // constant-gap tag on the read's first row
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// A staged part's reads and haps, wave per item (grid-stride): item i packs
+// read i's rows (4 per lane) and hap i's table (8 columns per lane) from the
+// staged qualities, gap planes and code nibbles. Both
+// descriptors, then the first chunk of both, are loaded before either is
+// used, and the next item's descriptors while this one is packed: a wave keeps
+// several HBM requests in flight instead of one dependent chain per read.
+__device__ __forceinline__ void pack_items(const PackArgs& a)
 {
     const int lane = threadIdx.x & 63;
-    for (int h = blockIdx.x * 4 + (threadIdx.x >> 6); h < nhaps; h += gridDim.x * 4) {
-        const int4 hd = haps[h];
-        const int off = __builtin_amdgcn_readfirstlane(hd.x), H = __builtin_amdgcn_readfirstlane(hd.y);
-        hap_table(hap_bytes + off, H, hapw + __builtin_amdgcn_readfirstlane(hd.z), lane);
+    const int n = max(a.nreads, a.nhaps);
+    const int stride = gridDim.x * 4;
+    int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int4 z4 = make_int4(0, 0, 0, 0);
+    int4 rdn = i < a.nreads ? a.rdesc[i] : z4;
+    int4 hdn = i < a.nhaps ? a.hdesc[i] : z4;
+    for (; i < n; i += stride) {
+        const int off = __builtin_amdgcn_readfirstlane(rdn.x), len = __builtin_amdgcn_readfirstlane(rdn.y);
+        const int gw = __builtin_amdgcn_readfirstlane(rdn.z), goff = __builtin_amdgcn_readfirstlane(rdn.w);
+        const int hoff = __builtin_amdgcn_readfirstlane(hdn.x), H = __builtin_amdgcn_readfirstlane(hdn.y);
+        const int tw = __builtin_amdgcn_readfirstlane(hdn.z);
+        const int in = i + stride;
+        rdn = in < a.nreads ? a.rdesc[in] : z4;
+        hdn = in < a.nhaps ? a.hdesc[in] : z4;
+        const uint16_t* __restrict__ b16 = reinterpret_cast<const uint16_t*>(a.bases + off / 2);
+        const uint32_t* __restrict__ q32 = reinterpret_cast<const uint32_t*>(a.quals + off);
+        const uint32_t* __restrict__ g32 = reinterpret_cast<const uint32_t*>(a.gaps + goff);
+        const uint32_t* __restrict__ h32 = reinterpret_cast<const uint32_t*>(a.hap_bytes + hoff);
+        const int gs4 = int(a.gap_stride >> 2);
+        uint32_t b4 = 0, q4 = 0, i4 = 0, d4 = 0, c4 = 0, hx = 0;
+        if (4 * lane < len) {
+            b4 = b16[lane];
+            q4 = q32[lane];
+            if (gw < 0) {
+                i4 = g32[lane];
+                d4 = g32[gs4 + lane];
+                c4 = g32[2 * gs4 + lane];
+            }
+        }
+        if (8 * lane < H) hx = h32[lane];
+        // rows (len == 0: no read for this item)
+        uint4* __restrict__ rows = reinterpret_cast<uint4*>(a.rows + off);
+        for (int t0 = 0; 4 * t0 < len; t0 += 64) {
+            const int t = t0 + lane;
+            if (t0 > 0) {
+                if (4 * t < len) {
+                    b4 = b16[t];
+                    q4 = q32[t];
+                    if (gw < 0) {
+                        i4 = g32[t];
+                        d4 = g32[gs4 + t];
+                        c4 = g32[2 * gs4 + t];
+                    }
+                }
+            }
+            if (4 * t < len) rows[t] = rows_rec4(q4, b4, i4, d4, c4, gw, t == 0);
+        }
+        // table (H == 0: no hap for this item)
+        if (H > 0) {
+            uint32_t* __restrict__ o = a.hapw + tw;
+            const int nw = (H + 31) / 32;
+            hap_zero_rows(nw, o, lane);
+            for (int base = 0; base < H; base += 512) {
+                if (base > 0) hx = 8 * lane + base < H ? h32[base / 8 + lane] : 0u;
+                hap_words(hx, H - base - 8 * lane, base, nw, o, lane);
+            }
+        }
     }
 }
 
@@ -170,48 +213,18 @@ __device__ __forceinline__ void grid_waves(const GridSeg* __restrict__ segs, int
     }
 }
 
-__global__ __launch_bounds__(256) void grid_pairs_kernel(const GridBlock* __restrict__ blocks, int nblocks,
-                                                         long long npairs, const int4* __restrict__ rdesc,
-                                                         const int4* __restrict__ hdesc, PairDesc* __restrict__ pairs)
-{
-    grid_pairs(blocks, nblocks, npairs, rdesc, hdesc, pairs);
-}
-
-__global__ __launch_bounds__(256) void grid_waves_kernel(const GridSeg* __restrict__ segs, int nsegs,
-                                                         long long nslots, int nwaves, const int* __restrict__ rord,
-                                                         const int* __restrict__ hord, const int4* __restrict__ rdesc,
-                                                         int* __restrict__ order, LaneWave* __restrict__ waves)
-{
-    grid_waves(segs, nsegs, nslots, nwaves, rord, hord, rdesc, order, waves);
-}
-
-__global__ __launch_bounds__(256) void pack_reads_kernel(const uint8_t* __restrict__ bases,
-                                                         const uint8_t* __restrict__ quals,
-                                                         const uint8_t* __restrict__ gaps, long long gap_stride,
-                                                         const int4* __restrict__ rdesc, int nreads,
-                                                         uint32_t* __restrict__ rows)
-{
-    pack_reads(bases, quals, gaps, gap_stride, rdesc, nreads, rows);
-}
-
-__global__ __launch_bounds__(256) void hap_tables_kernel(const uint8_t* __restrict__ hap_bytes,
-                                                         const int4* __restrict__ haps, int nhaps,
-                                                         uint32_t* __restrict__ hapw)
-{
-    hap_tables(hap_bytes, haps, nhaps, hapw);
-}
-
 // Everything a structured (region) part needs before its pass, in one launch
 // (each step is a grid-stride loop over its own items; none reads another's
 // output): the run counters zeroed, reads packed, hap tables, pair
 // descriptors, slot order and waves — four fewer launches per region call.
+__global__ __launch_bounds__(256) void pack_batch_kernel(PackArgs a) { pack_items(a); }
+
 __global__ __launch_bounds__(256) void prepare_grid_kernel(GridPrepArgs a)
 {
     if (blockIdx.x == 0 && threadIdx.x < kNumCounters) a.counters[threadIdx.x] = 0;
-    pack_reads(a.bases, a.quals, a.gaps, a.gap_stride, a.rdesc, a.nreads, a.rows);
-    hap_tables(a.hap_bytes, a.hdesc, a.nhaps, a.hapw);
-    grid_pairs(a.blocks, a.nblocks, a.npairs, a.rdesc, a.hdesc, a.pairs);
-    grid_waves(a.segs, a.nsegs, a.nslots, a.nwaves, a.rord, a.hord, a.rdesc, a.order, a.waves);
+    pack_items(a.pack);
+    grid_pairs(a.blocks, a.nblocks, a.npairs, a.pack.rdesc, a.pack.hdesc, a.pairs);
+    grid_waves(a.segs, a.nsegs, a.nslots, a.nwaves, a.rord, a.hord, a.pack.rdesc, a.order, a.waves);
 }
 
 // ---------------------------------------------------------------------------
@@ -223,75 +236,6 @@ __global__ __launch_bounds__(256) void prepare_grid_kernel(GridPrepArgs a)
 // vary, then the hap's base codes as nibbles; every field 4-byte aligned.
 __host__ __device__ constexpr int align4(int x) { return (x + 3) & ~3; }
 
-// Rows of one read from its record, four rows per lane (one 32-bit load of
-// qualities, one 16-bit load of codes, one 128-bit store).
-__device__ __forceinline__ void pack_read_rec(const uint8_t* __restrict__ quals, const uint8_t* __restrict__ codes,
-                                              const uint8_t* __restrict__ gaps, int R, int gw,
-                                              uint32_t* __restrict__ rows, int lane)
-{
-    const int qa = align4(R);
-    for (int t = lane; 4 * t < R; t += 64) {
-        const uint32_t q4 = reinterpret_cast<const uint32_t*>(quals)[t];
-        const uint32_t c4 = reinterpret_cast<const uint16_t*>(codes)[t];
-        uint32_t w[4];
-        if (gw >= 0) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                w[j] = ((q4 >> (8 * j)) & 127u) | (uint32_t(gw) << 7) | (((c4 >> (4 * j)) & 15u) << 28);
-            if (t == 0) w[0] |= 0x80000000u;   // constant-gap tag on the read's first row
-        } else {
-            const uint32_t i4 = reinterpret_cast<const uint32_t*>(gaps)[t];
-            const uint32_t d4 = reinterpret_cast<const uint32_t*>(gaps + qa)[t];
-            const uint32_t g4 = reinterpret_cast<const uint32_t*>(gaps + 2 * qa)[t];
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                w[j] = ((q4 >> (8 * j)) & 127u) | (((i4 >> (8 * j)) & 127u) << 7) | (((d4 >> (8 * j)) & 127u) << 14) |
-                       (((g4 >> (8 * j)) & 127u) << 21) | (((c4 >> (4 * j)) & 15u) << 28);
-        }
-        reinterpret_cast<uint4*>(rows)[t] = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-}
-
-// Nibbles equal to zero (values <= 7): bit 0 of each such nibble.
-__device__ __forceinline__ uint32_t zero_nibbles(uint32_t t) { return ~(t | (t >> 1) | (t >> 2)) & 0x11111111u; }
-
-// Match table of one hap from its code nibbles: a lane takes 8 columns (one
-// 32-bit load), forms for each read code the 8 match bits (MSB first), and
-// each quad of lanes joins its four bytes into one table word (DPP
-// quad_perm): 512 columns per wave step.
-__device__ __forceinline__ void hap_table_rec(const uint8_t* __restrict__ hc, int H, uint32_t* __restrict__ o, int lane)
-{
-    const int nw = (H + 31) / 32;
-    if (lane < 5 * kHapLead) o[lane] = 0u;
-    if (lane < 5) o[(kHapLead + nw) * 5 + lane] = 0u;
-    const uint32_t* __restrict__ h32 = reinterpret_cast<const uint32_t*>(hc);
-    for (int base = 0; base < H; base += 512) {
-        const int col0 = base + 8 * lane;
-        const int nv = H - col0;   // valid columns of this lane (<= 0: none)
-        const uint32_t x = nv > 0 ? h32[base / 8 + lane] : 0u;
-        const uint32_t vmask = nv >= 8 ? 0x11111111u : (nv > 0 ? 0x11111111u & ((1u << (4 * nv)) - 1u) : 0u);
-        const uint32_t isN = zero_nibbles(x ^ 0x44444444u);
-        uint32_t word[5];
-#pragma unroll
-        for (int rc = 0; rc < 5; ++rc) {
-            // read code rc matches: equal code, hap 'N' (matches every rc), or read 'N'
-            const uint32_t eq = (rc == 4 ? 0x11111111u : (zero_nibbles(x ^ (uint32_t(rc) * 0x11111111u)) | isN)) & vmask;
-            uint32_t m = 0;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) m |= ((eq >> (4 * j)) & 1u) << (7 - j);
-            const uint32_t m1 = __builtin_amdgcn_mov_dpp(int(m), 0x55, 0xf, 0xf, false);   // quad_perm [1,1,1,1]
-            const uint32_t m2 = __builtin_amdgcn_mov_dpp(int(m), 0xaa, 0xf, 0xf, false);   // quad_perm [2,2,2,2]
-            const uint32_t m3 = __builtin_amdgcn_mov_dpp(int(m), 0xff, 0xf, 0xf, false);   // quad_perm [3,3,3,3]
-            word[rc] = (m << 24) | (m1 << 16) | (m2 << 8) | m3;
-        }
-        const int w = base / 32 + (lane >> 2);
-        if ((lane & 3) == 0 && w < nw) {
-#pragma unroll
-            for (int rc = 0; rc < 5; ++rc) o[(kHapLead + w) * 5 + rc] = word[rc];
-        }
-    }
-}
-
 // One wave per pair (grid-stride): its rows, its hap table, its pair
 // descriptor, and its plan key — the cheaper of its two (block width, lanes)
 // candidates by the host planner's cost model, and the counting-sort bin of
@@ -300,21 +244,62 @@ __global__ __launch_bounds__(256) void flat_prep_kernel(FlatPlanArgs a)
 {
     if (blockIdx.x == 0 && threadIdx.x < kNumCounters) a.counters[threadIdx.x] = 0;
     const int lane = threadIdx.x & 63;
-    for (int p = blockIdx.x * 4 + (threadIdx.x >> 6); p < a.n; p += gridDim.x * 4) {
-        const FlatDesc d = a.desc[p];
-        const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(d.rec & 0xffffffffll));
-        const unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(d.rec >> 32));
+    const int stride = gridDim.x * 4;
+    int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+    FlatDesc dn{};
+    if (p < a.n) dn = a.desc[p];
+    // As pack_items: the record's first chunk (rows and hap columns) is loaded
+    // before either is used and the next pair's descriptor while this one packs.
+    for (; p < a.n; p += stride) {
+        const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(dn.rec & 0xffffffffll));
+        const unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(dn.rec >> 32));
         const uint8_t* quals = a.img + (long long)(((unsigned long long)hi << 32) | lo);
-        const int R = __builtin_amdgcn_readfirstlane(d.R), H = __builtin_amdgcn_readfirstlane(d.H);
-        const int ro = __builtin_amdgcn_readfirstlane(d.row_off), ho = __builtin_amdgcn_readfirstlane(d.hapw_off);
-        const int gw = __builtin_amdgcn_readfirstlane(d.gapw);
-        const uint8_t* codes = quals + align4(R);
-        const uint8_t* gaps = codes + align4((R + 1) / 2);
-        pack_read_rec(quals, codes, gaps, R, gw, a.rows + ro, lane);
-        hap_table_rec(gaps + (gw < 0 ? 3 * align4(R) : 0), H, a.hapw + ho, lane);
+        const int R = __builtin_amdgcn_readfirstlane(dn.R), H = __builtin_amdgcn_readfirstlane(dn.H);
+        const int ro = __builtin_amdgcn_readfirstlane(dn.row_off), ho = __builtin_amdgcn_readfirstlane(dn.hapw_off);
+        const int gw = __builtin_amdgcn_readfirstlane(dn.gapw);
+        if (p + stride < a.n) dn = a.desc[p + stride];
+        const int qa = align4(R);
+        const uint32_t* __restrict__ q32 = reinterpret_cast<const uint32_t*>(quals);
+        const uint16_t* __restrict__ c16 = reinterpret_cast<const uint16_t*>(quals + qa);
+        const uint32_t* __restrict__ g32 = reinterpret_cast<const uint32_t*>(quals + qa + align4((R + 1) / 2));
+        const uint32_t* __restrict__ h32 = g32 + (gw < 0 ? 3 * (qa >> 2) : 0);
+        const int qa4 = qa >> 2;
+        uint32_t q4 = 0, c4 = 0, i4 = 0, d4 = 0, g4 = 0, hx = 0;
+        if (4 * lane < R) {
+            q4 = q32[lane];
+            c4 = c16[lane];
+            if (gw < 0) {
+                i4 = g32[lane];
+                d4 = g32[qa4 + lane];
+                g4 = g32[2 * qa4 + lane];
+            }
+        }
+        if (8 * lane < H) hx = h32[lane];
+        const int2 c = a.ctab[H];
+        uint4* __restrict__ rows = reinterpret_cast<uint4*>(a.rows + ro);
+        for (int t0 = 0; 4 * t0 < R; t0 += 64) {
+            const int t = t0 + lane;
+            if (t0 > 0 && 4 * t < R) {
+                q4 = q32[t];
+                c4 = c16[t];
+                if (gw < 0) {
+                    i4 = g32[t];
+                    d4 = g32[qa4 + t];
+                    g4 = g32[2 * qa4 + t];
+                }
+            }
+            if (4 * t < R) rows[t] = rows_rec4(q4, c4, i4, d4, g4, gw, t == 0);
+        }
+        uint32_t* __restrict__ o = a.hapw + ho;
+        const int nw = (H + 31) / 32;
+        hap_zero_rows(nw, o, lane);
+        for (int base = 0; base < H; base += 512) {
+            const int nv = H - base - 8 * lane;   // valid columns of this lane (<= 0: none)
+            if (base > 0) hx = nv > 0 ? h32[base / 8 + lane] : 0u;
+            hap_words(hx, nv, base, nw, o, lane);
+        }
         if (lane == 0) {
             a.pairs[p] = make_int4(ro, R, ho, H);
-            const int2 c = a.ctab[H];
             // modelled wave instructions of each candidate (plan_model.hpp seg_cost)
             const int bc0 = c.x & 0xff, nb0 = (c.x >> 8) & 0xff, bc1 = c.y & 0xff, nb1 = (c.y >> 8) & 0xff;
             const float k0 = float((long long)nb0 * (13 * bc0 + 26) * (R + nb0 - 1)) * a.waste[nb0];
@@ -421,8 +406,74 @@ __global__ __launch_bounds__(256) void flat_waves_kernel(FlatPlanArgs a)
         v.npairs = s1 - s0;
         v.nsteps = rmax + g.y - 1;
         v.carry_row = 0;
-        a.waves[w] = v;
+        (a.tail > 0 ? a.waves_tmp : a.waves)[w] = v;
     }
+}
+
+// Dispatch order (one workgroup), as the host planner's (planner.cpp): the
+// bulk in packing order (co-resident waves share one width's code), the
+// `tail` shortest waves (modelled duration BC x steps, in 1024 buckets) last,
+// longest first, so the chip drains evenly; order inside a bucket arbitrary.
+__global__ __launch_bounds__(1024) void flat_tail_kernel(FlatPlanArgs a)
+{
+    constexpr int NB = 1024;
+    __shared__ int hist[NB], cur[NB], part[1024];
+    __shared__ int cmax_s, thr_s;
+    const int t = threadIdx.x;
+    const int nw = *a.nwaves;
+    const LaneWave* __restrict__ in = a.waves_tmp;
+    hist[t] = 0;
+    if (t == 0) cmax_s = 1;
+    __syncthreads();
+    const int C = (nw + 1023) / 1024;
+    const int w0 = min(nw, t * C), w1 = min(nw, w0 + C);
+    int m = 1;
+    for (int w = w0; w < w1; ++w) m = max(m, in[w].ncols * in[w].nsteps);
+    atomicMax(&cmax_s, m);
+    __syncthreads();
+    const long long cm = cmax_s;
+    auto bucket = [&](const LaneWave& v) { return int((long long)(v.ncols * v.nsteps) * (NB - 1) / cm); };
+    for (int w = w0; w < w1; ++w) atomicAdd(&hist[bucket(in[w])], 1);
+    __syncthreads();
+    if (t == 0) {   // the smallest bucket threshold holding at least `tail` waves below it
+        int acc = 0, thr = 0;
+        while (thr < NB && acc < a.tail) acc += hist[thr++];
+        thr_s = acc >= nw ? 0 : thr;   // nothing to gain when every wave is in the tail
+        int off = 0;   // tail buckets longest first
+        for (int b = thr_s - 1; b >= 0; --b) {
+            cur[b] = off;
+            off += hist[b];
+        }
+    }
+    __syncthreads();
+    const int thr = thr_s;
+    // the bulk (bucket >= thr) in packing order: chunk counts, block scan
+    int mine = 0;
+    for (int w = w0; w < w1; ++w) mine += bucket(in[w]) >= thr;
+    part[t] = mine;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    const int nbulk = part[1023];
+    int pos = part[t] - mine;
+    for (int w = w0; w < w1; ++w) {
+        const LaneWave v = in[w];
+        const int bk = bucket(v);
+        if (bk >= thr)
+            a.waves[pos++] = v;
+        else
+            a.waves[nbulk + atomicAdd(&cur[bk], 1)] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void store_to_host_kernel(uint4* __restrict__ host, const uint4* __restrict__ dev,
+                                                            long long n16)
+{
+    for (long long k = blockIdx.x * 256ll + threadIdx.x; k < n16; k += 256ll * gridDim.x) host[k] = dev[k];
 }
 
 int grid_for(long long waves)
@@ -433,47 +484,30 @@ int grid_for(long long waves)
 
 }  // namespace
 
-hipError_t launch_pack_reads(const uint8_t* bases, const uint8_t* quals, const uint8_t* gaps, long long gap_stride,
-                             const int4* rdesc, int nreads, uint32_t* rows, hipStream_t s)
+hipError_t launch_pack_batch(const PackArgs& a, hipStream_t s)
 {
-    if (nreads <= 0) return hipSuccess;
-    hipLaunchKernelGGL(pack_reads_kernel, dim3(grid_for(nreads)), dim3(256), 0, s, bases, quals, gaps, gap_stride,
-                       rdesc, nreads, rows);
-    return hipGetLastError();
-}
-
-hipError_t launch_hap_tables(const uint8_t* hap_bytes, const int4* haps, int nhaps, uint32_t* hapw, hipStream_t s)
-{
-    if (nhaps <= 0) return hipSuccess;
-    hipLaunchKernelGGL(hap_tables_kernel, dim3(grid_for(nhaps)), dim3(256), 0, s, hap_bytes, haps, nhaps, hapw);
-    return hipGetLastError();
-}
-
-hipError_t launch_grid_pairs(const GridBlock* blocks, int nblocks, long long npairs, const int4* rdesc,
-                             const int4* hdesc, PairDesc* pairs, hipStream_t s)
-{
-    if (npairs <= 0 || nblocks <= 0) return hipSuccess;
-    const long long g = (npairs + 255) / 256;
-    hipLaunchKernelGGL(grid_pairs_kernel, dim3(unsigned(g < 8192 ? g : 8192)), dim3(256), 0, s, blocks, nblocks, npairs,
-                       rdesc, hdesc, pairs);
-    return hipGetLastError();
-}
-
-hipError_t launch_grid_waves(const GridSeg* segs, int nsegs, long long nslots, int nwaves, const int* rord,
-                             const int* hord, const int4* rdesc, int* order, LaneWave* waves, hipStream_t s)
-{
-    if (nsegs <= 0 || (nslots <= 0 && nwaves <= 0)) return hipSuccess;
-    const long long g = (nslots + 255) / 256;
-    hipLaunchKernelGGL(grid_waves_kernel, dim3(unsigned(g < 4096 ? (g > 0 ? g : 1) : 4096)), dim3(256), 0, s, segs,
-                       nsegs, nslots, nwaves, rord, hord, rdesc, order, waves);
+    const int items = std::max(a.nreads, a.nhaps);
+    if (items <= 0) return hipSuccess;
+    hipLaunchKernelGGL(pack_batch_kernel, dim3(grid_for(items)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_prepare_grid(const GridPrepArgs& a, hipStream_t s)
 {
-    const long long items = std::max<long long>({(long long)a.nreads, (long long)a.nhaps, a.npairs / 64, a.nslots / 64, 1});
+    const long long items =
+        std::max<long long>({(long long)a.pack.nreads, (long long)a.pack.nhaps, a.npairs / 64, a.nslots / 64, 1});
     const int grid = grid_for(items);
     hipLaunchKernelGGL(prepare_grid_kernel, dim3(grid), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_store_to_host(void* host, const void* dev, size_t bytes, hipStream_t s)
+{
+    const long long n16 = (long long)(bytes / 16);
+    if (n16 <= 0) return hipSuccess;
+    const long long g = std::min<long long>(1024, (n16 + 255) / 256);
+    hipLaunchKernelGGL(store_to_host_kernel, dim3(unsigned(g)), dim3(256), 0, s, static_cast<uint4*>(host),
+                       static_cast<const uint4*>(dev), n16);
     return hipGetLastError();
 }
 
@@ -488,6 +522,7 @@ hipError_t launch_flat_plan(const FlatPlanArgs& a, hipStream_t s)
     hipLaunchKernelGGL(flat_scatter_kernel, dim3(gs), dim3(256), 0, s, a);
     const int gw = std::max(1, std::min(8192, (a.max_waves + 255) / 256));
     hipLaunchKernelGGL(flat_waves_kernel, dim3(gw), dim3(256), 0, s, a);
+    if (a.tail > 0) hipLaunchKernelGGL(flat_tail_kernel, dim3(1), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 

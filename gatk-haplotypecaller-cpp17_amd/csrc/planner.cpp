@@ -392,8 +392,10 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     int32_t* gapw = S.gapw.data();
     int32_t* hlen = S.hlen.data();
     std::atomic<int> bad_read{0}, bad_hap{0}, rlen_max{0};
+    std::atomic<int64_t> rows_sum{0};
     parallel_for(nr, [&](int64_t lo, int64_t hi) {
         int rm = 0;
+        int64_t rs = 0;
         for (int64_t r = lo; r < hi; ++r) {
             const ReadView v = src.read(loc.read_id(r));
             if (v.len <= 0 || v.len > HC_PHMM_MAX_READ_LEN || !v.bases || !v.q || !v.i || !v.d || !v.c) {
@@ -404,9 +406,11 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             }
             rlen[size_t(r)] = v.len;
             rm = std::max(rm, v.len);
+            rs += v.len;
             gapw[size_t(r)] = constant_gaps(v) ? int32_t((v.i[0] & 127) | ((v.d[0] & 127) << 7) | ((v.c[0] & 127) << 14))
                                                : -1;
         }
+        rows_sum.fetch_add(rs);
         int cur = rlen_max.load();
         while (rm > cur && !rlen_max.compare_exchange_weak(cur, rm)) {
         }
@@ -423,12 +427,15 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     if (bad_hap.load())
         return fail(HC_PHMM_EINVAL, "haplotype with invalid length (1.." + std::to_string(HC_PHMM_MAX_HAP_LEN) +
                                         ") or null bases");
-    // rows / irregular gap rows / table words / hap bytes
+    // rows / irregular gap rows / table words / hap code bytes. Bases and hap
+    // bases are staged as ConvertChar codes, two per byte; a read's rows start
+    // at a multiple of 4, a hap's codes at a multiple of 8 columns: the packer
+    // loads 4 rows / 8 hap columns per lane (launch_pack_batch).
     std::vector<int64_t>&row_off = S.row_off, &gap_off = S.gap_off, &hap_w = S.hap_w, &hap_b = S.hap_b;
-    prefix_sum(nr, row_off, [&](int64_t r) -> int64_t { return rlen[size_t(r)]; });
-    prefix_sum(nr, gap_off, [&](int64_t r) -> int64_t { return gapw[size_t(r)] < 0 ? rlen[size_t(r)] : 0; });
+    prefix_sum(nr, row_off, [&](int64_t r) -> int64_t { return (rlen[size_t(r)] + 3) & ~3; });
+    prefix_sum(nr, gap_off, [&](int64_t r) -> int64_t { return gapw[size_t(r)] < 0 ? (rlen[size_t(r)] + 3) & ~3 : 0; });
     prefix_sum(nh, hap_w, [&](int64_t h) -> int64_t { return hap_table_words(hlen[size_t(h)]); });
-    prefix_sum(nh, hap_b, [&](int64_t h) -> int64_t { return hlen[size_t(h)]; });
+    prefix_sum(nh, hap_b, [&](int64_t h) -> int64_t { return ((hlen[size_t(h)] + 7) & ~7) / 2; });
     const int64_t nrows = row_off[size_t(nr)], ngap = gap_off[size_t(nr)];
     if (nrows > INT32_MAX || hap_w[size_t(nh)] > INT32_MAX || hap_b[size_t(nh)] > INT32_MAX || ngap > INT32_MAX)
         return fail(HC_PHMM_EINVAL, "batch too large (row or hap pool exceeds 2^31)");
@@ -440,7 +447,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const size_t o_rd = U.take(sizeof(int4) * size_t(nr));
     const size_t o_hd = U.take(sizeof(int4) * size_t(nh));
     const size_t o_ord = U.take(sizeof(int) * size_t(npairs));
-    const size_t o_bases = U.take(size_t(nrows) + 16);
+    const size_t o_bases = U.take(size_t(nrows) / 2 + 16);
     const size_t o_quals = U.take(size_t(nrows) + 16);
     const size_t gap_stride = (size_t(ngap) + 16 + 15) & ~size_t(15);
     const size_t o_gaps = U.take(ngap ? 3 * gap_stride : 0);
@@ -454,7 +461,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const size_t n1 = size_t(std::max<int64_t>(npairs, 1));
     const size_t res_o64 = (sizeof(float) * n1 + 255) & ~size_t(255);
     const size_t res_ofl = res_o64 + ((sizeof(double) * n1 + 255) & ~size_t(255));
-    const size_t res_bytes = res_ofl + n1;
+    const size_t res_bytes = (res_ofl + n1 + 15) & ~size_t(15);   // whole 16-byte stores (launch_store_to_host)
     const size_t host_upload_cap = o_lw + waves_max;
     const size_t host_res_off = (host_upload_cap + 255) & ~size_t(255);
     char* host = nullptr;
@@ -494,7 +501,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     std::atomic<int64_t> wide_a{0};
     std::atomic<int> hmax_a{0};
     // Modelled wave instructions at each cap (plan_model.hpp), for the cap choice.
-    const double ravg = double(nrows) / double(std::max<int64_t>(nr, 1));
+    const double ravg = double(rows_sum.load()) / double(std::max<int64_t>(nr, 1));
     std::mutex work_mu;
     std::array<int64_t, kNCaps> lanes_at{};
     std::array<double, kNCaps> work_at{};
@@ -898,7 +905,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         for (int64_t r = b; r < e; ++r) {
             const ReadView v = src.read(loc.read_id(r));
             const size_t o = size_t(row_off[size_t(r)]);
-            std::memcpy(hb + o, v.bases, size_t(v.len));
+            pack_nibbles(v.bases, v.len, hb + o / 2);
             std::memcpy(hq + o, v.q, size_t(v.len));
             const int32_t g = gapw[size_t(r)];
             int go = 0;
@@ -916,7 +923,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     parallel_for(nh, [&](int64_t b, int64_t e) {
         for (int64_t h = b; h < e; ++h) {
             const HapView v = src.hapv(loc.hap_id(h));
-            std::memcpy(hbytes + hap_b[size_t(h)], v.bases, size_t(v.len));
+            pack_nibbles(v.bases, v.len, hbytes + hap_b[size_t(h)]);
             hdesc[h] = make_int4(int(hap_b[size_t(h)]), v.len, int(hap_w[size_t(h)]), 0);
         }
     }, 256);
@@ -1051,6 +1058,18 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         b->join = dv.join;
     }
     hipStream_t s = b->stream;
+    PackArgs pack{};
+    pack.bases = reinterpret_cast<const uint8_t*>(dev + o_bases);
+    pack.quals = reinterpret_cast<const uint8_t*>(dev + o_quals);
+    pack.gaps = reinterpret_cast<const uint8_t*>(dev + o_gaps);
+    pack.gap_stride = (long long)gap_stride;
+    pack.rdesc = reinterpret_cast<const int4*>(dev + o_rd);
+    pack.nreads = int(nr);
+    pack.rows = b->d_rows;
+    pack.hap_bytes = reinterpret_cast<const uint8_t*>(dev + o_hb);
+    pack.hdesc = reinterpret_cast<const int4*>(dev + o_hd);
+    pack.nhaps = int(nh);
+    pack.hapw = b->d_hapw;
     auto enqueue = [&]() -> int {
         if (!b->slot_ev)
             for (auto& e : b->pack_ev) HIP_TRY(hipEventCreate(&e));
@@ -1063,17 +1082,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             HIP_TRY(hipMemcpyAsync(dev + o_gb, host + o_gb, upload - o_gb, hipMemcpyHostToDevice, s));
             HIP_TRY(hipEventRecord(b->pack_ev[0], s));
             GridPrepArgs g{};
-            g.bases = reinterpret_cast<const uint8_t*>(dev + o_bases);
-            g.quals = reinterpret_cast<const uint8_t*>(dev + o_quals);
-            g.gaps = reinterpret_cast<const uint8_t*>(dev + o_gaps);
-            g.gap_stride = (long long)gap_stride;
-            g.rdesc = reinterpret_cast<const int4*>(dev + o_rd);
-            g.nreads = int(nr);
-            g.rows = b->d_rows;
-            g.hap_bytes = reinterpret_cast<const uint8_t*>(dev + o_hb);
-            g.hdesc = reinterpret_cast<const int4*>(dev + o_hd);
-            g.nhaps = int(nh);
-            g.hapw = b->d_hapw;
+            g.pack = pack;
             g.blocks = reinterpret_cast<const GridBlock*>(dev + o_gb);
             g.nblocks = int(spec.blocks.size());
             g.npairs = (long long)npairs;
@@ -1093,12 +1102,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             HIP_TRY(hipMemcpyAsync(dev + up0, host + up0, upload - up0, hipMemcpyHostToDevice, s));
             HIP_TRY(hipMemsetAsync(b->d_count, 0, kNumCounters * sizeof(int), s));
             HIP_TRY(hipEventRecord(b->pack_ev[0], s));
-            HIP_TRY(launch_pack_reads(reinterpret_cast<const uint8_t*>(dev + o_bases),
-                                      reinterpret_cast<const uint8_t*>(dev + o_quals),
-                                      reinterpret_cast<const uint8_t*>(dev + o_gaps), (long long)gap_stride,
-                                      reinterpret_cast<const int4*>(dev + o_rd), int(nr), b->d_rows, s));
-            HIP_TRY(launch_hap_tables(reinterpret_cast<const uint8_t*>(dev + o_hb),
-                                      reinterpret_cast<const int4*>(dev + o_hd), int(nh), b->d_hapw, s));
+            HIP_TRY(launch_pack_batch(pack, s));
             HIP_TRY(hipEventRecord(b->pack_ev[1], s));
         }
         if (with_run) {

@@ -166,7 +166,7 @@ int run_part(Part* b, hipStream_t s)
 
 int enqueue_results(Part* b, hipStream_t s)
 {
-    HIP_TRY(hipMemcpyAsync(b->host_res, b->own_raw32, b->res_bytes, hipMemcpyDeviceToHost, s));
+    HIP_TRY(launch_store_to_host(b->host_res, b->own_raw32, b->res_bytes, s));
     if (!b->done) HIP_TRY(hipEventCreateWithFlags(&b->done, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(b->done, s));
     return HC_PHMM_OK;
