@@ -299,7 +299,7 @@ void scan_pass(const Src& src, int64_t lo, int64_t n, bool scan_gaps, Mini* mini
                 M.rmin = std::min(M.rmin, R);
                 M.hmax = std::max(M.hmax, H);
                 M.hmin = std::min(M.hmin, H);
-                M.nwide += H > 64 * 32;
+                M.nwide += H > kSeg64MaxH;
                 if (k % stride == 0) hsamp[k / stride] = H;
             }
         }

@@ -522,7 +522,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
                 cl = H > kW64Threshold ? 3 : 2;
             hc[h] = uint8_t(cl);
             hm = std::max(hm, H);
-            w += H > 64 * 32 ? loc.hap_mult(h) : 0;
+            w += H > kSeg64MaxH ? loc.hap_mult(h) : 0;
         }
         wide_a += w;
         int cur = hmax_a.load();

@@ -310,6 +310,50 @@ def test_fp64_rescue_tiers(engine, oracle_lib, monkeypatch, shape, in_wave):
     assert_same(res, ref, shape)
 
 
+@pytest.mark.parametrize("chain", [2, 3, 16])
+def test_fp64_chained_rescue_forced(engine, oracle_lib, monkeypatch, chain):
+    """Chained fp64 waves (lane_kernel.hip run_chain): the rescued pairs of the
+    32- and 64-lane classes run back to back per lane group, each lane starting
+    the next pair's row 1 the step after its previous row R. Forced here on a
+    list too short to chain by itself; reads of 20-250 bases against haps of
+    520-2048 put some pairs in unchained classes (a read not longer than its
+    slot) next to the chained ones, and leave partial chains and groups."""
+    monkeypatch.setenv("HC_PHMM_RESCUE_IN_WAVE", "0")
+    monkeypatch.setenv("HC_PHMM_RESCUE_CHAIN", str(chain))
+    b = W.generate(900, (520, 2048), (20, 250), 0.08, seed=29)
+    ref = oracle_lib.pairs(b, nthreads=16)
+    assert ref["rescued"].sum() > 450
+    bt = engine.Batch(b)
+    for _ in range(2):   # the second run reuses the plan buffers and counters
+        bt.run()
+        assert_same(bt.results(), ref, f"chain {chain}")
+    assert bt.stats().rescue_chain == chain
+    bt.close()
+
+
+def test_fp64_chained_rescue_s4_20k(engine, oracle_lib, monkeypatch):
+    """configs[4] at 20 000 pairs: the rescue list is long
+    enough to chain by itself. Same bits as the unchained pass
+    (HC_PHMM_RESCUE_CHAIN=0) on every pair, and a sample equals the oracle."""
+    b = W.config("S4", 20_000)
+    bt = engine.Batch(b)
+    bt.run()
+    res = bt.results()
+    assert bt.stats().rescue_chain >= 2
+    bt.close()
+    monkeypatch.setenv("HC_PHMM_RESCUE_CHAIN", "0")
+    bt = engine.Batch(b)
+    bt.run()
+    plain = bt.results()
+    assert bt.stats().rescue_chain == 0
+    bt.close()
+    for k in res:
+        assert np.array_equal(bits(res[k]), bits(plain[k])), k
+    assert res["rescued"].sum() > 15_000
+    idx = np.random.default_rng(31).choice(20_000, 300, replace=False)
+    assert_same({k: res[k][idx] for k in res}, oracle_lib.pairs(W.subset(b, idx), nthreads=16), "S4-20k")
+
+
 def test_in_wave_rescue_on_s2_shard(engine, oracle_lib):
     """S2's rare rescues (a 125k-pair shard: about two) are recomputed inside
     the fp32 pass by the waves that flag them: every rescued pair, plus a
