@@ -337,7 +337,7 @@ int gather_regions(const hc_phmm_region* regions, int32_t n_regions, RegionSet& 
 // C ABI
 extern "C" {
 
-int hc_phmm_version(void) { return 30100; }   // 3.1: hc_phmm_stats.rescue_chain
+int hc_phmm_version(void) { return 30000; }
 
 const char* hc_phmm_last_error(void) { return hcphmm::eng::last_error(); }
 
@@ -641,12 +641,8 @@ int hc_phmm_batch_stats(hc_phmm_batch* b, hc_phmm_stats* st)
             st->kernel_ms_f64 = std::max(st->kernel_ms_f64, sc / double(p->ev_used));
             st->run_ms = std::max(st->run_ms, (sa + sc) / double(p->ev_used));
             p->ev_used = 0;
-            int cnt[4] = {}, chain = 0;
+            int cnt[4] = {};
             HIP_TRY(hipMemcpy(cnt, p->d_count, sizeof(cnt), hipMemcpyDeviceToHost));
-            if (cnt[p->parity ^ 1] > 0) {   // an empty list's plan is not written past its wave total
-                HIP_TRY(hipMemcpy(&chain, &p->d_plan->chain, sizeof(chain), hipMemcpyDeviceToHost));
-                st->rescue_chain = std::max<int64_t>(st->rescue_chain, chain);
-            }
             // in-wave attempts past the limit were appended to the list instead
             st->n_rescued += cnt[p->parity ^ 1] + std::min(cnt[2 + (p->parity ^ 1)], p->inker_limit);
         }

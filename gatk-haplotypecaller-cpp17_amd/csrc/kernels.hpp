@@ -65,24 +65,16 @@ struct DiagArgs {
 // (lane_kernel.hip rescue_plan_kernel). A pair takes a slot of 2^k lanes
 // (64 >> k pairs per wave) and the narrowest fp64 block width that covers its
 // hap on those lanes, so the slot's lanes are all used: (k, width) is its
-// class. Long lists chain the pairs of the 2^k = 32 / 64-lane classes: a slot
-// runs `chain` pairs back to back, each lane starting the next pair's first
-// row the step after its last row of the previous one, so the pipeline skew
-// (2^k - 1 steps) is paid once per chain instead of once per pair. Classes are
-// numbered chained first, then widest slot and block first (the longest waves
+// class. Classes are numbered widest slot and block first (the longest waves
 // are dispatched first); the last class holds haps wider than 64 blocks of 32
 // (anti-diagonal kernel, through `big`).
 constexpr int kSeg64Widths = 7;   // fp64 block widths 8, 12, ..., 32
-constexpr int kSeg64ChainClasses = 2 * kSeg64Widths;   // k = 6, 5 chained
-constexpr int kSeg64Classes = kSeg64ChainClasses + 7 * kSeg64Widths + 1;
+constexpr int kSeg64Classes = 7 * kSeg64Widths + 1;
 constexpr int kSeg64MaxH = 64 * 32;   // longer haps: anti-diagonal fp64 kernel (host n_wide)
-constexpr int kSeg64ChainMax = 16;    // pairs per chain
 __host__ __device__ constexpr int seg64_width(int wi) { return 8 + 4 * wi; }
 struct Seg64Plan {
     int bc0;                        // block width bound of the pass (32, or 16 / 8 for short lists)
     int dynamic;                    // waves fetched from a counter (more than two per SIMD)
-    int chain;                      // longest chain of the pass (0: unchained)
-    int chain_len[kSeg64ChainClasses];   // pairs per chain of each chained class
     int n_class[kSeg64Classes];
     int off_class[kSeg64Classes];   // class c's entries in `sorted` start here
     int wave_base[kSeg64Classes];   // first wave of class c; [last] = total waves
@@ -105,8 +97,6 @@ struct Seg64Args {
     int* wave_order;          // dispatch position -> wave (n entries), see rescue_plan_kernel
     int* next_wave;           // dynamic wave counter (zeroed by the plan)
     int n_simd;               // SIMDs of the device (4 per CU)
-    int chain_force;          // >= 0: pairs per chain forced (0: unchained; tests, A/B); -1: by list length
-    int chain_tail;           // rounds of resident waves left unchained after the chained waves
 };
 // Lane-per-pair kernel (large batches): one lane owns one pair and sweeps it
 // row by row over register-resident blocks of kLaneBlock columns. A wave holds

@@ -48,8 +48,6 @@ int run_part(Part* b, hipStream_t s)
     r.wave_order = env_i64("HC_PHMM_RESCUE_ORDER", 1) != 0 ? b->d_worder : nullptr;   // 0: class order (A/B)
     r.next_wave = b->d_count + kNextWave;
     r.n_simd = 4 * dv.n_cu;
-    r.chain_force = int(std::min<int64_t>(env_i64("HC_PHMM_RESCUE_CHAIN", -1), kSeg64ChainMax));
-    r.chain_tail = int(std::max<int64_t>(0, env_i64("HC_PHMM_RESCUE_CHAIN_TAIL", 2)));
     if (b->n_lane > 0) {
         LaneArgs a{};
         a.pairs = b->d_pairs;

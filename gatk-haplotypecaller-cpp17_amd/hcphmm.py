@@ -69,8 +69,7 @@ class Stats(C.Structure):
                 ("kernel_ms_f32", C.c_double), ("kernel_ms_f64", C.c_double),
                 ("run_ms", C.c_double), ("n_launch_waves", C.c_int64), ("n_runs", C.c_int64),
                 ("n_lane_pairs", C.c_int64), ("n_seg_waves", C.c_int64), ("n_devices", C.c_int64),
-                ("pack_ms", C.c_double), ("upload_bytes", C.c_int64),
-                ("rescue_chain", C.c_int64)]
+                ("pack_ms", C.c_double), ("upload_bytes", C.c_int64)]
 
 
 def build() -> None:

@@ -93,8 +93,6 @@ typedef struct hc_phmm_stats {
     double pack_ms;         /* device packing of a new batch (rows + hap tables),
                                done once at create; max over devices               */
     int64_t upload_bytes;   /* host -> device bytes of the batch's inputs            */
-    int64_t rescue_chain;   /* fp64 rescue pairs run back to back per lane group in the
-                               last run's chained waves (0: unchained); max over parts */
 } hc_phmm_stats;
 
 /* Select the device (HIP ordinal; -1 = current) and build the device LUTs.
