@@ -86,6 +86,27 @@ def test_async_jobs_collected_out_of_order(engine, oracle_lib):
         jobs[0].collect()
 
 
+def test_shutdown_refused_while_work_is_live(engine, oracle_lib):
+    """hc_phmm_shutdown refuses (error, engine intact) while a submitted job
+    or a prepared batch still holds device memory; after collect / close it
+    succeeds, and the engine comes back with init (advisor round 2)."""
+    b = W.generate(800, (100, 400), (50, 200), 0.02, seed=43)
+    ref = oracle_lib.pairs(b, nthreads=16)
+    job = engine.submit_pairs(b)
+    with pytest.raises(engine.PairHMMError):
+        engine.shutdown()
+    assert_same(job.collect(), ref, "job after refused shutdown")
+    bt = engine.Batch(b)
+    with pytest.raises(engine.PairHMMError):
+        engine.shutdown()
+    bt.run()
+    assert_same(bt.results(), ref, "batch after refused shutdown")
+    bt.close()
+    engine.shutdown()
+    engine.init(0)
+    assert_same(engine.pairs(b), ref, "after re-init")
+
+
 def test_async_jobs_overlap_inputs_released(engine, oracle_lib):
     """Inputs may be dropped as soon as submit returns (they are staged)."""
     b = W.generate(2000, (100, 500), (50, 250), 0.01, seed=41)
