@@ -362,12 +362,15 @@ int hc_phmm_device_count(void)
 
 int hc_phmm_shutdown(void)
 {
+    bool busy;
     {
         // Refuse while calls run or jobs / batches hold parts (they keep raw
-        // Device and Slot pointers); shutdown_engine re-checks under the lock.
+        // Device and Slot pointers): shutdown_engine reports it, re-checking
+        // under its own lock (g_mu is not recursive: not held here).
         std::lock_guard<std::mutex> lk(g_mu);
-        if (g_active_calls > 0 || g_live_parts > 0) return shutdown_engine();
+        busy = g_active_calls > 0 || g_live_parts > 0;
     }
+    if (busy) return shutdown_engine();
     hcphmm::sw_release();
     hcphmm::gt_release();
     return shutdown_engine();
