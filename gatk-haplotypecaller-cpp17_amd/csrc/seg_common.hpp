@@ -177,11 +177,14 @@ struct SegSteps {
 // Rows of read words a lane keeps in flight (loaded PD steps before use). A
 // lone step of a narrow block is too short to cover a global load, so narrow
 // blocks prefetch deeper; the step loop is unrolled by PD so every word lands
-// in its own register and is not touched (no wait) until its step.
+// in its own register and is not touched (no wait) until its step. fp32
+// blocks of 32-64 columns take two steps too (round 3: S2 fp32 pass 8.884 ->
+// 8.815 ms, a 125k-pair shard -1.5 %, S1w at 1M pairs +0.8 %; three steps no
+// better: profiles/r03_prefetch_depth_ab.jsonl).
 template <typename T, int BC>
 constexpr int seg_prefetch()
 {
-    return sizeof(T) == 8 ? (BC >= 16 ? 1 : 2) : (BC >= 32 ? 1 : (BC >= 16 ? 2 : 4));
+    return sizeof(T) == 8 ? (BC >= 16 ? 1 : 2) : (BC >= 16 ? 2 : 4);
 }
 
 // Call f(integral_constant<P>) for P = 0 .. N-1 (compile-time phases).
