@@ -434,6 +434,9 @@ def main():
             dist.init_process_group("gloo", rank=rank, world_size=world)
         else:
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    # Refuse a stale binary: the library's compiled-in source hashes must be
+    # this tree's (the bench line carries them as build_id).
+    build_id = hcphmm.check_build_id()
     hcphmm.init(gpu)
 
     batch = W.config(args.workload, args.pairs)
@@ -528,7 +531,7 @@ def main():
                     lds_bank_conflict_cycles=pmc.get("lds_bank_conflict_cycles"),
                     valu_lane_instr_per_cell=pmc.get("valu_lane_instr_per_cell"),
                     traffic_source=pmc.get("traffic_source"), traffic_note=pmc.get("traffic_note"),
-                    kernel_src_hash=pmc.get("kernel_src_hash"),
+                    kernel_src_hash=build_id["tree_kernel"], lib_kernel_src_hash=build_id["kernel"],
                     profile_kernel_ms_warm=pmc.get("profile_kernel_ms_warm"), profile_frac=pmc.get("profile_frac"))
 
     out = {
@@ -549,6 +552,7 @@ def main():
         "new_batch_device_ms": round(st.run_ms + st.pack_ms, 4),
         "pack_ms": round(st.pack_ms, 4),
         "upload_bytes": int(st.upload_bytes),
+        "build_id": build_id,
     }
 
     cpu_res = None

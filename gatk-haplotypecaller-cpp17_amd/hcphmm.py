@@ -73,7 +73,28 @@ class Stats(C.Structure):
 
 
 def build() -> None:
-    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    subprocess.run(["make", "-s", "-C", HERE, "-j8"], check=True)
+
+
+def ensure_built() -> dict:
+    """Build the library if it is missing, or rebuild it if its build id does
+    not match the tree's sources (make decides by timestamps, which a copied
+    tree may not keep: a binary stale by content is rebuilt with -B); returns
+    the verified build id."""
+    if _lib is None:
+        if not os.path.exists(LIB_PATH) or _stale_by_content():
+            build()
+        if _stale_by_content():
+            subprocess.run(["make", "-s", "-B", "-C", HERE, "-j8"], check=True)
+    return check_build_id()
+
+
+def _stale_by_content() -> bool:
+    """Build id of the binary on disk (read from its bytes, without loading it)
+    against the tree's hashes."""
+    data = open(LIB_PATH, "rb").read()
+    t = tree_hashes()
+    return f"kernel={t['kernel']} lib={t['lib']}".encode() not in data
 
 
 _lib = None
@@ -95,6 +116,7 @@ def lib():
     L.hc_phmm_job_ready.argtypes = [C.c_void_p]
     L.hc_phmm_collect.argtypes = [C.c_void_p]
     L.hc_phmm_last_error.restype = C.c_char_p
+    L.hc_phmm_build_id.restype = C.c_char_p
     flat = [C.c_int64, _i64p, _i32p, _i64p, _i32p] + [_u8p] * 6
     L.hc_phmm_pairs_flat.argtypes = flat + [_f64p, _f32p, _f64p, _u8p]
     L.hc_phmm_cross.argtypes = [C.POINTER(Read), C.c_int32, C.POINTER(Hap), C.c_int32, _f64p]
@@ -111,6 +133,37 @@ def lib():
     L.hc_phmm_get_luts.argtypes = [_f32p, _f64p, _f32p, _f64p]
     _lib = L
     return L
+
+
+def build_id() -> dict:
+    """The loaded library's build id (hc_phmm_build_id): {"kernel": hash of the
+    device kernel sources, "lib": hash of every library source and flag,
+    "git": HEAD at build time}."""
+    txt = lib().hc_phmm_build_id().decode()
+    return dict(kv.split("=", 1) for kv in txt.split())
+
+
+def tree_hashes() -> dict:
+    """The same two hashes of the source tree this module sits in
+    (tools/kernel_src_hash.py)."""
+    import importlib.util
+    path = os.path.join(os.path.dirname(HERE), "tools", "kernel_src_hash.py")
+    spec = importlib.util.spec_from_file_location("_hc_kernel_src_hash", path)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return {"kernel": m.kernel_src_hash(), "lib": m.lib_src_hash()}
+
+
+def check_build_id() -> dict:
+    """Refuse a stale binary: the loaded library's source hashes must equal the
+    tree's. Returns the build id (with the tree's hashes) on success."""
+    tree = tree_hashes()
+    bid = build_id()
+    if bid.get("kernel") != tree["kernel"] or bid.get("lib") != tree["lib"]:
+        raise PairHMMError(ENODEV, f"{LIB_PATH} is stale: built from kernel={bid.get('kernel')} "
+                                   f"lib={bid.get('lib')}, tree has kernel={tree['kernel']} lib={tree['lib']} "
+                                   f"(rebuild: make -C {HERE})")
+    return dict(bid, tree_kernel=tree["kernel"], tree_lib=tree["lib"])
 
 
 def declared_symbols(header: str = HEADER):

@@ -109,6 +109,12 @@ int hc_phmm_device_count(void);   /* configured device slots (0: not initialised
 int hc_phmm_shutdown(void);       /* releases every engine (PairHMM, SW, genotyper) */
 const char* hc_phmm_last_error(void);
 int hc_phmm_version(void);   /* major*10000 + minor*100 + patch */
+/* Which sources this binary was built from (no reference equivalent): a static
+ * string "kernel=<16 hex> lib=<16 hex> git=<HEAD>[-dirty]" — the device-kernel
+ * source hash, the hash of every library source and build flag
+ * (tools/kernel_src_hash.py), and the git HEAD at build time. Callers compare
+ * the hashes with their source tree to refuse a stale binary. */
+const char* hc_phmm_build_id(void);
 
 /* All reads x all haps. out is n_reads*n_haps doubles, read-major
  * (out[r*n_haps + h]), log10 likelihoods before normalisation.

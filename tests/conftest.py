@@ -40,8 +40,8 @@ def oracle_lib():
 def engine():
     """The HIP engine on cuda:0 (gpu tests only)."""
     import hcphmm
-    if not os.path.exists(hcphmm.LIB_PATH):
-        hcphmm.build()
+    bid = hcphmm.ensure_built()   # refuses a binary not built from this tree
+    print(f"[engine] libhcpairhmm build id: {bid}")
     hcphmm.init(0)
     return hcphmm
 

@@ -2,6 +2,7 @@
 side (LUTs, argument checks) is correct without a GPU."""
 import ctypes
 import os
+import re
 import subprocess
 
 import numpy as np
@@ -12,9 +13,18 @@ import hcphmm
 
 @pytest.fixture(scope="module")
 def built():
-    if not os.path.exists(hcphmm.LIB_PATH):
-        hcphmm.build()
+    hcphmm.ensure_built()
     return hcphmm.lib()
+
+
+def test_build_id_matches_tree(built):
+    """The loaded binary says which sources it was built from
+    (hc_phmm_build_id), and they are this tree's."""
+    bid = hcphmm.build_id()
+    assert set(bid) >= {"kernel", "lib", "git"}
+    tree = hcphmm.tree_hashes()
+    assert bid["kernel"] == tree["kernel"] and bid["lib"] == tree["lib"], (bid, tree)
+    assert re.fullmatch(r"[0-9a-f]{16}", bid["kernel"]) and re.fullmatch(r"[0-9a-f]{16}", bid["lib"])
 
 
 def test_exports_every_declared_symbol(built):

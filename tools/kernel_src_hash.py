@@ -1,13 +1,34 @@
-"""Hash of the PairHMM device code's sources and build flags: a committed PMC
-summary (profiles/r*_pmc_*.json) describes the kernels only while this hash is
-unchanged; bench.py reports PMC traffic only when the hashes agree."""
+"""Hashes of the PairHMM engine's sources and build flags.
+
+kernel_src_hash(): the device kernels only — a committed PMC summary
+(profiles/r*_pmc_*.json) describes the kernels while this hash is unchanged;
+bench.py reports PMC traffic only when the hashes agree.
+
+lib_src_hash(): every source of libhcpairhmm.so (csrc/, include/, the
+Makefile's flag lines, the Jacobian table generator).
+
+    python tools/kernel_src_hash.py                  # kernel hash
+    python tools/kernel_src_hash.py --header OUT.h   # both hashes + git HEAD as C macros
+
+The Makefile compiles that header into the library (hc_phmm_build_id()), so a
+run can prove which sources the binary it loaded was built from: bench.py and
+__graft_entry__.smoke() compare the library's hashes with the tree's and
+refuse a stale binary."""
 import hashlib
 import os
+import subprocess
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "gatk-haplotypecaller-cpp17_amd", "csrc")
+PKG = os.path.join(ROOT, "gatk-haplotypecaller-cpp17_amd")
+SRC = os.path.join(PKG, "csrc")
 FILES = ["lane_kernel.hip", "seg_common.hpp", "kernels.hpp", "kernels.hip", "pack_kernels.hip", "luts.hpp",
          "device_common.hpp"]
+
+
+def _flag_lines(prefixes):
+    mk = open(os.path.join(PKG, "Makefile")).read()
+    return "".join(ln for ln in mk.splitlines() if ln.startswith(prefixes)).encode()
 
 
 def kernel_src_hash() -> str:
@@ -15,10 +36,53 @@ def kernel_src_hash() -> str:
     for f in FILES:
         h.update(f.encode())
         h.update(open(os.path.join(SRC, f), "rb").read())
-    mk = open(os.path.join(ROOT, "gatk-haplotypecaller-cpp17_amd", "Makefile")).read()
-    h.update("".join(ln for ln in mk.splitlines() if ln.startswith("DEV_FLAGS")).encode())
+    h.update(_flag_lines(("DEV_FLAGS",)))
     return h.hexdigest()[:16]
 
 
+def lib_src_hash() -> str:
+    h = hashlib.sha256()
+    files = [os.path.join(SRC, f) for f in sorted(os.listdir(SRC))]
+    inc = os.path.join(ROOT, "include")
+    files += [os.path.join(inc, f) for f in sorted(os.listdir(inc))]
+    files.append(os.path.join(ROOT, "tools", "gen_jacobian.py"))
+    for p in files:
+        if not os.path.isfile(p):
+            continue
+        h.update(os.path.relpath(p, ROOT).encode())
+        h.update(open(p, "rb").read())
+    h.update(_flag_lines(("DEV_FLAGS", "HOST_FLAGS")))
+    return h.hexdigest()[:16]
+
+
+def git_head() -> str:
+    try:
+        head = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                              text=True, timeout=10).stdout.strip()
+        dirty = subprocess.run(["git", "-C", ROOT, "status", "--porcelain", "--untracked-files=no"],
+                               capture_output=True, text=True, timeout=10).stdout.strip()
+        return (head or "unknown") + ("-dirty" if head and dirty else "")
+    except (OSError, subprocess.SubprocessError):
+        return "unknown"
+
+
+def write_header(path: str) -> None:
+    txt = (f'#define HC_KERNEL_SRC_HASH "{kernel_src_hash()}"\n'
+           f'#define HC_LIB_SRC_HASH "{lib_src_hash()}"\n'
+           f'#define HC_GIT_HEAD "{git_head()}"\n')
+    try:
+        if open(path).read() == txt:
+            return   # unchanged: keep the timestamp (no relink)
+    except OSError:
+        pass
+    with open(path, "w") as f:
+        f.write(txt)
+
+
 if __name__ == "__main__":
-    print(kernel_src_hash())
+    if len(sys.argv) == 3 and sys.argv[1] == "--header":
+        write_header(sys.argv[2])
+    elif len(sys.argv) == 2 and sys.argv[1] == "--lib":
+        print(lib_src_hash())
+    else:
+        print(kernel_src_hash())
