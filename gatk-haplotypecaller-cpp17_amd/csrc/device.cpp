@@ -33,6 +33,8 @@ std::mutex g_mu;
 std::vector<Device*> g_devs;
 int64_t g_live_parts = 0;
 int64_t g_active_calls = 0;
+std::atomic<uint32_t> g_flags{0};
+bool g_shutting = false;
 DryDump g_dump;
 TimelineRef g_tl;
 
@@ -166,6 +168,10 @@ int init_devices_locked(const int32_t* devices, int32_t n, bool any_ok)
 CallGuard::CallGuard()
 {
     std::lock_guard<std::mutex> lk(g_mu);
+    if (g_shutting) {   // hc_phmm_shutdown has committed: no new work
+        rc = fail(HC_PHMM_ENODEV, "the engine is shutting down");
+        return;
+    }
     const int32_t cur = -1;
     rc = init_devices_locked(&cur, 1, true);
     if (rc) return;
@@ -317,17 +323,31 @@ int timeline_records(unsigned long long* out, int max_waves)
     return n;
 }
 
-// hc_phmm_shutdown: refused while a call runs or a part (job / batch) is alive.
-int shutdown_engine()
+// hc_phmm_shutdown, in two steps so that the decision is taken once, under
+// g_mu: begin_shutdown refuses while a call runs or a part (job / batch) is
+// alive, else commits (new calls are refused from then on, so nothing can
+// become live again); the caller then releases the aligner and genotyper, and
+// finish_shutdown drops the devices.
+int begin_shutdown()
 {
     std::lock_guard<std::mutex> lk(g_mu);
+    if (g_shutting) return fail(HC_PHMM_EINVAL, "shutdown already in progress");
     if (g_active_calls > 0 || g_live_parts > 0)
         return fail(HC_PHMM_EINVAL, "shutdown while " + std::to_string(g_active_calls) + " call(s) run and " +
                                         std::to_string(g_live_parts) +
                                         " part(s) of uncollected jobs / live batches exist: collect and destroy "
                                         "them first");
+    g_shutting = true;
+    return HC_PHMM_OK;
+}
+
+int finish_shutdown()
+{
+    std::lock_guard<std::mutex> lk(g_mu);
     for (Device* d : g_devs) release_device(d);
     g_devs.clear();
+    g_flags.store(0);
+    g_shutting = false;
     return HC_PHMM_OK;
 }
 

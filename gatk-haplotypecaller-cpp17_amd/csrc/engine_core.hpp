@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -120,6 +121,9 @@ extern std::mutex g_mu;
 extern std::vector<Device*> g_devs;
 extern int64_t g_live_parts;
 extern int64_t g_active_calls;
+// hc_phmm_init flags of the most recent successful init (HC_PHMM_FLAG_*),
+// read by every run: HC_PHMM_FLAG_F64 = initNative(use_double = true).
+extern std::atomic<uint32_t> g_flags;
 
 int init_devices_locked(const int32_t* devices, int32_t n, bool any_ok);
 Slot* take_slot(Device& d);
@@ -228,6 +232,7 @@ struct Part {
     } cls[2];
     int n_lane = 0;
     int n_seg_waves = 0;
+    int seg_tail = 0;                // last seg waves in LPT order: the persistent pass's tail queue
     int lane_waves = 0;
     int lane_variant = 0;
     const int* d_nwaves = nullptr;   // device-planned parts: the wave count lives on the device
@@ -255,6 +260,7 @@ struct Part {
     int* d_big_count = nullptr;
     Seg64Plan* d_plan = nullptr;
     int64_t n_wide = 0;
+    int wide_ring_blocks = 0;     // fp64 wide pass: workgroups its global ring has room for (0: ring in LDS)
     int* d_count = nullptr;
     int inker_limit = 0;   // in-wave rescues allowed in the last run
     int parity = 0;
@@ -282,6 +288,30 @@ struct Part {
 Part* new_part(Device* d);   // counted in g_live_parts
 void free_part(Part* p);
 void discard_part(Part* p);  // failed before hand-out: the slot and its memory stay with the caller
+
+// A part under construction: discarded (after its stream drains) when the
+// planner leaves by an error return or an exception, unless handed out.
+class PartGuard {
+public:
+    explicit PartGuard(Part* p) : p_(p) {}
+    ~PartGuard()
+    {
+        if (!p_) return;
+        if (p_->stream) (void)hipStreamSynchronize(p_->stream);
+        discard_part(p_);
+    }
+    PartGuard(const PartGuard&) = delete;
+    PartGuard& operator=(const PartGuard&) = delete;
+    Part* release()
+    {
+        Part* q = p_;
+        p_ = nullptr;
+        return q;
+    }
+
+private:
+    Part* p_;
+};
 
 // planner.cpp: plan one part on device d (host planning + staging, then the
 // H2D, device packing and, with_run, the device pass and the D2H of the

@@ -512,14 +512,22 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
         for (int g = 0; g < ngroups; ++g) gt[g] = make_int2(keys[size_t(g)] >> 8, keys[size_t(g)] & 0xff);
     }
 
-    auto* b = new_part(&dv);
-    b->spec = spec;
+    Part* b = nullptr;
+    try {
+        b = new_part(&dv);
+    } catch (...) {
+        if (!slot) (void)hipFree(dev);
+        throw;
+    }
+    PartGuard guard(b);   // error returns and exceptions discard it (and a batch's own allocation)
     b->slot = slot;
     b->dev_base = dev;   // a batch's own allocation (freed with it), or the slot's
+    b->spec = spec;
     b->n = n;
     b->Hmax = hmax;
     b->n_lane = int(n);
     b->n_seg_waves = int(max_waves);
+    b->seg_tail = tail;
     b->lane_waves = int(max_waves);
     b->d_nwaves = reinterpret_cast<int*>(dev + o_nw);
     b->d_pairs = reinterpret_cast<PairDesc*>(dev + o_pairs);
@@ -627,12 +635,8 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     };
     rc = enqueue();
     tm.mark("flat: enqueue");
-    if (rc) {
-        (void)hipStreamSynchronize(s);
-        discard_part(b);   // the caller returns the slot (and keeps its memory)
-        return rc;
-    }
-    *out = b;
+    if (rc) return rc;   // the guard drains the stream and discards the part (the caller returns the slot)
+    *out = guard.release();
     return HC_PHMM_OK;
 }
 

@@ -36,9 +36,16 @@ using PairDesc = int4;
 // Run counters of a part (zeroed when the part is prepared): [0, 1] rescue
 // list lengths and [2, 3] in-wave rescue counts, by run parity (a run zeroes
 // the other parity's for the next run: no memset per run); [4] the fp64
-// pass's wave counter (zeroed by its plan each run).
-constexpr int kNumCounters = 8;
+// pass's wave counter (zeroed by its plan each run); from kSegHeads the
+// persistent fp32 pass's queue heads (8 XCD queues + the tail queue, one
+// 64-byte line each) and its finished-wave count, which the last wave to
+// finish zeroes again for the next run (lane_kernel.hip phmm_seg_kernel).
 constexpr int kNextWave = 4;
+constexpr int kSegHeads = 16;
+constexpr int kSegQueues = 9;          // 8 XCD queues + the tail queue
+constexpr int kSegHeadStride = 16;     // ints: one 64-byte line per head
+constexpr int kSegDone = kSegHeads + kSegQueues * kSegHeadStride;
+constexpr int kNumCounters = kSegDone + 16;
 
 struct DiagArgs {
     const PairDesc* pairs;
@@ -139,6 +146,11 @@ struct LaneArgs {
     // Diagnostics (HC_PHMM_TIMELINE=1, seg waves only): per wave
     // {start, end} of s_memrealtime (100 MHz) and the HW_ID register; null = off.
     unsigned long long* timeline;
+    // Persistent seg pass (phmm_seg_kernel): the run counters (kSegHeads..),
+    // null = one wave per launched slot (the classic grid); the last n_tail
+    // waves of the order form the shared tail queue (shortest, longest first).
+    int* seg_counters;
+    int n_tail;
 };
 
 constexpr int kInWaveRescueMaxH = 512;   // one pair over 64 lanes of 8 columns
@@ -152,13 +164,20 @@ const LaneVariant& lane_variant(int id);
 hipError_t launch_lane_f32(int variant, const LaneArgs& a, hipStream_t s);
 // Column-segmented waves only (lane_kernel.hip run_seg): a pair of hap length H
 // takes ceil(H / BC) lanes; BC per wave, one of the compiled block widths.
-hipError_t launch_lane_seg_f32(const LaneArgs& a, hipStream_t s);
+// max_blocks > 0: at most that many workgroups (4 waves each), persistent
+// waves fetching the rest (a.seg_counters must be set).
+hipError_t launch_lane_seg_f32(const LaneArgs& a, int max_blocks, hipStream_t s);
 bool seg_width_ok(int bc);
 int seg_width_ceil(int bc);   // narrowest compiled width >= bc (-1: none)
 constexpr int kSegMaxBC = 64;
 constexpr int kSegMinBC = 8;    // narrowest compiled fp32 block width
 
 hipError_t launch_rescue_seg64(const Seg64Args& a, int grid, hipStream_t s);
+// initNative(use_double = true) (intel_pairhmm.hpp:71,81,135): result_float is
+// 0 for every pair, so every pair takes the fp64 path. The fp32 pass is
+// replaced by this fill: raw_f32 = 0, rescued = 1 and the rescue list = all n
+// pairs (pair ids 0 .. n-1), *count = n.
+hipError_t launch_all_f64_list(int n, float* raw32, uint8_t* flag, int* list, int* count, hipStream_t s);
 
 // Launchers (kernels.hip). W = lanes per pair: 16, 32 or 64.
 hipError_t launch_diag_f32(int W, const DiagArgs& a, int grid, hipStream_t s);
@@ -170,6 +189,7 @@ size_t diag_lds_bytes(int W, int ring_len, bool f64);
 // kDiagRingBlocks workgroups, each looping over its share of the pairs.
 constexpr size_t kDiagLdsMax = size_t(152) * 1024;
 constexpr int kDiagRingBlocks = 1024;
+constexpr int kWideRing64Blocks = 64;   // the fp64 wide-hap rescue pass's global ring (planner.cpp)
 inline bool diag_ring_in_lds(int W, int ring_len, bool f64) { return diag_lds_bytes(W, ring_len, f64) <= kDiagLdsMax; }
 hipError_t configure_kernels();   // raise the dynamic-LDS limit once
 

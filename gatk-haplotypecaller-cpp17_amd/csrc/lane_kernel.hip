@@ -19,6 +19,7 @@
 //                             device from the rescue list (rescue_plan_kernel);
 //   phmm_lane_kernel  (fp32)  one lane per pair, blocks chained through a
 //                             global carry buffer (haps too long to segment).
+#include <algorithm>
 #include <type_traits>
 
 #include "seg_common.hpp"
@@ -395,10 +396,34 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
         a.timeline[3 * size_t(wid)] = t_start;
         a.timeline[3 * size_t(wid) + 1] = t_end;
-        a.timeline[3 * size_t(wid) + 2] = unsigned(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));
+        // HW_ID (CU / SIMD / SE) in the low word, XCC_ID (hwreg 20) above it
+        a.timeline[3 * size_t(wid) + 2] = (unsigned long long)unsigned(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))) |
+                                          ((unsigned long long)unsigned(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11))) << 32);
     }
 }
 
+
+// Persistent form of the pass (more waves than the launch's wave slots): the
+// reference's schedule(dynamic, 1) over the pairs (intel_pairhmm.hpp:128-130)
+// at wave granularity, with XCD locality. The order (packing order: one block
+// width's waves together; the shortest waves last, longest first) is cut into
+// 8 contiguous ranges, one per XCD group (workgroup b serves group b % 8:
+// workgroups are dealt round-robin over the 8 XCDs, so a group is one XCD, for
+// speed only), and the last n_tail waves form a shared tail queue. A wave
+// takes its group's range first — the first round statically (its own
+// position, no atomic), then from the group's head counter — then the other
+// groups' ranges in turn, then the tail. Each XCD thus works through a
+// window of the order 8x narrower than the whole chip's, so the waves
+// resident on a CU pair share few block widths' code (at 125k pairs the
+// chip's window of 3 072 waves spans ~8 widths of ~10 KB of unrolled step
+// code each). The wave that finishes last zeroes the counters for the next
+// run (every other wave has fetched its last by then).
+__device__ __forceinline__ int seg_fetch(int* head)
+{
+    int v = 0;
+    if ((threadIdx.x & 63) == 0) v = atomicAdd(head, 1);
+    return __builtin_amdgcn_readfirstlane(v);
+}
 
 template <int OCC>
 __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
@@ -407,10 +432,44 @@ __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
     // Device-planned parts launch an upper bound of waves: surplus workgroups
     // leave before the LDS fill (workgroup-uniform).
     const int n_waves = a.n_waves_dev ? __builtin_amdgcn_readfirstlane(*a.n_waves_dev) : a.n_waves;
-    if (int(blockIdx.x) * kSegWPB >= n_waves) return;
+    const int launched = int(gridDim.x) * kSegWPB;
+    const bool persist = a.seg_counters && n_waves > launched;
+    if (!persist && int(blockIdx.x) * kSegWPB >= n_waves) return;
     load_slut(slut, a.lut);
-    const int wid = blockIdx.x * kSegWPB + (threadIdx.x >> 6);
-    if (wid < n_waves) seg_wave(a, wid, slut);
+    int* const heads = a.seg_counters + kSegHeads;
+    const int G = int(gridDim.x);
+    const int bulk = n_waves - min(a.n_tail, n_waves);
+    const int q0 = int(blockIdx.x) & 7;
+    // Range of group r: [r * bulk / 8, (r + 1) * bulk / 8); queue 8 = the tail.
+    auto lo_of = [&](int r) { return r < 8 ? int((long long)r * bulk / 8) : bulk; };
+    auto hi_of = [&](int r) { return r < 8 ? int((long long)(r + 1) * bulk / 8) : n_waves; };
+    // waves launched in group r (workgroups r, r + 8, ...): its static round
+    auto nstat_of = [&](int r) { return r < 8 && r < G ? ((G - 1 - r) / 8 + 1) * kSegWPB : 0; };
+    // k = -1: the static position (one wave per slot without persistence);
+    // k = 0..7: group (q0 + k) % 8's range; k = 8: the tail queue. One call
+    // site of seg_wave (its width switch is large: a second copy spills).
+    for (int k = -1; k <= 8;) {
+        int pos;
+        if (k < 0) {
+            k = persist ? 0 : 9;
+            pos = persist ? lo_of(q0) + (int(blockIdx.x) >> 3) * kSegWPB + (threadIdx.x >> 6)
+                          : int(blockIdx.x) * kSegWPB + (threadIdx.x >> 6);
+            if (pos >= (persist ? hi_of(q0) : n_waves)) continue;
+        } else {
+            const int r = k < 8 ? (q0 + k) & 7 : 8;
+            pos = lo_of(r) + nstat_of(r) + seg_fetch(heads + r * kSegHeadStride);
+            if (pos >= hi_of(r)) {
+                ++k;
+                continue;
+            }
+            __builtin_amdgcn_wave_barrier();   // the previous wave's last use of its LDS slots
+        }
+        seg_wave(a, pos, slut);
+    }
+    if (persist && seg_fetch(a.seg_counters + kSegDone) == launched - 1 && (threadIdx.x & 63) < kSegQueues) {
+        heads[(threadIdx.x & 63) * kSegHeadStride] = 0;
+        if ((threadIdx.x & 63) == 0) a.seg_counters[kSegDone] = 0;
+    }
 }
 
 // Wave-uniform max / min of a per-lane int (once per wave).
@@ -484,6 +543,18 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
     }
 }
 
+__global__ __launch_bounds__(256) void all_f64_list_kernel(int n, float* __restrict__ raw32,
+                                                          uint8_t* __restrict__ flag, int* __restrict__ list,
+                                                          int* __restrict__ count)
+{
+    for (int p = blockIdx.x * 256 + threadIdx.x; p < n; p += gridDim.x * 256) {
+        raw32[p] = 0.f;   // result_float = 0.0f (intel_pairhmm.hpp:135)
+        flag[p] = 1;      // 0 < MIN_ACCEPTED: the double kernel for every pair
+        list[p] = p;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *count = n;
+}
+
 }  // namespace
 
 // One-lane kernel variants: {pairs per lane, block columns, waves per SIMD}.
@@ -534,11 +605,19 @@ int seg_width_ceil(int bc)
     return -1;
 }
 
-hipError_t launch_lane_seg_f32(const LaneArgs& a, hipStream_t s)
+hipError_t launch_lane_seg_f32(const LaneArgs& a, int max_blocks, hipStream_t s)
 {
     if (a.n_waves <= 0) return hipSuccess;
-    const int grid = (a.n_waves + kSegWPB - 1) / kSegWPB;
+    int grid = (a.n_waves + kSegWPB - 1) / kSegWPB;
+    if (max_blocks > 0 && a.seg_counters && grid > max_blocks) grid = max_blocks;
     hipLaunchKernelGGL((phmm_seg_kernel<kSegOcc>), dim3(grid), dim3(64 * kSegWPB), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_all_f64_list(int n, float* raw32, uint8_t* flag, int* list, int* count, hipStream_t s)
+{
+    const int grid = n <= 0 ? 1 : std::min((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(all_f64_list_kernel, dim3(grid), dim3(256), 0, s, n, raw32, flag, list, count);
     return hipGetLastError();
 }
 

@@ -786,6 +786,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         }
     }
     tm.mark("seg pack: greedy");
+    int seg_tail = 0;   // waves at the end of the order in LPT order (persistent tail queue)
     // Dispatch order: the bulk in packing order (co-resident waves share one
     // width's code), the shortest waves filling the last tail_rounds rounds of
     // wave slots last, longest first (LPT, duration ~ BC * nsteps), so the chip
@@ -798,6 +799,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         const int64_t tail_rounds = std::max<int64_t>(0, env_i64("HC_PHMM_TAIL_ROUNDS", grid ? 0 : 2));
         const size_t nw = lw.size();
         const size_t K = std::min(nw, size_t(tail_rounds) * 4 * size_t(dv.n_cu) * kSegWavesPerSimd);
+        seg_tail = 0;
         std::vector<int64_t>& wc = S.wcost;
         wc.resize(nw);
         int64_t cmin = INT64_MAX, cmax = 0;
@@ -827,6 +829,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
                 if (!in_tail[k]) ordered.push_back(lw[k]);
             for (size_t k = 0; k < K; ++k) ordered.push_back(lw[key[k] & 0xffffffffu]);
             lw.swap(ordered);
+            seg_tail = int(K);   // the persistent pass's shared tail queue
         }
     }
     tm.mark("seg pack");
@@ -979,16 +982,23 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         }
     }
     const int Hmax = hmax_a.load();
+    // The fp64 wide pass runs only for rescued wide pairs (usually none or a
+    // few), so its global ring is sized for kWideRing64Blocks workgroups (each
+    // loops over its share of the list), not for every wide pair: a call with
+    // a thousand 262k-base haps would otherwise reserve ~4 GB, kept by its slot
+    // (advisor round 3).
+    int wide_ring_blocks = 0;
     if (wide_a.load() > 0 && !diag_ring_in_lds(64, Hmax + 2 * 64 + 16, true)) {
-        const size_t blocks = std::min<size_t>(size_t(wide_a.load()), kDiagRingBlocks);
-        ring_bytes = std::max(ring_bytes, blocks * size_t(Hmax + 2 * 64 + 16) * 2 * sizeof(double));
+        wide_ring_blocks = int(std::min<int64_t>(wide_a.load(), kWideRing64Blocks));
+        ring_bytes = std::max(ring_bytes, size_t(wide_ring_blocks) * size_t(Hmax + 2 * 64 + 16) * 2 * sizeof(double));
     }
     const size_t o_ring = L.take(ring_bytes);
     const size_t total = L.off;
 
     auto* b = new_part(&dv);
-    b->spec = spec;
+    PartGuard guard(b);   // error returns and exceptions discard it (the caller returns the slot)
     b->slot = slot;
+    b->spec = spec;
     char* dev = nullptr;
     int rc = HC_PHMM_OK;
     if (slot) {
@@ -997,16 +1007,14 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     } else if (hipMalloc(&dev, total) != hipSuccess) {
         rc = fail(HC_PHMM_ENOMEM, "device allocation failed (" + std::to_string(total >> 20) + " MiB)");
     }
-    if (rc) {
-        discard_part(b);   // the caller returns the slot
-        return rc;
-    }
+    if (rc) return rc;
     b->dev_base = dev;
     b->n = npairs;
     b->cells = cells_a.load();
     b->Hmax = Hmax;
     b->n_lane = int(size_t(n_seg_slots) + one_ord.size());
     b->n_seg_waves = n_seg_waves;
+    b->seg_tail = seg_tail;
     b->lane_variant = lane_var;
     b->lane_waves = dev_plan ? n_seg_waves : int(lw.size());
     b->upload_bytes = dev_pairs ? (up_mid - up0) + (o_lw - o_bases) + (upload - o_gb) : upload - up0;
@@ -1038,6 +1046,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     b->d_big_count = reinterpret_cast<int*>(dev + o_bigc);
     b->d_plan = reinterpret_cast<Seg64Plan*>(dev + o_plan);
     b->n_wide = wide_a.load();
+    b->wide_ring_blocks = wide_ring_blocks;
     b->d_carry = carry_rows ? reinterpret_cast<float2*>(dev + o_carry) : nullptr;
     if (slot) b->host_res = host + host_res_off;
 
@@ -1117,12 +1126,8 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     };
     rc = enqueue();
     tm.mark("enqueue");
-    if (rc) {
-        (void)hipStreamSynchronize(s);
-        discard_part(b);   // the caller returns the slot
-        return rc;
-    }
-    *out = b;
+    if (rc) return rc;   // the guard drains the stream and discards the part
+    *out = guard.release();
     return HC_PHMM_OK;
 }
 

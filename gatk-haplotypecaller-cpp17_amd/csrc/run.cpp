@@ -48,7 +48,11 @@ int run_part(Part* b, hipStream_t s)
     r.wave_order = env_i64("HC_PHMM_RESCUE_ORDER", 1) != 0 ? b->d_worder : nullptr;   // 0: class order (A/B)
     r.next_wave = b->d_count + kNextWave;
     r.n_simd = 4 * dv.n_cu;
-    if (b->n_lane > 0) {
+    // initNative(use_double = true): no fp32 pass, every pair to the fp64 one
+    // (intel_pairhmm.hpp:71,81,135-140).
+    const bool all_f64 = (g_flags.load(std::memory_order_relaxed) & HC_PHMM_FLAG_F64) != 0;
+    if (all_f64) HIP_TRY(launch_all_f64_list(int(b->n), b->d_raw32, b->d_flag, b->d_list, count, s));
+    if (b->n_lane > 0 && !all_f64) {
         LaneArgs a{};
         a.pairs = b->d_pairs;
         a.order = b->d_lane_order;
@@ -100,11 +104,19 @@ int run_part(Part* b, hipStream_t s)
             g.waves = b->d_lane_waves;
             g.n_waves = b->n_seg_waves;
             g.n_waves_dev = b->d_nwaves;
+            // Persistent waves (HC_PHMM_SEG_PERSIST=0: one wave per launched
+            // slot, the hardware dispatching them in order; A/B only).
+            int max_blocks = 0;
+            if (env_i64("HC_PHMM_SEG_PERSIST", 1) != 0) {
+                g.seg_counters = b->d_count;
+                g.n_tail = b->seg_tail;
+                max_blocks = int(std::max<int64_t>(1, env_i64("HC_PHMM_SEG_BLOCKS_PER_CU", 3))) * dv.n_cu;
+            }
             if (fork) {
                 HIP_TRY(hipEventRecord(b->fork, s));
                 HIP_TRY(hipStreamWaitEvent(b->side, b->fork, 0));
             }
-            HIP_TRY(launch_lane_seg_f32(g, fork ? b->side : s));
+            HIP_TRY(launch_lane_seg_f32(g, max_blocks, fork ? b->side : s));
             if (fork) HIP_TRY(hipEventRecord(b->join, b->side));
         }
         if (n_one > 0) {
@@ -115,7 +127,7 @@ int run_part(Part* b, hipStream_t s)
         if (fork) HIP_TRY(hipStreamWaitEvent(s, b->join, 0));
     }
     for (auto& c : b->cls) {
-        if (c.n == 0) continue;
+        if (c.n == 0 || all_f64) continue;
         DiagArgs a{};
         a.pairs = b->d_pairs;
         a.order = c.d_order;
@@ -156,7 +168,8 @@ int run_part(Part* b, hipStream_t s)
             a.ring_len = b->Hmax + 2 * 64 + 16;
             a.ring_global = diag_ring_in_lds(64, a.ring_len, true) ? nullptr : b->d_ring;
             a.raw_out = b->d_raw64;
-            HIP_TRY(launch_diag_f64(64, a, int(std::min<int64_t>(b->n_wide, 2048)), s));
+            const int64_t cap = a.ring_global ? b->wide_ring_blocks : 2048;
+            HIP_TRY(launch_diag_f64(64, a, int(std::max<int64_t>(1, std::min<int64_t>(b->n_wide, cap))), s));
         }
     }
     HIP_TRY(hipEventRecord(b->ev[2], s));

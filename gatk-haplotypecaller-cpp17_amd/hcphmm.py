@@ -116,7 +116,8 @@ def lib():
     L.hc_phmm_job_ready.argtypes = [C.c_void_p]
     L.hc_phmm_collect.argtypes = [C.c_void_p]
     L.hc_phmm_last_error.restype = C.c_char_p
-    L.hc_phmm_build_id.restype = C.c_char_p
+    if hasattr(L, "hc_phmm_build_id"):   # (absent from pre-round-4 builds loaded for A/B)
+        L.hc_phmm_build_id.restype = C.c_char_p
     flat = [C.c_int64, _i64p, _i32p, _i64p, _i32p] + [_u8p] * 6
     L.hc_phmm_pairs_flat.argtypes = flat + [_f64p, _f32p, _f64p, _u8p]
     L.hc_phmm_cross.argtypes = [C.POINTER(Read), C.c_int32, C.POINTER(Hap), C.c_int32, _f64p]
@@ -156,7 +157,14 @@ def tree_hashes() -> dict:
 
 def check_build_id() -> dict:
     """Refuse a stale binary: the loaded library's source hashes must equal the
-    tree's. Returns the build id (with the tree's hashes) on success."""
+    tree's. Returns the build id (with the tree's hashes) on success. An A/B
+    build loaded through HC_PHMM_LIB is reported, not checked."""
+    if os.environ.get("HC_PHMM_LIB"):
+        try:
+            bid = build_id()
+        except AttributeError:
+            bid = {}
+        return dict(bid, ab_lib=LIB_PATH, tree_kernel=tree_hashes()["kernel"], tree_lib=tree_hashes()["lib"])
     tree = tree_hashes()
     bid = build_id()
     if bid.get("kernel") != tree["kernel"] or bid.get("lib") != tree["lib"]:
@@ -182,19 +190,25 @@ def _p(a, t):
     return None if a is None else a.ctypes.data_as(t)
 
 
-def init(device: int = -1) -> None:
-    """Select the device (-1: current / whatever the engine already runs on)."""
-    _check(lib().hc_phmm_init(0, device))
+FLAG_F64 = 1   # HC_PHMM_FLAG_F64: initNative(use_double = true), every pair in fp64 only
 
 
-def init_devices(devices=None) -> None:
+def init(device: int = -1, use_double: bool = False) -> None:
+    """Select the device (-1: current / whatever the engine already runs on).
+    use_double: initNative(use_double) (intel_pairhmm.hpp:71,81,135) — every
+    pair computed in fp64 only (process-wide until the next init)."""
+    _check(lib().hc_phmm_init(FLAG_F64 if use_double else 0, device))
+
+
+def init_devices(devices=None, use_double: bool = False) -> None:
     """Configure device slots (HIP ordinals; None = every visible device). An
     ordinal may repeat: two streams on one GPU."""
+    fl = FLAG_F64 if use_double else 0
     if devices is None:
-        _check(lib().hc_phmm_init_devices(0, None, 0))
+        _check(lib().hc_phmm_init_devices(fl, None, 0))
         return
     arr = np.ascontiguousarray(devices, np.int32)
-    _check(lib().hc_phmm_init_devices(0, _p(arr, _i32p), len(arr)))
+    _check(lib().hc_phmm_init_devices(fl, _p(arr, _i32p), len(arr)))
 
 
 def device_count() -> int:

@@ -95,9 +95,18 @@ typedef struct hc_phmm_stats {
     int64_t upload_bytes;   /* host -> device bytes of the batch's inputs            */
 } hc_phmm_stats;
 
-/* Select the device (HIP ordinal; -1 = current) and build the device LUTs.
- * flags: reserved, pass 0. (intel_pairhmm.hpp:77-113 initNative.) Calling it
- * again is a no-op for the same device or for -1; naming a different device
+/* hc_phmm_init / hc_phmm_init_devices flags. */
+#define HC_PHMM_FLAG_F64 1u   /* initNative(use_double = true), intel_pairhmm.hpp:71,81,135:
+                                 result_float = 0 for every pair, so every pair is computed
+                                 in fp64 only: raw_f32 = 0, rescued = 1, raw_f64 = the fp64
+                                 sum, loglik = log10(raw_f64) - log10(2^1020) */
+
+/* Select the device (HIP ordinal; -1 = current) and build the device LUTs
+ * (intel_pairhmm.hpp:77-113 initNative). flags: 0 or HC_PHMM_FLAG_F64; other
+ * bits are HC_PHMM_EINVAL. The flags of the latest successful init apply to
+ * every later run in the process (batches included) until the next init or
+ * hc_phmm_shutdown (which resets them to 0). Calling it again is a no-op for
+ * the same device or for -1 (apart from the flags); naming a different device
  * than the engine runs on is HC_PHMM_EINVAL (hc_phmm_shutdown first). */
 int hc_phmm_init(uint32_t flags, int device);
 /* Several device slots in one process: devices[k] is a HIP ordinal (-1 =

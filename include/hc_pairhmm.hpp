@@ -28,13 +28,16 @@ namespace hc {
 
 class MI355XPairHMM {
 public:
-    explicit MI355XPairHMM(int device = -1) : device_(device) {}
+    // use_double: initNative(use_double) (intel_pairhmm.hpp:71,81): every pair
+    // in fp64 only. The mode is process-wide in the engine (hc_phmm_init
+    // flags), set again by each compute_likelihoods call.
+    explicit MI355XPairHMM(int device = -1, bool use_double = false) : device_(device), use_double_(use_double) {}
 
     template <class HaplotypeT, class SAMRecordT>
     std::vector<std::vector<double>> compute_likelihoods(const std::vector<HaplotypeT>& haplotypes,
                                                          std::vector<SAMRecordT>& reads)
     {
-        check(hc_phmm_init(0, device_));
+        check(hc_phmm_init(use_double_ ? HC_PHMM_FLAG_F64 : 0u, device_));
         const int nr = static_cast<int>(reads.size()), nh = static_cast<int>(haplotypes.size());
         std::vector<std::string> gaps;   // owned i/d/c strings where the record's are short
         gaps.reserve(3 * reads.size());
@@ -84,6 +87,7 @@ private:
             throw std::runtime_error(std::string("hc_pairhmm: ") + hc_phmm_last_error());
     }
     int device_;
+    bool use_double_;
 };
 
 }  // namespace hc

@@ -135,3 +135,12 @@ def test_flat_record_nibble_packing():
         L.hcx_pack_nibbles(s.ctypes.data, n, got.ctypes.data)
         assert np.array_equal(got[: (n + 1) // 2], exp), n
         assert (got[(n + 1) // 2:] == 0xEE).all(), n   # nothing written past the record field
+
+
+def test_init_rejects_unknown_flags(built):
+    """hc_phmm_init flags: 0 or HC_PHMM_FLAG_F64 (initNative's use_double);
+    any other bit is refused before a device is touched."""
+    L = hcphmm.lib()
+    assert L.hc_phmm_init(2, 0) == hcphmm.EINVAL
+    assert b"flags" in L.hc_phmm_last_error()
+    assert L.hc_phmm_init_devices(0x80, None, 0) == hcphmm.EINVAL

@@ -199,3 +199,27 @@ def test_region_planner_ragged_vs_oracle(engine, oracle_lib, monkeypatch, grid):
         for k, (g, e) in enumerate(zip(got, _regions_ref(oracle_lib, batch))):
             assert g.shape == e.shape
             assert np.array_equal(bits(g), bits(e)), f"grid={grid} region {k}"
+
+
+def test_submit_unwinds_on_exception(engine, oracle_lib, many_parts):
+    """A part whose planning throws (bad_alloc injected by a test hook) makes
+    the submit fail with HC_PHMM_ENOMEM and free the parts it had already
+    enqueued, so nothing stays live: shutdown then succeeds and the engine
+    works again after init (advisor round 3: submit leaked the job and its
+    parts, and shutdown was refused for the rest of the process)."""
+    import ctypes as C
+    L = engine.lib()
+    L.hcx_inject_plan_throw.argtypes = [C.c_int]
+    L.hcx_inject_plan_throw.restype = None
+    b = W.generate(3000, (100, 500), (50, 250), 0.01, seed=44)
+    ref = oracle_lib.pairs(b, nthreads=16)
+    L.hcx_inject_plan_throw(2)   # the second part of the call throws
+    try:
+        with pytest.raises(engine.PairHMMError) as e:
+            engine.pairs(b)
+        assert e.value.code == engine.ENOMEM
+    finally:
+        L.hcx_inject_plan_throw(0)
+    engine.shutdown()            # refused if any part had leaked
+    engine.init(0)
+    assert_same(engine.pairs(b), ref, "after unwinding")

@@ -385,3 +385,44 @@ def test_flat_device_planner_ragged_and_long(engine, oracle_lib):
     assert_same(engine.pairs(b), oracle_lib.pairs(b, nthreads=16), "ragged")
     c = W.generate(300, (3000, 6000), (50, 200), 0.02, seed=78)
     assert_same(engine.pairs(c), oracle_lib.pairs(c, nthreads=16), "long haps")
+
+
+def test_use_double_every_golden_pair(engine, golden, golden_batch):
+    """initNative(use_double = true) (intel_pairhmm.hpp:71,81,135-140) through
+    hc_phmm_init(HC_PHMM_FLAG_F64): result_float = 0 for every pair, so every
+    pair's fp64 sum must equal the reference's double kernel on that pair
+    (golden raw_f64_all, computed for every pair) bit for bit, and the
+    likelihood is glibc log10(raw_f64) - log10(2^1020) — on the flat device
+    planner, the host planner and a prepared batch."""
+    import ctypes
+    libm = ctypes.CDLL("libm.so.6")
+    libm.log10.restype = ctypes.c_double
+    libm.log10.argtypes = [ctypes.c_double]
+    l10 = libm.log10(2.0 ** 1020)
+    exp64 = golden["raw_f64_all"]
+    exp_ll = np.array([libm.log10(float(x)) - l10 for x in exp64])
+    engine.init(0, use_double=True)
+    try:
+        runs = {"flat": engine.pairs(golden_batch)}
+        import os
+        os.environ["HC_PHMM_FLAT_PLAN"] = "0"
+        try:
+            runs["host"] = engine.pairs(golden_batch)
+        finally:
+            del os.environ["HC_PHMM_FLAT_PLAN"]
+        bt = engine.Batch(golden_batch)
+        bt.run()
+        runs["batch"] = bt.results()
+        bt.close()
+    finally:
+        engine.init(0, use_double=False)
+    for name, res in runs.items():
+        assert (res["raw_f32"] == 0).all(), name
+        assert res["rescued"].all(), name
+        d = res["raw_f64"].view(np.uint64) != exp64.view(np.uint64)
+        assert not d.any(), f"{name}: {d.sum()} raw_f64 mismatches, first {np.nonzero(d)[0][:10]}"
+        ll = res["loglik"].view(np.uint64) != exp_ll.view(np.uint64)
+        assert not ll.any(), f"{name}: {ll.sum()} loglik mismatches"
+    # and the default mode is back: the fp32 pass decides again
+    res = engine.pairs(golden_batch)
+    assert np.array_equal(res["rescued"], golden["rescued"])
