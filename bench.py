@@ -94,12 +94,22 @@ def pmc_from_profiles(workload, cells, kernel_ms, world):
             d = json.load(open(path))
             if d.get("kernel_src_hash") != want or int(d.get("cells", -1)) != int(cells):
                 continue
-            k = d["kernels"][d["dominant_kernel"]]
+            k = d["kernels"][d.get("fp32_kernel") or d["dominant_kernel"]]
             out = dict(traffic=int(d["hbm_bytes_per_launch"]), traffic_source=os.path.relpath(path, ROOT),
                        kernel_src_hash=want, profile_kernel_ms_warm=k.get("avg_ms_warm"),
                        profile_frac=d.get("frac_from_warm_avg"),
                        lds_bank_conflict_cycles=int(k.get("SQ_LDS_BANK_CONFLICT", 0)),
-                       valu_lane_instr_per_cell=d.get("valu_lane_instr_per_cell"))
+                       valu_lane_instr_per_cell=d.get("valu_lane_instr_per_cell"),
+                       write_bytes_per_launch=d.get("write_bytes_per_launch"),
+                       dominant_kernel=d.get("dominant_kernel"))
+            if d.get("fp64_kernel") and d.get("rescued_cells"):
+                k64 = d["kernels"][d["fp64_kernel"]]
+                out["fp64_pmc"] = dict(kernel=d["fp64_kernel"], profile_kernel_ms_warm=k64.get("avg_ms_warm"),
+                                       rescued_cells=d["rescued_cells"],
+                                       profile_frac=d.get("fp64_frac_from_warm_avg"),
+                                       valu_lane_instr_per_rescued_cell=d.get("fp64_valu_lane_instr_per_rescued_cell"),
+                                       mean_resident_waves_per_busy_cycle=d.get(
+                                           "fp64_mean_resident_waves_per_busy_cycle"))
             if kernel_ms > 0:
                 out["hbm_measured_GBs"] = round(out["traffic"] / (kernel_ms * 1e-3) / 1e9, 2)
             return out
@@ -257,11 +267,12 @@ def gt_secondary(no_cpu: bool):
 FP64_PEAK_TOPS = 39.3   # AMD MI355X FP64 vector 78.6 TFLOPS (FMA = 2) -> 39.3 T non-FMA op/s; the guide has no FP64 row
 
 
-def resident_pass(hcphmm, W, name, npairs, prof):
+def resident_pass(hcphmm, W, name, npairs, prof, batch=None):
     """One BASELINE config as a device-resident batch: 5 timed device passes
     (HIP events). S4 also prices its fp64 rescue pass (intel_pairhmm.hpp:
-    137-139): 12 f64 ops per rescued cell / fp64 pass time vs the fp64 peak."""
-    b = W.config(name, npairs)
+    137-139): 12 f64 ops per rescued cell / fp64 pass time vs the fp64 peak.
+    `batch`: a given batch (a shard) instead of the config's."""
+    b = W.config(name, npairs) if batch is None else batch
     bb = hcphmm.Batch(b)
     for _ in range(2):
         bb.run()
@@ -279,8 +290,9 @@ def resident_pass(hcphmm, W, name, npairs, prof):
                new_batch_device_ms=round(s2.run_ms + s2.pack_ms, 4))
     pmc = pmc_from_profiles(prof, cells, s2.kernel_ms_f32, 1)
     if "traffic" in pmc:
-        ent["pmc"] = {k: pmc[k] for k in ("traffic", "traffic_source", "profile_kernel_ms_warm", "profile_frac",
-                                          "hbm_measured_GBs", "valu_lane_instr_per_cell")}
+        ent["pmc"] = {k: pmc.get(k) for k in ("traffic", "traffic_source", "profile_kernel_ms_warm", "profile_frac",
+                                              "hbm_measured_GBs", "valu_lane_instr_per_cell", "write_bytes_per_launch",
+                                              "dominant_kernel", "fp64_pmc")}
     if s2.n_rescued and s2.kernel_ms_f64 > 0:
         r = bb.results()
         m = r["rescued"].astype(bool)
@@ -395,6 +407,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="S2", choices=["S1", "S1w", "S2", "S4"])
     ap.add_argument("--pairs", type=int, default=None, help="override pair count")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="run rank 0's shard of an N-way split of the batch (shard.shard_pairs), at one GPU")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core of this process's CPU set")
     ap.add_argument("--cpu-reps", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
@@ -440,6 +454,8 @@ def main():
     hcphmm.init(gpu)
 
     batch = W.config(args.workload, args.pairs)
+    if args.shard_of > 1:   # one rank's share of configs[3], measured alone
+        batch = W.subset(batch, shard.shard_pairs(batch["R"], batch["H"], args.shard_of)[0])
     n_total = len(batch["R"])
     total_cells = W.cells(batch)
     shards = shard.shard_pairs(batch["R"], batch["H"], world)
@@ -518,8 +534,10 @@ def main():
     # Dominant kernel: the fp32 PairHMM pass. Algorithmic work 12 ops/cell.
     k_ms = st.kernel_ms_f32
     achieved = FLOPS_PER_CELL * my_cells / (k_ms * 1e-3) / 1e12 if k_ms > 0 else 0.0
-    pmc = pmc_from_profiles(args.workload if args.pairs is None else f"{args.workload}_{args.pairs}",
-                            my_cells, k_ms, world)
+    prof_name = args.workload if args.pairs is None else f"{args.workload}_{args.pairs}"
+    if args.shard_of > 1:
+        prof_name = f"{args.workload}shard_{args.shard_of}"
+    pmc = pmc_from_profiles(prof_name, my_cells, k_ms, world)
     roofline = dict(bound="valu", achieved=round(achieved, 3), peak=VALU_PEAK_TOPS, unit="TFLOP/s",
                     frac=round(achieved / VALU_PEAK_TOPS, 4), traffic=pmc.get("traffic"),
                     kernel=(("phmm_seg_kernel" if st.n_seg_waves > 0 else "phmm_lane_kernel")
@@ -531,7 +549,7 @@ def main():
                     lds_bank_conflict_cycles=pmc.get("lds_bank_conflict_cycles"),
                     valu_lane_instr_per_cell=pmc.get("valu_lane_instr_per_cell"),
                     traffic_source=pmc.get("traffic_source"), traffic_note=pmc.get("traffic_note"),
-                    kernel_src_hash=build_id["tree_kernel"], lib_kernel_src_hash=build_id["kernel"],
+                    kernel_src_hash=build_id["tree_kernel"], lib_kernel_src_hash=build_id.get("kernel"),
                     profile_kernel_ms_warm=pmc.get("profile_kernel_ms_warm"), profile_frac=pmc.get("profile_frac"))
 
     out = {
@@ -573,6 +591,8 @@ def main():
     if rank == 0 and world == 1:
         r = bt.results()
         out["config"]["rescued_fp64"] = int(r["rescued"].sum())
+        m = r["rescued"].astype(bool)
+        out["config"]["rescued_cells"] = int(np.dot(sub["R"][m].astype(np.int64), sub["H"][m].astype(np.int64)))
         if cpu_res is not None:
             same = all(np.array_equal(np.ascontiguousarray(r[k]).view(np.uint8),
                                       np.ascontiguousarray(cpu_res[k]).view(np.uint8))
@@ -588,6 +608,16 @@ def main():
         for label, name, npairs in (("S1", "S1", None), ("S1w", "S1w", None), ("S1w1M", "S1w", 1_000_000),
                                     ("S4", "S4", None), ("S4_20k", "S4", 20_000)):
             sec[label] = resident_pass(hcphmm, W, name, npairs, name if npairs is None else f"{name}_{npairs}")
+        # configs[3]'s per-rank work: rank 0's shard of the S2 batch at 8 and 4
+        # ranks (shard.shard_pairs, the same cut bench.py makes at N > 1), so the
+        # driver's 1-GPU run carries the per-rank cost of its 8-GPU curve.
+        for label, nr in ((("S2_shard_125k", 8), ("S2_shard_250k", 4)) if args.workload == "S2" and not args.pairs
+                          and not args.shard_of else ()):
+            sh = W.subset(batch, shard.shard_pairs(batch["R"], batch["H"], nr)[0])
+            sec[label] = resident_pass(hcphmm, W, "S2", None, f"S2shard_{nr}", batch=sh)
+            sec[label]["per_rank_of"] = nr
+            sec[label]["implied_efficiency_vs_1gpu"] = round(
+                out["device_pass_ms"] / (nr * sec[label]["device_pass_ms"]), 4) if sec[label]["device_pass_ms"] else None
         sec.update(region_calls(hcphmm, W, args.no_cpu))
         sec["smith_waterman"] = sw_secondary(args.no_cpu)
         sec["genotyper"] = gt_secondary(args.no_cpu)

@@ -253,6 +253,8 @@ struct Part {
     double* d_spec64 = nullptr;   // speculative fp64 results (small batches, run.cpp)
     size_t res_bytes = 0;         // bytes of that contiguous output block
     size_t res_o64 = 0, res_ofl = 0;
+    uint4* d_rec = nullptr;       // seg slot result records (LaneArgs::rec), gathered by the fp64 launch
+    int* d_slot_of = nullptr;     // pair -> seg slot (-1: one-lane / anti-diagonal pair)
     int* d_list = nullptr;
     int* d_sorted = nullptr;
     int* d_worder = nullptr;      // fp64 pass: dispatch position -> wave

@@ -33,7 +33,6 @@ namespace eng {
 namespace {
 
 constexpr int kMini = 512;              // pairs per mini-task of the host passes
-constexpr size_t kRowPadBefore = 256;   // words of slack before the packed rows (run_seg prefetch)
 constexpr int kMaxGroups = 1024;        // flat_scan_kernel: one group per thread
 constexpr int kMaxBins = 1 << 20;
 
@@ -452,6 +451,8 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     const size_t tab_bytes = sizeof(int2) * (size_t(hmax) + 1) + sizeof(float) * 65 + sizeof(int2) * size_t(ngroups);
     const size_t o_tab = L.take(tab_bytes);
     const size_t row_pad = kRowPadBefore + size_t(rmax) + 256;
+    if (int64_t(rows) + int64_t(row_pad) > kMaxRowWords)
+        return fail(HC_PHMM_EINVAL, "batch too large (read bases of one part exceed 2^30)");
     const size_t o_rows = L.take(sizeof(uint32_t) * (size_t(rows) + row_pad));
     const size_t o_hapw = L.take(sizeof(uint32_t) * (size_t(hapw) + 16));
     const size_t o_pairs = L.take(sizeof(PairDesc) * n1);
@@ -467,6 +468,8 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     const size_t o_nw = L.take(sizeof(int));
     const size_t o_res = L.take(res_bytes);
     const size_t o_list = L.take(sizeof(int) * n1);
+    const size_t o_rec = L.take(sizeof(uint4) * n1);   // seg slot records (every pair is a seg pair)
+    const size_t o_slotof = L.take(sizeof(int) * n1);
     const size_t o_count = L.take(kNumCounters * sizeof(int));
     const size_t o_sorted = L.take(sizeof(int) * n1);
     const size_t o_worder = L.take(sizeof(int) * n1);
@@ -548,6 +551,8 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     b->d_big = reinterpret_cast<int*>(dev + o_big);
     b->d_big_count = reinterpret_cast<int*>(dev + o_bigc);
     b->d_plan = reinterpret_cast<Seg64Plan*>(dev + o_plan);
+    b->d_rec = reinterpret_cast<uint4*>(dev + o_rec);
+    b->d_slot_of = reinterpret_cast<int*>(dev + o_slotof);
     b->n_wide = nwide;
     if (slot) {
         b->host_res = host + host_res_off;
@@ -617,6 +622,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
         a.ngroups = ngroups;
         a.gtab = reinterpret_cast<int*>(dev + o_gtab);
         a.order = b->d_lane_order;
+        a.slot_of = b->d_slot_of;
         a.waves = b->d_lane_waves;
         a.waves_tmp = reinterpret_cast<LaneWave*>(dev + o_wtmp);
         a.tail = tail;

@@ -32,6 +32,12 @@ inline int hap_table_words(int H) { return ((H + 31) / 32 + kHapPadWords) * 5; }
 
 // Per pair descriptor: {row offset into rows[], R, word offset into hapw[], H}.
 using PairDesc = int4;
+// Words of slack before the packed rows (the column-segmented kernels
+// prefetch read words ahead without clamping). The kernels address a row word
+// as a 32-bit byte offset from rows - kRowPadBefore (one VGPR per lane, the
+// base in SGPRs), so a part's rows + slack stay below kMaxRowWords.
+constexpr long long kRowPadBefore = 256;
+constexpr long long kMaxRowWords = (1ll << 30) - 1024;
 
 // Run counters of a part (zeroed when the part is prepared): [0, 1] rescue
 // list lengths and [2, 3] in-wave rescue counts, by run parity (a run zeroes
@@ -41,6 +47,8 @@ using PairDesc = int4;
 // 64-byte line each) and its finished-wave count, which the last wave to
 // finish zeroes again for the next run (lane_kernel.hip phmm_seg_kernel).
 constexpr int kNextWave = 4;
+constexpr int kPlanTicket = 5;   // [5, 6] fp64 planner ticket, [7, 8] plan-published flag, by run parity
+constexpr int kPlanReady = 7;
 constexpr int kSegHeads = 16;
 constexpr int kSegQueues = 9;          // 8 XCD queues + the tail queue
 constexpr int kSegHeadStride = 16;     // ints: one 64-byte line per head
@@ -95,6 +103,10 @@ struct Seg64Args {
     const int* count;         // its length
     int* count_reset;         // the other run parity's counter, zeroed for the next run
     int* inker_reset;         // the other run parity's in-wave rescue counter, likewise
+    int* ticket;              // this run's planner ticket (the first workgroup to take it plans)
+    int* ready;               // this run's plan-published flag
+    int* ticket_reset;        // the other run parity's ticket and flag, zeroed for the next run
+    int* ready_reset;
     int* sorted;              // list in class order (n entries)
     int* big;                 // last-class pairs (anti-diagonal fp64 kernel)
     int* big_count;
@@ -104,6 +116,15 @@ struct Seg64Args {
     int* wave_order;          // dispatch position -> wave (n entries), see rescue_plan_kernel
     int* next_wave;           // dynamic wave counter (zeroed by the plan)
     int n_simd;               // SIMDs of the device (4 per CU)
+    // Gather of the seg slots' result records (LaneArgs::rec) into the
+    // per-pair outputs, done by this launch before its rescue work: pair p's
+    // slot is slot_of[p] (-1: computed by another kernel, already in place).
+    const uint4* rec;         // null: nothing to gather
+    const int* slot_of;
+    int n_pairs;
+    float* raw32;
+    uint8_t* flag;
+    int prio;   // as LaneArgs::prio
 };
 // Lane-per-pair kernel (large batches): one lane owns one pair and sweeps it
 // row by row over register-resident blocks of kLaneBlock columns. A wave holds
@@ -151,7 +172,17 @@ struct LaneArgs {
     // waves of the order form the shared tail queue (shortest, longest first).
     int* seg_counters;
     int n_tail;
+    // Column-segmented waves: per-slot result records instead of the per-pair
+    // outputs (null: write raw_out / rescue_flag / raw64_zero by pair id). A
+    // wave's pairs own consecutive slots, so its stores are contiguous; the
+    // fp64 pass gathers the records into the per-pair outputs (Seg64Args).
+    uint4* rec;
+    int prio;   // 1: issue priority by remaining steps (seg_common.hpp set_prio_by_remaining)
 };
+// Result record of one seg slot: {raw f32 bits, state, raw f64 low word, high
+// word}; state 0 = not rescued, 1 = rescued in the fp32 pass (raw f64 here),
+// 2 = rescued by the fp64 pass (raw f64 written there, by pair id).
+constexpr unsigned kRecPlain = 0, kRecInWave = 1, kRecListed = 2;
 
 constexpr int kInWaveRescueMaxH = 512;   // one pair over 64 lanes of 8 columns
 // Variants of the one-lane kernel (lane_kernel.hip kVariants): pairs per lane
@@ -166,7 +197,8 @@ hipError_t launch_lane_f32(int variant, const LaneArgs& a, hipStream_t s);
 // takes ceil(H / BC) lanes; BC per wave, one of the compiled block widths.
 // max_blocks > 0: at most that many workgroups (4 waves each), persistent
 // waves fetching the rest (a.seg_counters must be set).
-hipError_t launch_lane_seg_f32(const LaneArgs& a, int max_blocks, hipStream_t s);
+// queues: 8 = per-XCD queues + tail queue, 1 = one queue (persistent only).
+hipError_t launch_lane_seg_f32(const LaneArgs& a, int max_blocks, int queues, hipStream_t s);
 bool seg_width_ok(int bc);
 int seg_width_ceil(int bc);   // narrowest compiled width >= bc (-1: none)
 constexpr int kSegMaxBC = 64;
@@ -247,6 +279,7 @@ struct GridPrepArgs {
     int nwaves;
     const int *rord, *hord;
     int* order;
+    int* slot_of;    // pair -> its slot (inverse of order)
     LaneWave* waves;
     int* counters;   // kNumCounters ints zeroed (run counters)
 };
@@ -285,6 +318,7 @@ struct FlatPlanArgs {
     int ngroups;
     int* gtab;             // per group: {first slot, pairs, first wave}
     int* order;            // slot -> pair
+    int* slot_of;          // pair -> slot
     LaneWave* waves;       // the plan's waves (packing order), then the dispatch order
     LaneWave* waves_tmp;   // max_waves entries: the packing order while the tail is reordered
     int max_waves;         // waves the launch covers (upper bound of the plan's)

@@ -47,7 +47,7 @@ __device__ __forceinline__ void run_block(const LaneArgs& a, const LaneWave& wv,
         const int w0 = min(c0 / 32 + kHapLead, nwpad), w1 = min(c0 / 32 + kHapLead + 1, nwpad);
 #pragma unroll
         for (int c = 0; c < 5; ++c)
-            mt[c * 64 + lane] = make_uint2(cx.hw[w0 * 5 + c], (BC > 32) ? cx.hw[w1 * 5 + c] : 0u);
+            mt[c * 64 + lane] = make_uint2(hap_word(cx, w0 * 5 + c), (BC > 32) ? hap_word(cx, w1 * 5 + c) : 0u);
     }
     float T[BC], X[BC];
 #pragma unroll
@@ -59,7 +59,7 @@ __device__ __forceinline__ void run_block(const LaneArgs& a, const LaneWave& wv,
     const bool has_in = b > 0, has_out = b + 1 < nb;
     // Row 1's diagonal at column c0 is row 0's T (c0 = 0: column 0 of row 0, same value).
     float Tdiag = T0;
-    uint32_t wc = cx.rrow[0], wn = cx.rrow[min(2, cx.R) - 1];
+    uint32_t wc = row_word(cx, 0), wn = row_word(cx, min(2, cx.R) - 1);
     const float2 zero = make_float2(0.f, 0.f);
     float2 cin = has_in ? carry[64] : zero;   // {T, Y} of the block to the left, row 1
     RowConst<float> k;
@@ -73,7 +73,7 @@ __device__ __forceinline__ void run_block(const LaneArgs& a, const LaneWave& wv,
             row_const<float>(a.lut, wc, wn, k);
             mrow = mt[k.rc * 64 + lane];
         }
-        const uint32_t wnn = cx.rrow[min(i + 2, cx.R) - 1];
+        const uint32_t wnn = row_word(cx, min(i + 2, cx.R) - 1);
         const float2 cnext = (has_in && i < wv.rmax) ? carry[size_t(i + 1) * 64] : zero;
         float pm_n = 0.f, px_n = 0.f;
         uint2 m_n = mrow;
@@ -85,7 +85,7 @@ __device__ __forceinline__ void run_block(const LaneArgs& a, const LaneWave& wv,
         const int lim = (SUM && i == cx.R) ? cx.H - c0 : 0;
         float Ml = 0.f, Yl = cin.y;   // block 0: Y[i][1] = 0*my + 0*yy = 0
         const float M0 = Tdiag * prior_of<31>(mrow.x, k.pm, k.px);
-        cell<float, BC, 0, NC, SUM, EQ>(T, X, M0, Ml, Yl, mrow.x, mrow.y, k.pm, k.px, k, lim, sumM, sumX);
+        cell<float, BC, 0, NC, SUM, EQ, true>(T, X, M0, Ml, Yl, mrow.x, mrow.y, k.pm, k.px, k, lim, sumM, sumX);
         if (has_out) carry[size_t(i) * 64] = make_float2(T[NC - 1], y_next<EQ>(Ml, Yl, k.my, k.yy));
         // next row's diagonal at column c0: this row's T there (block 0: column 0 -> 0)
         Tdiag = has_in ? cin.x : 0.f;
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
     const bool active = slot < a.n_slots;
     const int pid = a.order[active ? slot : wv.slot0];
     const LaneCtx cx = pair_ctx(a.pairs, a.rows, a.hapw, pid);
-    const uint32_t w1 = cx.rrow[0];
+    const uint32_t w1 = row_word(cx, 0);
     const float T0 = row0_t<float>(a.lut, w1, cx.H);
     const bool wave_cg = __builtin_amdgcn_ballot_w64(!read_cg(w1)) == 0;
     const bool wave_eq = __builtin_amdgcn_ballot_w64(!read_eq(w1)) == 0;
@@ -217,117 +217,127 @@ __device__ __forceinline__ int rescue_class(int H, int bc0)
 // first, in descending cost, and the rest after them in ascending cost — the
 // heaviest wave shares its SIMD with the lightest. With more, waves are
 // fetched from a counter in descending cost (greedy longest-first). Wave
-// cost: (rows + skew) steps x (14 ops per column + ~40 per step).
+// cost: (rows + skew) steps x (14 ops per column + ~40 per step), sorted by a
+// counting sort over 256 cost buckets (order inside a bucket is arbitrary).
 constexpr int kMaxSortWaves = 8192;
+constexpr int kPlanThreads = 256;   // the planning workgroup (a phmm_seg64_kernel workgroup)
 
-__global__ __launch_bounds__(1024) void rescue_plan_kernel(Seg64Args a)
+struct PlanLds {
+    int cnt[kSeg64Classes], fill[kSeg64Classes], wbase[kSeg64Classes];
+    int hist[256];
+    unsigned long long lanes;
+    unsigned cmax;
+    unsigned cost[kMaxSortWaves];
+};
+
+// Cost of wave w (class order) of the plan in L.
+__device__ __forceinline__ unsigned wave_cost(const Seg64Args& a, const PlanLds& L, int w)
 {
     constexpr int NC = kSeg64Classes;
-    __shared__ int cnt[NC], fill[NC], wbase[NC];
-    __shared__ unsigned long long lanes_sh;
-    __shared__ unsigned long long key[kMaxSortWaves];
-    const int n = *a.count;
+    int lo = 0, hi = NC - 1;   // the last class whose first wave is <= w
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (L.wbase[mid] <= w) lo = mid;
+        else hi = mid;
+    }
+    const int c = lo;
+    const int kk = 6 - c / kSeg64Widths, per = 64 >> kk;
+    const int bc = seg64_width(kSeg64Widths - 1 - c % kSeg64Widths);
+    const int off = L.fill[c] - L.cnt[c];   // the class's first entry (fill ran past it)
+    const int e0 = off + (w - L.wbase[c]) * per;
+    const int e1 = min(off + L.cnt[c], e0 + per);
+    int rmax = 0;
+    for (int e = e0; e < e1; ++e) rmax = max(rmax, a.pairs[a.sorted[e]].y);
+    return unsigned(rmax + (1 << kk) - 1) * unsigned(bc * 14 + 40);
+}
+
+// The fp64 pass's plan over the n > 0 listed pairs, by one workgroup of the
+// fp64 launch (the first to arrive; the others wait for its flag): the width
+// bound bc0 (32 unless the lanes at width 32 give fewer than min_lanes, 2
+// waves per SIMD, then 16, then 8), the classes, the list scattered into class
+// order (`sorted`; the last class into `big`), and the dispatch order.
+__device__ void plan_rescue(const Seg64Args& a, int n, PlanLds& L)
+{
+    constexpr int NC = kSeg64Classes;
     const int t = threadIdx.x;
+    if (t < NC) L.cnt[t] = 0;
     if (t == 0) {
-        *a.count_reset = 0;
-        *a.inker_reset = 0;
+        L.lanes = 0;
+        L.cmax = 1;
         *a.next_wave = 0;
     }
-    if (n == 0) {   // most runs: an empty plan (the fp64 kernels read only its wave total and big count)
-        if (t == 0) {
-            a.plan->wave_base[NC - 1] = 0;
-            *a.big_count = 0;
-        }
-        return;
-    }
-    if (t < NC) cnt[t] = 0;
-    if (t == 0) lanes_sh = 0;
     __syncthreads();
-    // Width bound: 32 unless the lanes at width 32 give fewer than min_lanes
-    // (2 waves per SIMD), then 16, then 8.
     unsigned long long mine = 0;
-    for (int i = t; i < n; i += blockDim.x) mine += (a.pairs[a.list[i]].w + 31) / 32;
-    if (mine) atomicAdd(&lanes_sh, mine);   // an empty list (most runs) takes no atomics
+    for (int i = t; i < n; i += kPlanThreads) mine += (a.pairs[a.list[i]].w + 31) / 32;
+    if (mine) atomicAdd(&L.lanes, mine);
     __syncthreads();
-    const long long l32 = (long long)lanes_sh;
+    const long long l32 = (long long)L.lanes;
     const int bc0 = l32 >= a.min_lanes ? 32 : (2 * l32 >= a.min_lanes ? 16 : 8);
-    for (int i = t; i < n; i += blockDim.x) atomicAdd(&cnt[rescue_class(a.pairs[a.list[i]].w, bc0)], 1);
+    for (int i = t; i < n; i += kPlanThreads) atomicAdd(&L.cnt[rescue_class(a.pairs[a.list[i]].w, bc0)], 1);
     __syncthreads();
     if (t == 0) {
         Seg64Plan* __restrict__ p = a.plan;   // written in place (a local copy would live in registers)
         p->bc0 = bc0;
         int off = 0, wb = 0;
         for (int c = 0; c < NC; ++c) {
-            p->n_class[c] = cnt[c];
+            p->n_class[c] = L.cnt[c];
             p->off_class[c] = off;
-            fill[c] = off;
-            off += cnt[c];
+            L.fill[c] = off;
+            off += L.cnt[c];
             p->wave_base[c] = wb;
-            wbase[c] = wb;
+            L.wbase[c] = wb;
             if (c < NC - 1) {
                 const int per = 64 >> (6 - c / kSeg64Widths);
-                wb += (cnt[c] + per - 1) / per;
+                wb += (L.cnt[c] + per - 1) / per;
             }
         }
         p->dynamic = a.wave_order != nullptr && wb > 2 * a.n_simd;
-        *a.big_count = cnt[NC - 1];
+        *a.big_count = L.cnt[NC - 1];
     }
     __syncthreads();
-    for (int i = t; i < n; i += blockDim.x) {
+    for (int i = t; i < n; i += kPlanThreads) {
         const int pid = a.list[i];
         const int c = rescue_class(a.pairs[pid].w, bc0);
-        const int pos = atomicAdd(&fill[c], 1);
+        const int pos = atomicAdd(&L.fill[c], 1);
         if (c < NC - 1)
             a.sorted[pos] = pid;
         else
-            a.big[pos - (n - cnt[NC - 1])] = pid;
+            a.big[pos - (n - L.cnt[NC - 1])] = pid;
     }
     __syncthreads();
-    const int W = wbase[NC - 1];   // segmented waves
+    const int W = L.wbase[NC - 1];   // segmented waves
     if (W <= 1 || !a.wave_order) return;
     if (W > kMaxSortWaves) {   // classes longest first, fetched in that order
-        for (int w = t; w < W; w += blockDim.x) a.wave_order[w] = w;
+        for (int w = t; w < W; w += kPlanThreads) a.wave_order[w] = w;
         return;
     }
-    // Cost of every wave, then a bitonic sort (descending) in LDS.
-    int N = 1;
-    while (N < W) N <<= 1;
-    for (int w = t; w < N; w += blockDim.x) {
-        unsigned long long k = 0;
-        if (w < W) {
-            int c = 0;
-            while (c + 1 < NC - 1 && wbase[c + 1] <= w) ++c;
-            const int kk = 6 - c / kSeg64Widths, per = 64 >> kk;
-            const int bc = seg64_width(kSeg64Widths - 1 - c % kSeg64Widths);
-            const int off = fill[c] - cnt[c];   // the class's first entry (fill ran past it)
-            const int e0 = off + (w - wbase[c]) * per;
-            const int e1 = min(off + cnt[c], e0 + per);
-            int rmax = 0;
-            for (int e = e0; e < e1; ++e) rmax = max(rmax, a.pairs[a.sorted[e]].y);
-            const unsigned cost = unsigned(rmax + (1 << kk) - 1) * unsigned(bc * 14 + 40);
-            k = ((unsigned long long)cost << 32) | unsigned(w);
+    // Costs, then a counting sort by cost descending over 256 buckets.
+    for (int w = t; w < W; w += kPlanThreads) {
+        const unsigned c = wave_cost(a, L, w);
+        L.cost[w] = c;
+        atomicMax(&L.cmax, c);
+    }
+    L.hist[t] = 0;
+    __syncthreads();
+    const unsigned cmax = L.cmax;
+    auto bucket = [&](unsigned c) { return 255 - int((unsigned long long)c * 255 / cmax); };   // 0: costliest
+    for (int w = t; w < W; w += kPlanThreads) atomicAdd(&L.hist[bucket(L.cost[w])], 1);
+    __syncthreads();
+    if (t == 0) {   // exclusive prefix over the buckets
+        int acc = 0;
+        for (int b = 0; b < 256; ++b) {
+            const int v = L.hist[b];
+            L.hist[b] = acc;
+            acc += v;
         }
-        key[w] = k;
     }
     __syncthreads();
-    for (int size = 2; size <= N; size <<= 1)
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = t; i < N / 2; i += blockDim.x) {
-                const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
-                const bool desc = (lo & size) == 0;
-                const unsigned long long x = key[lo], y = key[hi];
-                if ((x < y) == desc) {
-                    key[lo] = y;
-                    key[hi] = x;
-                }
-            }
-            __syncthreads();
-        }
     const int S = a.n_simd;
-    for (int p = t; p < W; p += blockDim.x) {
+    for (int w = t; w < W; w += kPlanThreads) {
+        const int r = atomicAdd(&L.hist[bucket(L.cost[w])], 1);   // rank in descending cost
         // two waves per SIMD at most: positions S.. pair the heaviest with the lightest
-        const int r = (W <= 2 * S && p >= S) ? S + (W - 1 - p) : p;
-        a.wave_order[p] = int(key[r] & 0xffffffffu);
+        const int pos = (W <= 2 * S && r >= S) ? S + (W - 1 - r) : r;
+        a.wave_order[pos] = w;
     }
 }
 
@@ -365,14 +375,15 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
     const int g = gmap[lane];
     int s = gmap[64 + lane];
     __builtin_amdgcn_wave_barrier();
-    const int pid = a.order[wv.slot0 + (g >= 0 ? g : 0)];
+    const int slot = wv.slot0 + (g >= 0 ? g : 0);
+    const int pid = a.order[slot];
     const LaneCtx cx = pair_ctx(a.pairs, a.rows, a.hapw, pid);
     const bool owner = g >= 0 && s == (cx.H + bc - 1) / bc - 1;
     if (g < 0) s = 0;
-    const uint32_t w1 = cx.rrow[0];
+    const uint32_t w1 = row_word(cx, 0);
     const float T0 = row0_t<float>(a.lut, w1, cx.H);
     const bool wave_eq = __builtin_amdgcn_ballot_w64(!read_eq(w1)) == 0;
-    const SegSteps st{wv.rmax, wv.rmin, wv.nsteps};
+    const SegSteps st{wv.rmax, wv.rmin, wv.nsteps, a.prio};
     float sumM = 0.f, sumX = 0.f;
     switch (bc) {
 #define HC_SEG_CASE(W) \
@@ -386,12 +397,20 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
     if (owner) {
         const float raw = sumM + sumX;
         resc = raw < 1e-28f;   // MIN_ACCEPTED, pairhmm_common.h:16
-        a.raw_out[pid] = raw;
-        a.rescue_flag[pid] = resc;
-        if (!resc) a.raw64_zero[pid] = 0.0;
+        if (a.rec) {
+            // The wave's pairs own consecutive slots: one 16-byte record each,
+            // contiguous over the wave (3 partial lines per pair by pair id
+            // before: 0.2 GB of writes per S2 launch for 13 MB of results).
+            // A rescue in this wave rewrites the state and raw f64 after this.
+            a.rec[slot] = make_uint4(__float_as_uint(raw), resc ? kRecListed : kRecPlain, 0u, 0u);
+        } else {
+            a.raw_out[pid] = raw;
+            a.rescue_flag[pid] = resc;
+            if (!resc) a.raw64_zero[pid] = 0.0;
+        }
     }
     const uint64_t todo = __builtin_amdgcn_ballot_w64(resc);
-    if (todo) rescue_in_wave(a, todo, pid, lane, mt);
+    if (todo) rescue_in_wave(a, todo, pid, slot, lane, mt);
     if (a.timeline && lane == 0) {
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
         a.timeline[3 * size_t(wid)] = t_start;
@@ -432,31 +451,42 @@ __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
     // Device-planned parts launch an upper bound of waves: surplus workgroups
     // leave before the LDS fill (workgroup-uniform).
     const int n_waves = a.n_waves_dev ? __builtin_amdgcn_readfirstlane(*a.n_waves_dev) : a.n_waves;
+    if (int(blockIdx.x) * kSegWPB >= n_waves) return;
+    load_slut(slut, a.lut);
+    const int wid = blockIdx.x * kSegWPB + (threadIdx.x >> 6);
+    if (wid < n_waves) seg_wave(a, wid, slut);
+}
+
+// The persistent form (a separate instance: its fetch loop around the width
+// switch costs registers that the one-wave-per-slot kernel does not pay).
+// NQ = 8: per-XCD ranges + the tail queue (above); NQ = 1: one queue over the
+// whole order (the planner's order, fetched from one counter).
+template <int OCC, int NQ>
+__global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_persist_kernel(LaneArgs a)
+{
+    __shared__ float slut[kSlutLen];
+    const int n_waves = a.n_waves_dev ? __builtin_amdgcn_readfirstlane(*a.n_waves_dev) : a.n_waves;
     const int launched = int(gridDim.x) * kSegWPB;
-    const bool persist = a.seg_counters && n_waves > launched;
-    if (!persist && int(blockIdx.x) * kSegWPB >= n_waves) return;
     load_slut(slut, a.lut);
     int* const heads = a.seg_counters + kSegHeads;
     const int G = int(gridDim.x);
-    const int bulk = n_waves - min(a.n_tail, n_waves);
-    const int q0 = int(blockIdx.x) & 7;
-    // Range of group r: [r * bulk / 8, (r + 1) * bulk / 8); queue 8 = the tail.
-    auto lo_of = [&](int r) { return r < 8 ? int((long long)r * bulk / 8) : bulk; };
-    auto hi_of = [&](int r) { return r < 8 ? int((long long)(r + 1) * bulk / 8) : n_waves; };
-    // waves launched in group r (workgroups r, r + 8, ...): its static round
-    auto nstat_of = [&](int r) { return r < 8 && r < G ? ((G - 1 - r) / 8 + 1) * kSegWPB : 0; };
-    // k = -1: the static position (one wave per slot without persistence);
-    // k = 0..7: group (q0 + k) % 8's range; k = 8: the tail queue. One call
-    // site of seg_wave (its width switch is large: a second copy spills).
-    for (int k = -1; k <= 8;) {
+    const int bulk = NQ == 1 ? n_waves : n_waves - min(a.n_tail, n_waves);
+    const int q0 = NQ == 1 ? 0 : int(blockIdx.x) & 7;
+    // Range of group r: [r * bulk / NQ, (r + 1) * bulk / NQ); queue NQ = the tail.
+    auto lo_of = [&](int r) { return r < NQ ? int((long long)r * bulk / NQ) : bulk; };
+    auto hi_of = [&](int r) { return r < NQ ? int((long long)(r + 1) * bulk / NQ) : n_waves; };
+    // waves launched in group r (workgroups r, r + NQ, ...): its static round
+    auto nstat_of = [&](int r) { return r < NQ && r < G ? ((G - 1 - r) / NQ + 1) * kSegWPB : 0; };
+    // k = -1: the static position; k = 0 .. NQ-1: group (q0 + k) % NQ's
+    // range; k = NQ: the tail queue. One call site of seg_wave.
+    for (int k = -1; k <= NQ;) {
         int pos;
         if (k < 0) {
-            k = persist ? 0 : 9;
-            pos = persist ? lo_of(q0) + (int(blockIdx.x) >> 3) * kSegWPB + (threadIdx.x >> 6)
-                          : int(blockIdx.x) * kSegWPB + (threadIdx.x >> 6);
-            if (pos >= (persist ? hi_of(q0) : n_waves)) continue;
+            k = 0;
+            pos = lo_of(q0) + (int(blockIdx.x) / NQ) * kSegWPB + (threadIdx.x >> 6);
+            if (pos >= hi_of(q0)) continue;
         } else {
-            const int r = k < 8 ? (q0 + k) & 7 : 8;
+            const int r = k < NQ ? (q0 + k) % NQ : NQ;
             pos = lo_of(r) + nstat_of(r) + seg_fetch(heads + r * kSegHeadStride);
             if (pos >= hi_of(r)) {
                 ++k;
@@ -466,7 +496,7 @@ __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
         }
         seg_wave(a, pos, slut);
     }
-    if (persist && seg_fetch(a.seg_counters + kSegDone) == launched - 1 && (threadIdx.x & 63) < kSegQueues) {
+    if (seg_fetch(a.seg_counters + kSegDone) == launched - 1 && (threadIdx.x & 63) < kSegQueues) {
         heads[(threadIdx.x & 63) * kSegHeadStride] = 0;
         if ((threadIdx.x & 63) == 0) a.seg_counters[kSegDone] = 0;
     }
@@ -491,9 +521,72 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
 {
     __shared__ uint2 mtab[4][5 * 64];
     __shared__ double slut[kSlutLen];
+    __shared__ PlanLds plan_lds;
+    __shared__ int role;
+    const int t = threadIdx.x;
+    // The fp32 pass's rescue list is complete (stream order). Its plan is
+    // made here, not by a launch of its own: an empty list (most runs) needs
+    // none, and otherwise the first workgroup to arrive plans while the others
+    // gather the seg records, then wait for its flag (they never wait on a
+    // workgroup that is not running: the planner is the first one running).
+    const int n = __builtin_amdgcn_readfirstlane(*a.count);
+    if (blockIdx.x == 0 && t == 0) {   // the other run parity's counters, zeroed for the next run
+        *a.count_reset = 0;
+        *a.inker_reset = 0;
+        *a.ticket_reset = 0;
+        *a.ready_reset = 0;
+        if (n == 0) *a.big_count = 0;   // the wide fp64 kernel's list (the plan writes it otherwise)
+    }
+    if (t == 0) role = n > 0 ? atomicAdd(a.ticket, 1) : 1;
+    __syncthreads();
+    const bool planner = role == 0;
+    if (planner) {
+        plan_rescue(a, n, plan_lds);
+        // Publish (MI355X_MICROARCH.md, inter-workgroup visibility): every
+        // storing wave drains its stores, then one lane releases and flags.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(a.ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (a.rec) {
+        // The fp32 pass's seg results, slot records -> per-pair outputs (pair
+        // order: coalesced stores; the record reads are gathers). A pair the
+        // rescue below recomputes (state kRecListed) gets its raw f64 there.
+        for (int q = blockIdx.x * 256 + threadIdx.x; q < a.n_pairs; q += gridDim.x * 256) {
+            const int s = a.slot_of[q];
+            if (s < 0) continue;   // computed by a one-lane / anti-diagonal kernel: in place already
+            const uint4 r = a.rec[s];
+            a.raw32[q] = __uint_as_float(r.x);
+            a.flag[q] = r.y != kRecPlain;
+            if (r.y != kRecListed)
+                a.raw_out[q] = __longlong_as_double((long long)(((unsigned long long)r.w << 32) | r.z));
+        }
+    }
+    if (n == 0) return;   // most runs: nothing to rescue
+    if (!planner) {
+        if (t == 0) {
+            int ok = 0;
+            for (int it = 0; it < (1 << 24); ++it) {   // bounded: a wave never waits forever
+                if (__hip_atomic_load(a.ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                    ok = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(8);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            role = ok ? 1 : -1;
+        }
+        __syncthreads();
+        if (role < 0) return;   // (not expected) no plan: leave the rescue undone rather than read a stale one
+    }
     const Seg64Plan* __restrict__ p = a.plan;
     const int total = __builtin_amdgcn_readfirstlane(p->wave_base[kSeg64Classes - 1]);
-    if (int(blockIdx.x) * 4 >= total) return;   // workgroup-uniform: an empty or short list costs no LDS fill
+    if (int(blockIdx.x) * 4 >= total) return;   // workgroup-uniform: a short list costs no LDS fill
     load_slut(slut, a.lut);
     uint2* mt = mtab[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
@@ -524,8 +617,8 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
         const bool owner = valid && s == nb - 1;
         if (!valid) s = 0;
         const SegSteps st{wave_max(valid ? cx.R : 0), wave_min(valid ? cx.R : INT32_MAX),
-                          wave_max(valid ? cx.R + nb - 1 : 0)};
-        const uint32_t w1 = cx.rrow[0];
+                          wave_max(valid ? cx.R + nb - 1 : 0), a.prio};
+        const uint32_t w1 = row_word(cx, 0);
         const double T0 = row0_t<double>(a.lut, w1, cx.H);
         const bool wave_eq = __builtin_amdgcn_ballot_w64(!read_eq(w1)) == 0;
         double sumM = 0.0, sumX = 0.0;
@@ -605,12 +698,20 @@ int seg_width_ceil(int bc)
     return -1;
 }
 
-hipError_t launch_lane_seg_f32(const LaneArgs& a, int max_blocks, hipStream_t s)
+hipError_t launch_lane_seg_f32(const LaneArgs& a, int max_blocks, int queues, hipStream_t s)
 {
     if (a.n_waves <= 0) return hipSuccess;
-    int grid = (a.n_waves + kSegWPB - 1) / kSegWPB;
-    if (max_blocks > 0 && a.seg_counters && grid > max_blocks) grid = max_blocks;
-    hipLaunchKernelGGL((phmm_seg_kernel<kSegOcc>), dim3(grid), dim3(64 * kSegWPB), 0, s, a);
+    const int grid = (a.n_waves + kSegWPB - 1) / kSegWPB;
+    // Persistent only when the waves outnumber the launch's slots (device-
+    // planned parts: their upper bound does; the kernel re-reads the count).
+    if (max_blocks > 0 && a.seg_counters && grid > max_blocks) {
+        if (queues == 8)
+            hipLaunchKernelGGL((phmm_seg_persist_kernel<kSegOcc, 8>), dim3(max_blocks), dim3(64 * kSegWPB), 0, s, a);
+        else
+            hipLaunchKernelGGL((phmm_seg_persist_kernel<kSegOcc, 1>), dim3(max_blocks), dim3(64 * kSegWPB), 0, s, a);
+    } else {
+        hipLaunchKernelGGL((phmm_seg_kernel<kSegOcc>), dim3(grid), dim3(64 * kSegWPB), 0, s, a);
+    }
     return hipGetLastError();
 }
 
@@ -623,9 +724,6 @@ hipError_t launch_all_f64_list(int n, float* raw32, uint8_t* flag, int* list, in
 
 hipError_t launch_rescue_seg64(const Seg64Args& a, int grid, hipStream_t s)
 {
-    hipLaunchKernelGGL(rescue_plan_kernel, dim3(1), dim3(1024), 0, s, a);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((phmm_seg64_kernel<kSeg64Occ>), dim3(grid), dim3(256), 0, s, a);
     return hipGetLastError();
 }

@@ -173,7 +173,7 @@ __device__ __forceinline__ void grid_pairs(const GridBlock* __restrict__ blocks,
 __device__ __forceinline__ void grid_waves(const GridSeg* __restrict__ segs, int nsegs, long long nslots, int nwaves,
                                            const int* __restrict__ rord, const int* __restrict__ hord,
                                            const int4* __restrict__ rdesc, int* __restrict__ order,
-                                           LaneWave* __restrict__ waves)
+                                           int* __restrict__ slot_of, LaneWave* __restrict__ waves)
 {
     const long long stride = 256ll * gridDim.x;
     for (long long t = blockIdx.x * 256ll + threadIdx.x; t < nslots; t += stride) {
@@ -186,7 +186,9 @@ __device__ __forceinline__ void grid_waves(const GridSeg* __restrict__ segs, int
         const GridSeg g = segs[lo];
         const long long i = t - g.slot0;
         const int rr = int(i / g.G), hh = int(i % g.G);
-        order[t] = int(g.p0 + (long long)(rord[g.r0 + rr] - g.r0) * g.nh + (hord[g.g0 + hh] - g.h0));
+        const int p = int(g.p0 + (long long)(rord[g.r0 + rr] - g.r0) * g.nh + (hord[g.g0 + hh] - g.h0));
+        order[t] = p;
+        slot_of[p] = int(t);
     }
     for (long long w = blockIdx.x * 256ll + threadIdx.x; w < nwaves; w += stride) {
         int lo = 0, hi = nsegs;   // the last segment with w0 <= w (segments without waves share w0)
@@ -224,7 +226,7 @@ __global__ __launch_bounds__(256) void prepare_grid_kernel(GridPrepArgs a)
     if (blockIdx.x == 0 && threadIdx.x < kNumCounters) a.counters[threadIdx.x] = 0;
     pack_items(a.pack);
     grid_pairs(a.blocks, a.nblocks, a.npairs, a.pack.rdesc, a.pack.hdesc, a.pairs);
-    grid_waves(a.segs, a.nsegs, a.nslots, a.nwaves, a.rord, a.hord, a.pack.rdesc, a.order, a.waves);
+    grid_waves(a.segs, a.nsegs, a.nslots, a.nwaves, a.rord, a.hord, a.pack.rdesc, a.order, a.slot_of, a.waves);
 }
 
 // ---------------------------------------------------------------------------
@@ -373,6 +375,7 @@ __global__ __launch_bounds__(256) void flat_scatter_kernel(FlatPlanArgs a)
     for (int p = blockIdx.x * 256 + threadIdx.x; p < a.n; p += gridDim.x * 256) {
         const int pos = atomicAdd(&a.hist[a.bin_of[p]], 1);
         a.order[pos] = p;
+        a.slot_of[p] = pos;
     }
 }
 

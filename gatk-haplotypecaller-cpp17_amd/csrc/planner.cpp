@@ -21,7 +21,6 @@ namespace {
 
 constexpr int kW64Threshold = 768;     // anti-diagonal kernel: H above this -> one pair per wave
 constexpr int kLaneMaxH = 4096;        // longer haps stay on the anti-diagonal kernel (policy "auto")
-constexpr size_t kRowPadBefore = 256;  // words of slack before the packed rows (run_seg prefetch)
 constexpr int kSegWavesPerSimd = 3;    // resident seg waves per SIMD (phmm_seg_kernel occupancy)
 
 int lane_variant_id() { return int(env_i64("HC_PHMM_LANE_VARIANT", 0)); }
@@ -447,6 +446,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const size_t o_rd = U.take(sizeof(int4) * size_t(nr));
     const size_t o_hd = U.take(sizeof(int4) * size_t(nh));
     const size_t o_ord = U.take(sizeof(int) * size_t(npairs));
+    const size_t o_slotof = U.take(sizeof(int) * size_t(npairs));   // pair -> seg slot (-1: other kernels)
     const size_t o_bases = U.take(size_t(nrows) / 2 + 16);
     const size_t o_quals = U.take(size_t(nrows) + 16);
     const size_t gap_stride = (size_t(ngap) + 16 + 15) & ~size_t(15);
@@ -878,6 +878,13 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const size_t o_ord0 = size_t(n_seg_slots) + one_ord.size();
     std::memcpy(ordp + o_ord0, ord2[0].data(), sizeof(int) * ord2[0].size());
     std::memcpy(ordp + o_ord0 + ord2[0].size(), ord2[1].data(), sizeof(int) * ord2[1].size());
+    if (!dev_plan) {   // structured plans build it on the device (grid_waves)
+        int* so = reinterpret_cast<int*>(host + o_slotof);
+        parallel_for(npairs, [&](int64_t lo, int64_t hi) { std::fill(so + lo, so + hi, -1); }, 1 << 16);
+        parallel_for(int64_t(seg_ord.size()), [&](int64_t lo, int64_t hi) {
+            for (int64_t k = lo; k < hi; ++k) so[seg_ord[size_t(k)]] = int(k);
+        }, 1 << 16);
+    }
     std::memcpy(host + o_lw, lw.data(), sizeof(LaneWave) * lw.size());
     size_t upload = o_lw + sizeof(LaneWave) * (dev_plan ? size_t(n_seg_waves) : lw.size());
     // Structured plans: the pair descriptors, the slot order and the waves are
@@ -954,9 +961,12 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     // shorter than its wave's longest read up to that length + 64 past it;
     // those words only feed rows that are never used.
     const size_t row_pad = kRowPadBefore + size_t(rlen_max.load()) + 256;
+    if (int64_t(nrows) + int64_t(row_pad) > kMaxRowWords)
+        return fail(HC_PHMM_EINVAL, "batch too large (read bases of one part exceed 2^30)");
     const size_t o_rows = L.take(sizeof(uint32_t) * (size_t(nrows) + row_pad));
     const size_t o_hapw = L.take(sizeof(uint32_t) * (size_t(hap_w[size_t(nh)]) + 16));
     const size_t o_res = L.take(res_bytes);
+    const size_t o_rec = L.take(sizeof(uint4) * std::max<size_t>(size_t(n_seg_slots), 1));   // seg slot records
     const size_t o_list = L.take(sizeof(int) * n1);
     const size_t o_count = L.take(kNumCounters * sizeof(int));   // run counters (kernels.hpp kNumCounters)
     const size_t o_sorted = L.take(sizeof(int) * n1);
@@ -1045,6 +1055,8 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     b->d_big = reinterpret_cast<int*>(dev + o_big);
     b->d_big_count = reinterpret_cast<int*>(dev + o_bigc);
     b->d_plan = reinterpret_cast<Seg64Plan*>(dev + o_plan);
+    b->d_rec = n_seg_slots > 0 ? reinterpret_cast<uint4*>(dev + o_rec) : nullptr;
+    b->d_slot_of = reinterpret_cast<int*>(dev + o_slotof);
     b->n_wide = wide_a.load();
     b->wide_ring_blocks = wide_ring_blocks;
     b->d_carry = carry_rows ? reinterpret_cast<float2*>(dev + o_carry) : nullptr;
@@ -1103,6 +1115,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             g.rord = reinterpret_cast<const int*>(dev + o_gr);
             g.hord = reinterpret_cast<const int*>(dev + o_gh);
             g.order = reinterpret_cast<int*>(dev + o_ord);
+            g.slot_of = b->d_slot_of;
             g.waves = reinterpret_cast<LaneWave*>(dev + o_lw);
             g.counters = b->d_count;
             HIP_TRY(launch_prepare_grid(g, s));

@@ -39,6 +39,10 @@ int run_part(Part* b, hipStream_t s)
     r.count = count;
     r.count_reset = b->d_count + (par ^ 1);
     r.inker_reset = b->d_count + 2 + (par ^ 1);
+    r.ticket = b->d_count + kPlanTicket + par;
+    r.ticket_reset = b->d_count + kPlanTicket + (par ^ 1);
+    r.ready = b->d_count + kPlanReady + par;
+    r.ready_reset = b->d_count + kPlanReady + (par ^ 1);
     r.sorted = b->d_sorted;
     r.big = b->d_big;
     r.big_count = b->d_big_count;
@@ -48,6 +52,15 @@ int run_part(Part* b, hipStream_t s)
     r.wave_order = env_i64("HC_PHMM_RESCUE_ORDER", 1) != 0 ? b->d_worder : nullptr;   // 0: class order (A/B)
     r.next_wave = b->d_count + kNextWave;
     r.n_simd = 4 * dv.n_cu;
+    r.n_pairs = int(b->n);
+    // Issue priority by remaining steps (seg_common.hpp set_prio_by_remaining):
+    // on for the fp64 pass (S4: fp64 0.476 -> 0.462 ms), off for the fp32 pass
+    // (S2 8.66 -> 8.81 ms, 125k pairs 1.22 -> 1.25 ms); HC_PHMM_PRIO /
+    // HC_PHMM_PRIO64 override (A/B).
+    const int prio = int(env_i64("HC_PHMM_PRIO", 0));
+    r.prio = int(env_i64("HC_PHMM_PRIO64", 1));
+    r.raw32 = b->d_raw32;
+    r.flag = b->d_flag;
     // initNative(use_double = true): no fp32 pass, every pair to the fp64 one
     // (intel_pairhmm.hpp:71,81,135-140).
     const bool all_f64 = (g_flags.load(std::memory_order_relaxed) & HC_PHMM_FLAG_F64) != 0;
@@ -67,6 +80,7 @@ int run_part(Part* b, hipStream_t s)
         a.rescue_count = count;
         a.raw64_zero = b->d_raw64;
         a.lut64 = dv.lut_d;
+        a.prio = prio;
         if (env_i64("HC_PHMM_RESCUE_IN_WAVE", 1) != 0) {
             a.inker_count = b->d_count + 2 + par;
             // A wave that rescues in place runs up to ~2.5x longer; a few such
@@ -104,10 +118,13 @@ int run_part(Part* b, hipStream_t s)
             g.waves = b->d_lane_waves;
             g.n_waves = b->n_seg_waves;
             g.n_waves_dev = b->d_nwaves;
-            // Persistent waves (HC_PHMM_SEG_PERSIST=0: one wave per launched
-            // slot, the hardware dispatching them in order; A/B only).
+            // Persistent waves fetching from per-XCD queues
+            // (HC_PHMM_SEG_PERSIST=1) or one queue (=2); default 0: one wave
+            // per launched slot, the hardware dispatching them in order (the
+            // persistent forms measured no faster).
             int max_blocks = 0;
-            if (env_i64("HC_PHMM_SEG_PERSIST", 1) != 0) {
+            const int persist = int(env_i64("HC_PHMM_SEG_PERSIST", 0));
+            if (persist != 0) {
                 g.seg_counters = b->d_count;
                 g.n_tail = b->seg_tail;
                 max_blocks = int(std::max<int64_t>(1, env_i64("HC_PHMM_SEG_BLOCKS_PER_CU", 3))) * dv.n_cu;
@@ -116,7 +133,10 @@ int run_part(Part* b, hipStream_t s)
                 HIP_TRY(hipEventRecord(b->fork, s));
                 HIP_TRY(hipStreamWaitEvent(b->side, b->fork, 0));
             }
-            HIP_TRY(launch_lane_seg_f32(g, max_blocks, fork ? b->side : s));
+            g.rec = b->d_rec;
+            r.rec = b->d_rec;   // the fp64 launch gathers the seg slots' records
+            r.slot_of = b->d_slot_of;
+            HIP_TRY(launch_lane_seg_f32(g, max_blocks, persist == 2 ? 1 : 8, fork ? b->side : s));
             if (fork) HIP_TRY(hipEventRecord(b->join, b->side));
         }
         if (n_one > 0) {

@@ -73,7 +73,10 @@ __device__ __forceinline__ double prior_of(uint32_t w, double pm, double px)
 // product M*mx that feeds X[J] is also the M*my term of the next column's Y:
 // one multiply fewer per cell, the same rounded values. Ml then carries that
 // product instead of M.
-template <typename T, int BC, int J, int NC, bool SUM, bool EQ>
+// MASK (the one-lane kernel, whose blocks start at column 1): only columns
+// J < lim enter the sums (lim = columns of the block inside the hap on the
+// pair's last row, else 0).
+template <typename T, int BC, int J, int NC, bool SUM, bool EQ, bool MASK = false>
 __device__ __forceinline__ void cell(T (&Tt)[BC], T (&X)[BC], T M, T& Ml, T& Yl, uint32_t mw0, uint32_t mw1,
                                      T pm, T px, const RowConst<T>& k, int lim, T& sumM, T& sumX)
 {
@@ -95,13 +98,19 @@ __device__ __forceinline__ void cell(T (&Tt)[BC], T (&X)[BC], T M, T& Ml, T& Yl,
             X[J] = M * k.mx + Xc * k.xx;
             Ml = M;
         }
-        if constexpr (SUM) {
+        if constexpr (SUM && MASK) {
             const bool c = J < lim;   // column c0+J+1 <= H on the pair's last row
             sumM = sumM + (c ? M : T(0));
             sumX = sumX + (c ? Xc : T(0));
+        } else if constexpr (SUM) {
+            // Every column of a block is a hap column or a zero padding column
+            // (run_seg), so the row's sums need no column mask; rows other than
+            // the pair's last accumulate values that run_seg discards.
+            sumM = sumM + M;
+            sumX = sumX + Xc;
         }
         Yl = Y;
-        cell<T, BC, J + 1, NC, SUM, EQ>(Tt, X, Mn, Ml, Yl, mw0, mw1, pm, px, k, lim, sumM, sumX);
+        cell<T, BC, J + 1, NC, SUM, EQ, MASK>(Tt, X, Mn, Ml, Yl, mw0, mw1, pm, px, k, lim, sumM, sumX);
     }
 }
 
@@ -116,11 +125,31 @@ __device__ __forceinline__ T y_next(T Ml, T Yl, T my, T yy)
         return Ml * my + Yl * yy;
 }
 
+// A lane's pair: its read rows and hap match table as 32-bit offsets from the
+// part's uniform bases (one VGPR each per lane and SGPR bases, so the loads
+// take the global_load SGPR-base + VGPR-offset form and no 64-bit address
+// stays live per lane: they spilled).
 struct LaneCtx {
-    const uint32_t* rrow;   // the read's packed rows
-    const uint32_t* hw;     // the hap's match table
+    const uint32_t* rbase;  // rows - kRowPadBefore (uniform)
+    uint32_t rbyte;         // byte offset of the read's first row word from rbase
+    const uint32_t* hbase;  // the part's hap tables (uniform)
+    uint32_t hbyte;         // byte offset of the hap's match table from hbase
     int R, H;
 };
+
+// Row word idx of the lane's read (idx may be negative, down to
+// -kRowPadBefore: prefetches before a read's first row).
+__device__ __forceinline__ uint32_t row_word(const LaneCtx& cx, int idx)
+{
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(cx.rbase) +
+                                             (cx.rbyte + unsigned(idx) * 4u));
+}
+// Word idx of the lane's hap match table.
+__device__ __forceinline__ uint32_t hap_word(const LaneCtx& cx, int idx)
+{
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(cx.hbase) +
+                                             (cx.hbyte + unsigned(idx) * 4u));
+}
 
 // Row-0 diagonal T0 = (0*mm + 0*gapm) + (INITIAL/H)*gapm with row 1's
 // constants (avx-pairhmm-template.h:160-166: Y[0][j] = INITIAL / H).
@@ -137,7 +166,7 @@ __device__ __forceinline__ LaneCtx pair_ctx(const PairDesc* pairs, const uint32_
                                             int pid)
 {
     const PairDesc pd = pairs[pid];
-    return LaneCtx{rows + pd.x, hapw + pd.z, pd.y, pd.w};
+    return LaneCtx{rows - kRowPadBefore, unsigned(pd.x + kRowPadBefore) * 4u, hapw, unsigned(pd.z) * 4u, pd.y, pd.w};
 }
 
 // Constant-gap tag of a read: bit 31 of its first row word (pack_reads_kernel).
@@ -169,10 +198,25 @@ __device__ __forceinline__ double masked(double v, uint32_t m)
 
 // Step bounds of a column-segmented wave (wave-uniform).
 struct SegSteps {
-    int rmax;     // rows swept by every lane
+    int rmax;     // max R of the wave's pairs
     int rmin;     // first step that may need the row sums
     int nsteps;   // max over the wave's pairs of R + nb - 1
+    int prio = 0; // 1: issue priority by remaining steps (set_prio_by_remaining)
 };
+
+// VALU issue between the waves of a SIMD is arbitrated by priority, then age
+// (MI355X_MICROARCH.md, two waves per SIMD): the oldest wave runs ahead and
+// the last waves of a pass, the youngest, are left to finish alone at half
+// the issue rate. With prio on, a wave raises its priority with the steps it
+// has left (longest remaining first), so co-resident waves tend to finish
+// together. s_setprio takes an immediate: four uniform branches.
+__device__ __forceinline__ void set_prio_by_remaining(int rem)
+{
+    if (rem > 192) __builtin_amdgcn_s_setprio(3);
+    else if (rem > 96) __builtin_amdgcn_s_setprio(2);
+    else if (rem > 32) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
 
 // Rows of read words a lane keeps in flight (loaded PD steps before use). A
 // lone step of a narrow block is too short to cover a global load, so narrow
@@ -224,21 +268,28 @@ __device__ __forceinline__ void load_slut(T* __restrict__ slut, const T* __restr
 //     one step in a register),
 //   - on row R, the running sums ΣM, ΣX, so the final sums are accumulated
 //     column by column left to right exactly as the reference does.
-// Lanes outside 1 <= i <= rmax (pipeline fill / drain) are masked off; columns
-// past H compute values that only flow right and are never summed.
+// A lane computes rows 1 .. R of its pair (pipeline fill / drain and a
+// shorter pair's steps past its R are masked off).
+// Block 0 starts `pad` = nb*BC - H columns left of column 1: those padding
+// columns hold exact zeros (row 0's T is 0 left of column 0, so their M, X, Y
+// and T stay 0 on every row, and column 0's T is T0 on row 0 and 0 below, as
+// the reference's boundary), so the pair's last block ends exactly at column
+// H and the last row's sums add only hap columns and leading +0.0 terms —
+// the reference's sums, with no per-column mask.
 // A lane's match window: columns c0+1 .. c0+64 of the hap's match table
 // (rows of 32 bits, MSB first, kHapLead zero rows before), for each of the 5
 // read codes, into its LDS slots mt[code * 64 + lane].
-__device__ __forceinline__ void fill_window(uint2* __restrict__ mt, int lane, const uint32_t* __restrict__ hw, int H,
-                                            int c0)
+__device__ __forceinline__ void fill_window(uint2* __restrict__ mt, int lane, const LaneCtx& cx, int c0)
 {
+    const int H = cx.H;
     const int nwpad = (H + 31) / 32 + kHapLead;   // the trailing zero row
-    const int w0 = c0 / 32 + kHapLead, r = c0 & 31;
+    const int w0 = (c0 >> 5) + kHapLead, r = c0 & 31;   // c0 >= -63 (block 0's padding): floor division
     const int i0 = min(w0, nwpad), i1 = min(w0 + 1, nwpad), i2 = min(w0 + 2, nwpad);
 #pragma unroll
     for (int c = 0; c < 5; ++c) {
-        const uint64_t x01 = (uint64_t(hw[i0 * 5 + c]) << 32) | hw[i1 * 5 + c];
-        const uint64_t x12 = (uint64_t(hw[i1 * 5 + c]) << 32) | hw[i2 * 5 + c];
+        const uint32_t h0 = hap_word(cx, i0 * 5 + c), h1 = hap_word(cx, i1 * 5 + c), h2 = hap_word(cx, i2 * 5 + c);
+        const uint64_t x01 = (uint64_t(h0) << 32) | h1;
+        const uint64_t x12 = (uint64_t(h1) << 32) | h2;
         mt[c * 64 + lane] = make_uint2(uint32_t((x01 << r) >> 32), uint32_t((x12 << r) >> 32));
     }
 }
@@ -249,25 +300,26 @@ __device__ __forceinline__ void run_seg(const T* __restrict__ lut, const T* __re
                                         uint2* __restrict__ mt)
 {
     constexpr int PD = seg_prefetch<T, BC>();
-    const int c0 = s * BC;
+    const int pad = ((cx.H + BC - 1) / BC) * BC - cx.H;   // zero columns left of column 1 (block 0)
+    const int c0 = s * BC - pad;                          // this block: columns c0+1 .. c0+BC
     const int R = cx.R;
-    fill_window(mt, lane, cx.hw, cx.H, c0);
+    fill_window(mt, lane, cx, c0);
     T Tt[BC], X[BC];
 #pragma unroll
     for (int j = 0; j < BC; ++j) {
-        Tt[j] = T0;   // row 0
+        Tt[j] = c0 + j + 1 >= 0 ? T0 : T(0);   // row 0: T0 from column 0 on, 0 on the padding left of it
         X[j] = T(0);
     }
     // wq[P]: the word of row i+1 (clamped to 1..R) at the steps of phase
     // P = (k-1) mod PD, for every lane at every step; the loads are issued
     // unconditionally so that each path has the same outstanding loads and
     // the wait for a word is the one PD steps after its load.
-    uint32_t wc = cx.rrow[0];
+    uint32_t wc = row_word(cx, 0);
     uint32_t wq[PD];
 #pragma unroll
-    for (int P = 0; P < PD; ++P) wq[P] = cx.rrow[min(max(P + 2 - s, 1), R) - 1];
+    for (int P = 0; P < PD; ++P) wq[P] = row_word(cx, min(max(P + 2 - s, 1), R) - 1);
     RowConst<T> k;
-    row_const<T>(lut, wc, cx.rrow[min(2, R) - 1], k);
+    row_const<T>(lut, wc, row_word(cx, min(2, R) - 1), k);
     uint2 mrow = mt[k.rc * 64 + lane];
     // A pair's last block (and any lane past it) hands zeros to the lane on its
     // right, so a group's first lane needs no select: it receives Y = 0 entering
@@ -277,8 +329,11 @@ __device__ __forceinline__ void run_seg(const T* __restrict__ lut, const T* __re
     const uint32_t keep = (s + 1) * BC < cx.H ? 0xffffffffu : 0u;
     T y_out = T(0);                      // handed to lane s+1: Y past column c0+BC,
     T t_out = masked(T0, keep);          //   T[BC-1] of the last row
-    T t_hold = T0;                       // lane s-1's right-edge T of the previous row
-    const int lim0 = cx.H - c0;     // columns of this block inside the hap (<= 0: none)
+    T t_hold = c0 >= 0 ? T0 : T(0);      // lane s-1's right-edge T of the previous row (row 0: column c0's)
+    // Running row sums (sumM, sumX): every lane adds its columns on every
+    // sum-variant step and restarts from its left neighbour's at its last row
+    // R; a lane stops at row R (rows past a pair's R feed nothing), so after
+    // the sweep the pair's last block holds the pair's sums.
     auto step = [&](int kk, auto sum_tag, auto ph_tag) {
         constexpr bool SUM = decltype(sum_tag)::value;
         constexpr int P = decltype(ph_tag)::value;
@@ -301,7 +356,7 @@ __device__ __forceinline__ void run_seg(const T* __restrict__ lut, const T* __re
         } else {
             asm volatile("" : "+v"(ridx) : "v"(wn));
         }
-        wq[P] = cx.rrow[ridx];
+        wq[P] = row_word(cx, ridx);
         const T y_in = from_left(y_out);
         const T t_in = from_left(t_out);
         T sM_in = T(0), sX_in = T(0);
@@ -315,20 +370,18 @@ __device__ __forceinline__ void run_seg(const T* __restrict__ lut, const T* __re
         const T Tdiag = t_hold;
         const T Yl0 = y_in;   // block 0: Y[i][1] = 0*my + 0*yy = 0 (likewise)
         t_hold = t_in;
-        if (unsigned(i - 1) < unsigned(st.rmax)) {
+        if (unsigned(i - 1) < unsigned(R)) {   // this lane's rows 1 .. R of its pair
             if constexpr (!CG) {
                 row_const<T>(lut, wc, wn, k);
                 mrow = mt[k.rc * 64 + lane];
             }
-            const bool last = SUM && i == R;
-            const int lim = last ? lim0 : 0;
-            if (last) {
+            if (SUM && i == R) {
                 sumM = s ? sM_in : T(0);
                 sumX = s ? sX_in : T(0);
             }
             T Ml = T(0), Yl = Yl0;
             const T M0 = Tdiag * prior_of<31>(mrow.x, k.pm, k.px);
-            cell<T, BC, 0, BC, SUM, EQ>(Tt, X, M0, Ml, Yl, mrow.x, mrow.y, k.pm, k.px, k, lim, sumM, sumX);
+            cell<T, BC, 0, BC, SUM, EQ>(Tt, X, M0, Ml, Yl, mrow.x, mrow.y, k.pm, k.px, k, 0, sumM, sumX);
             y_out = masked(y_next<EQ>(Ml, Yl, k.my, k.yy), keep);
             t_out = masked(Tt[BC - 1], keep);
             if constexpr (CG) {
@@ -346,10 +399,21 @@ __device__ __forceinline__ void run_seg(const T* __restrict__ lut, const T* __re
     // Groups of PD steps (phases 0..PD-1); the sum variant from the group that
     // holds step rmin on (extra steps past nsteps find every lane inactive).
     int kk = 1;
-    for (; kk + PD - 1 < st.rmin; kk += PD)
+    int pk = st.prio ? 1 : INT32_MAX;   // next step at which the priority is updated (every 16 steps)
+    for (; kk + PD - 1 < st.rmin; kk += PD) {
+        if (kk >= pk) {
+            set_prio_by_remaining(st.nsteps - kk);
+            pk += 16;
+        }
         for_phases<0, PD>([&](auto ph) { step(kk + decltype(ph)::value, std::false_type{}, ph); });
-    for (; kk <= st.nsteps; kk += PD)
+    }
+    for (; kk <= st.nsteps; kk += PD) {
+        if (kk >= pk) {
+            set_prio_by_remaining(st.nsteps - kk);
+            pk += 16;
+        }
         for_phases<0, PD>([&](auto ph) { step(kk + decltype(ph)::value, std::true_type{}, ph); });
+    }
 }
 
 // Two compiled paths per width: EQ (the reference's constant 'I'/'I'/'+' gap
@@ -374,27 +438,38 @@ __device__ __forceinline__ void run_seg_bc(const T* __restrict__ lut, const T* _
 // others are appended to the rescue list for that pass.
 // fp64 recompute of pair rp by the whole wave (H <= kInWaveRescueMaxH: 64
 // lanes of 8 columns), raw f64 sum to raw64_zero[rp].
-__device__ __forceinline__ void rescue_one(const LaneArgs& a, int rp, int lane, uint2* __restrict__ mt)
+__device__ __forceinline__ void rescue_one(const LaneArgs& a, int rp, int rs, int lane, uint2* __restrict__ mt)
 {
     const PairDesc pd = a.pairs[rp];
     const int R = __builtin_amdgcn_readfirstlane(pd.y), H = __builtin_amdgcn_readfirstlane(pd.w);
-    const LaneCtx cx{a.rows + __builtin_amdgcn_readfirstlane(pd.x), a.hapw + __builtin_amdgcn_readfirstlane(pd.z), R,
-                     H};
+    const int rx = __builtin_amdgcn_readfirstlane(pd.x);
+    const LaneCtx cx{a.rows - kRowPadBefore, unsigned(rx + kRowPadBefore) * 4u, a.hapw,
+                     unsigned(__builtin_amdgcn_readfirstlane(pd.z)) * 4u, R, H};
     const int nb = (H + 7) / 8;
     const SegSteps st{R, R, R + nb - 1};
-    const uint32_t w1 = cx.rrow[0];
+    const uint32_t w1 = row_word(cx, 0);
     const double T0 = row0_t<double>(a.lut64, w1, H);
     const bool eq = read_eq(w1);
     double sM = 0.0, sX = 0.0;
     run_seg_bc<double, 8>(a.lut64, a.lut64, st, lane, lane, cx, T0, sM, sX, mt, eq);
-    if (lane == nb - 1) a.raw64_zero[rp] = sM + sX;
+    if (lane == nb - 1) {
+        const double r = sM + sX;
+        if (a.rec) {   // record of slot rs: state and raw f64 (after the owner's store: same wave, program order)
+            const unsigned long long b = (unsigned long long)__double_as_longlong(r);
+            uint4* q = a.rec + rs;
+            q->y = kRecInWave;
+            *reinterpret_cast<uint2*>(&q->z) = make_uint2(unsigned(b), unsigned(b >> 32));
+        } else {
+            a.raw64_zero[rp] = r;
+        }
+    }
     __builtin_amdgcn_wave_barrier();   // the next pair rewrites mt
 }
 
 // Rescue pair rp in this wave if it qualifies and the run's in-wave budget
 // allows (wave-uniform), else append it to the rescue list (lane `owner_lane`).
-__device__ __forceinline__ void rescue_or_defer(const LaneArgs& a, bool few, int rp, int lane, int owner_lane,
-                                                uint2* __restrict__ mt)
+__device__ __forceinline__ void rescue_or_defer(const LaneArgs& a, bool few, int rp, int rs, int lane,
+                                                int owner_lane, uint2* __restrict__ mt)
 {
     bool here = few && __builtin_amdgcn_readfirstlane(a.pairs[rp].w) <= kInWaveRescueMaxH;
     if (here) {
@@ -403,19 +478,19 @@ __device__ __forceinline__ void rescue_or_defer(const LaneArgs& a, bool few, int
         here = __builtin_amdgcn_readfirstlane(c) < a.inker_limit;
     }
     if (here)
-        rescue_one(a, rp, lane, mt);
+        rescue_one(a, rp, rs, lane, mt);
     else if (lane == owner_lane)
         a.rescue_list[atomicAdd(a.rescue_count, 1)] = rp;
 }
 
-__device__ __forceinline__ void rescue_in_wave(const LaneArgs& a, uint64_t todo, int pid, int lane,
+__device__ __forceinline__ void rescue_in_wave(const LaneArgs& a, uint64_t todo, int pid, int slot, int lane,
                                                uint2* __restrict__ mt)
 {
     const bool few = a.inker_count != nullptr && __popcll(todo) <= 2;
     while (todo) {
         const int l = __builtin_ctzll(todo);
         todo &= todo - 1;
-        rescue_or_defer(a, few, __builtin_amdgcn_readlane(pid, l), lane, l, mt);
+        rescue_or_defer(a, few, __builtin_amdgcn_readlane(pid, l), __builtin_amdgcn_readlane(slot, l), lane, l, mt);
     }
 }
 

@@ -72,21 +72,38 @@ def main():
             per = kern.get(k, {}).get("launches_per_unit", 1)
             for c, v in cs.items():
                 kern.setdefault(k, {})[c] = round(sum(v) / len(v) * per, 3)
-    dom = opts.get("kernel", "phmm_seg_kernel")
-    dk = next((k for k in kern if dom in k), None)
-    s = dict(kernel_src_hash=kernel_src_hash(), cells=cells, dominant_kernel=dk, skip=skip,
-             unit="call" if calls else "launch",
+    # dominant_kernel: the engine kernel with the longest warm time per unit;
+    # fp32_kernel: the fp32 column-segmented pass (the bench roofline's kernel);
+    # fp64_kernel: the fp64 rescue pass, priced per rescued cell (--rescued-cells).
+    ours = {k: v for k, v in kern.items() if "phmm" in k or "rescue" in k or "kernel" in k}
+    timed = {k: v for k, v in ours.items() if "avg_ms_warm" in v}
+    dk = max(timed, key=lambda k: timed[k]["avg_ms_warm"]) if timed else None
+    f32 = opts.get("kernel", "phmm_seg_")
+    fk = next((k for k in timed if f32 in k and "seg64" not in k), None)
+    f64k = next((k for k in timed if "phmm_seg64_kernel" in k), None)
+    s = dict(kernel_src_hash=kernel_src_hash(), cells=cells, dominant_kernel=dk, fp32_kernel=fk, fp64_kernel=f64k,
+             skip=skip, unit="call" if calls else "launch",
              passes={n: d for n, d in passes}, kernels=kern)
-    if dk:
-        e = kern[dk]
+    if fk:
+        e = kern[fk]
         s["frac_from_warm_avg"] = round(12 * cells / (e["avg_ms_warm"] * 1e-3) / VALU_PEAK, 4)
         if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
             s["hbm_bytes_per_launch"] = int((2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024)
             s["hbm_bytes_per_cell"] = round(s["hbm_bytes_per_launch"] / cells, 5)
+            s["write_bytes_per_launch"] = int(e["WRITE_SIZE"] * 1024)
         if "SQ_INSTS_VALU" in e:
             s["valu_lane_instr_per_cell"] = round(e["SQ_INSTS_VALU"] * 64 / cells, 3)
         if "SQ_LDS_BANK_CONFLICT" in e:
             s["lds_bank_conflict_cycles_per_launch"] = int(e["SQ_LDS_BANK_CONFLICT"])
+    rc = int(opts.get("rescued-cells", "0"))
+    if f64k and rc > 0:
+        e = kern[f64k]
+        s["rescued_cells"] = rc
+        s["fp64_frac_from_warm_avg"] = round(12 * rc / (e["avg_ms_warm"] * 1e-3) / 39.3e12, 4)
+        if "SQ_INSTS_VALU" in e:
+            s["fp64_valu_lane_instr_per_rescued_cell"] = round(e["SQ_INSTS_VALU"] * 64 / rc, 3)
+        if "SQ_WAVE_CYCLES" in e and "SQ_BUSY_CYCLES" in e and e["SQ_BUSY_CYCLES"] > 0:
+            s["fp64_mean_resident_waves_per_busy_cycle"] = round(e["SQ_WAVE_CYCLES"] / e["SQ_BUSY_CYCLES"], 2)
     json.dump(s, open(out, "w"), indent=1)
     s["dominant"] = kern.get(dk)
     print(json.dumps({k: s[k] for k in s if k not in ("kernels", "passes")}))
