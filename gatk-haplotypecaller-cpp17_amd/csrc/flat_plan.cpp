@@ -470,6 +470,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     const size_t o_list = L.take(sizeof(int) * n1);
     const size_t o_rec = L.take(sizeof(uint4) * n1);   // seg slot records (every pair is a seg pair)
     const size_t o_slotof = L.take(sizeof(int) * n1);
+    const size_t o_sdesc = L.take(sizeof(PairDesc) * n1);
     const size_t o_count = L.take(kNumCounters * sizeof(int));
     const size_t o_sorted = L.take(sizeof(int) * n1);
     const size_t o_worder = L.take(sizeof(int) * n1);
@@ -553,6 +554,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     b->d_plan = reinterpret_cast<Seg64Plan*>(dev + o_plan);
     b->d_rec = reinterpret_cast<uint4*>(dev + o_rec);
     b->d_slot_of = reinterpret_cast<int*>(dev + o_slotof);
+    b->d_sdesc = reinterpret_cast<PairDesc*>(dev + o_sdesc);
     b->n_wide = nwide;
     if (slot) {
         b->host_res = host + host_res_off;
@@ -623,6 +625,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
         a.gtab = reinterpret_cast<int*>(dev + o_gtab);
         a.order = b->d_lane_order;
         a.slot_of = b->d_slot_of;
+        a.sdesc = b->d_sdesc;
         a.waves = b->d_lane_waves;
         a.waves_tmp = reinterpret_cast<LaneWave*>(dev + o_wtmp);
         a.tail = tail;

@@ -178,6 +178,7 @@ struct LaneArgs {
     // fp64 pass gathers the records into the per-pair outputs (Seg64Args).
     uint4* rec;
     int prio;   // 1: issue priority by remaining steps (seg_common.hpp set_prio_by_remaining)
+    const PairDesc* sdesc;   // seg slots' pair descriptors in slot order (pairs[order[slot]])
 };
 // Result record of one seg slot: {raw f32 bits, state, raw f64 low word, high
 // word}; state 0 = not rescued, 1 = rescued in the fp32 pass (raw f64 here),
@@ -244,6 +245,13 @@ struct PackArgs {
     const int4* hdesc;
     int nhaps;
     uint32_t* hapw;
+    // Host-planned parts: the seg slots' pair descriptors in slot order
+    // (sdesc[s] = pairs[order[s]], s < nslots), so a seg wave reads its pairs
+    // without the order indirection (one dependent load fewer per wave).
+    const int4* pairs;
+    const int* order;
+    int nslots;
+    int4* sdesc;
 };
 hipError_t launch_pack_batch(const PackArgs& a, hipStream_t s);
 // Pair descriptors of a structured (cross-product) plan, built on the device
@@ -280,6 +288,7 @@ struct GridPrepArgs {
     const int *rord, *hord;
     int* order;
     int* slot_of;    // pair -> its slot (inverse of order)
+    int4* sdesc;     // the slots' pair descriptors, slot order
     LaneWave* waves;
     int* counters;   // kNumCounters ints zeroed (run counters)
 };
@@ -319,6 +328,7 @@ struct FlatPlanArgs {
     int* gtab;             // per group: {first slot, pairs, first wave}
     int* order;            // slot -> pair
     int* slot_of;          // pair -> slot
+    int4* sdesc;           // slot -> pair descriptor
     LaneWave* waves;       // the plan's waves (packing order), then the dispatch order
     LaneWave* waves_tmp;   // max_waves entries: the packing order while the tail is reordered
     int max_waves;         // waves the launch covers (upper bound of the plan's)

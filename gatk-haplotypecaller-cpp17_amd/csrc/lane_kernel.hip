@@ -353,7 +353,7 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
     // Lane -> (group, block): group g's lanes start at the prefix sum of nb.
     int* gmap = reinterpret_cast<int*>(mt);   // 128 ints, used before the match table
     int nb_g = 0;
-    if (lane < wv.npairs) nb_g = (a.pairs[a.order[wv.slot0 + lane]].w + bc - 1) / bc;
+    if (lane < wv.npairs) nb_g = (a.sdesc[wv.slot0 + lane].w + bc - 1) / bc;
     int start = nb_g;   // inclusive scan of nb over lanes (Hillis-Steele through LDS)
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -376,8 +376,8 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
     int s = gmap[64 + lane];
     __builtin_amdgcn_wave_barrier();
     const int slot = wv.slot0 + (g >= 0 ? g : 0);
-    const int pid = a.order[slot];
-    const LaneCtx cx = pair_ctx(a.pairs, a.rows, a.hapw, pid);
+    const LaneCtx cx = desc_ctx(a.sdesc[slot], a.rows, a.hapw);   // slot-ordered: no order -> pairs indirection
+    const int pid = a.order[slot];   // needed only to write results by pair id
     const bool owner = g >= 0 && s == (cx.H + bc - 1) / bc - 1;
     if (g < 0) s = 0;
     const uint32_t w1 = row_word(cx, 0);
@@ -447,14 +447,18 @@ __device__ __forceinline__ int seg_fetch(int* head)
 template <int OCC>
 __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
 {
-    __shared__ float slut[kSlutLen];
-    // Device-planned parts launch an upper bound of waves: surplus workgroups
-    // leave before the LDS fill (workgroup-uniform).
+    // Each wave fills its own copy of the prior tables: no workgroup barrier
+    // between the kernel's start and a wave's first loads, so the fill
+    // overlaps the wave's descriptor loads (small batches are one round of
+    // waves: every wave's start-up latency is on the pass's critical path).
+    __shared__ float sluts[kSegWPB][kSlutLen];
     const int n_waves = a.n_waves_dev ? __builtin_amdgcn_readfirstlane(*a.n_waves_dev) : a.n_waves;
-    if (int(blockIdx.x) * kSegWPB >= n_waves) return;
-    load_slut(slut, a.lut);
     const int wid = blockIdx.x * kSegWPB + (threadIdx.x >> 6);
-    if (wid < n_waves) seg_wave(a, wid, slut);
+    if (wid >= n_waves) return;   // wave-uniform (device-planned parts launch an upper bound)
+    float* slut = sluts[threadIdx.x >> 6];
+    for (int t = threadIdx.x & 63; t < kSlutLen; t += 64) slut[t] = a.lut[t];
+    __builtin_amdgcn_wave_barrier();
+    seg_wave(a, wid, slut);
 }
 
 // The persistent form (a separate instance: its fetch loop around the width

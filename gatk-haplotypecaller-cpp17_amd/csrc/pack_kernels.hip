@@ -172,8 +172,9 @@ __device__ __forceinline__ void grid_pairs(const GridBlock* __restrict__ blocks,
 
 __device__ __forceinline__ void grid_waves(const GridSeg* __restrict__ segs, int nsegs, long long nslots, int nwaves,
                                            const int* __restrict__ rord, const int* __restrict__ hord,
-                                           const int4* __restrict__ rdesc, int* __restrict__ order,
-                                           int* __restrict__ slot_of, LaneWave* __restrict__ waves)
+                                           const int4* __restrict__ rdesc, const int4* __restrict__ hdesc,
+                                           int* __restrict__ order, int* __restrict__ slot_of,
+                                           int4* __restrict__ sdesc, LaneWave* __restrict__ waves)
 {
     const long long stride = 256ll * gridDim.x;
     for (long long t = blockIdx.x * 256ll + threadIdx.x; t < nslots; t += stride) {
@@ -186,9 +187,12 @@ __device__ __forceinline__ void grid_waves(const GridSeg* __restrict__ segs, int
         const GridSeg g = segs[lo];
         const long long i = t - g.slot0;
         const int rr = int(i / g.G), hh = int(i % g.G);
-        const int p = int(g.p0 + (long long)(rord[g.r0 + rr] - g.r0) * g.nh + (hord[g.g0 + hh] - g.h0));
+        const int r = rord[g.r0 + rr], h = hord[g.g0 + hh];
+        const int p = int(g.p0 + (long long)(r - g.r0) * g.nh + (h - g.h0));
         order[t] = p;
         slot_of[p] = int(t);
+        const int4 rd = rdesc[r], hd = hdesc[h];   // as grid_pairs
+        sdesc[t] = make_int4(rd.x, rd.y, hd.z, hd.y);
     }
     for (long long w = blockIdx.x * 256ll + threadIdx.x; w < nwaves; w += stride) {
         int lo = 0, hi = nsegs;   // the last segment with w0 <= w (segments without waves share w0)
@@ -219,14 +223,19 @@ __device__ __forceinline__ void grid_waves(const GridSeg* __restrict__ segs, int
 // (each step is a grid-stride loop over its own items; none reads another's
 // output): the run counters zeroed, reads packed, hap tables, pair
 // descriptors, slot order and waves — four fewer launches per region call.
-__global__ __launch_bounds__(256) void pack_batch_kernel(PackArgs a) { pack_items(a); }
+__global__ __launch_bounds__(256) void pack_batch_kernel(PackArgs a)
+{
+    pack_items(a);
+    for (int s = blockIdx.x * 256 + threadIdx.x; s < a.nslots; s += gridDim.x * 256) a.sdesc[s] = a.pairs[a.order[s]];
+}
 
 __global__ __launch_bounds__(256) void prepare_grid_kernel(GridPrepArgs a)
 {
     if (blockIdx.x == 0 && threadIdx.x < kNumCounters) a.counters[threadIdx.x] = 0;
     pack_items(a.pack);
     grid_pairs(a.blocks, a.nblocks, a.npairs, a.pack.rdesc, a.pack.hdesc, a.pairs);
-    grid_waves(a.segs, a.nsegs, a.nslots, a.nwaves, a.rord, a.hord, a.pack.rdesc, a.order, a.slot_of, a.waves);
+    grid_waves(a.segs, a.nsegs, a.nslots, a.nwaves, a.rord, a.hord, a.pack.rdesc, a.pack.hdesc, a.order, a.slot_of,
+               a.sdesc, a.waves);
 }
 
 // ---------------------------------------------------------------------------
@@ -376,6 +385,7 @@ __global__ __launch_bounds__(256) void flat_scatter_kernel(FlatPlanArgs a)
         const int pos = atomicAdd(&a.hist[a.bin_of[p]], 1);
         a.order[pos] = p;
         a.slot_of[p] = pos;
+        a.sdesc[pos] = a.pairs[p];
     }
 }
 

@@ -967,6 +967,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const size_t o_hapw = L.take(sizeof(uint32_t) * (size_t(hap_w[size_t(nh)]) + 16));
     const size_t o_res = L.take(res_bytes);
     const size_t o_rec = L.take(sizeof(uint4) * std::max<size_t>(size_t(n_seg_slots), 1));   // seg slot records
+    const size_t o_sdesc = L.take(sizeof(PairDesc) * std::max<size_t>(size_t(n_seg_slots), 1));   // slot -> descriptor
     const size_t o_list = L.take(sizeof(int) * n1);
     const size_t o_count = L.take(kNumCounters * sizeof(int));   // run counters (kernels.hpp kNumCounters)
     const size_t o_sorted = L.take(sizeof(int) * n1);
@@ -1057,6 +1058,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     b->d_plan = reinterpret_cast<Seg64Plan*>(dev + o_plan);
     b->d_rec = n_seg_slots > 0 ? reinterpret_cast<uint4*>(dev + o_rec) : nullptr;
     b->d_slot_of = reinterpret_cast<int*>(dev + o_slotof);
+    b->d_sdesc = reinterpret_cast<PairDesc*>(dev + o_sdesc);
     b->n_wide = wide_a.load();
     b->wide_ring_blocks = wide_ring_blocks;
     b->d_carry = carry_rows ? reinterpret_cast<float2*>(dev + o_carry) : nullptr;
@@ -1091,6 +1093,10 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     pack.hdesc = reinterpret_cast<const int4*>(dev + o_hd);
     pack.nhaps = int(nh);
     pack.hapw = b->d_hapw;
+    pack.pairs = b->d_pairs;
+    pack.order = d_ord;
+    pack.nslots = dev_pairs ? 0 : n_seg_slots;   // structured plans: grid_waves writes them
+    pack.sdesc = b->d_sdesc;
     auto enqueue = [&]() -> int {
         if (!b->slot_ev)
             for (auto& e : b->pack_ev) HIP_TRY(hipEventCreate(&e));
@@ -1116,6 +1122,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             g.hord = reinterpret_cast<const int*>(dev + o_gh);
             g.order = reinterpret_cast<int*>(dev + o_ord);
             g.slot_of = b->d_slot_of;
+            g.sdesc = b->d_sdesc;
             g.waves = reinterpret_cast<LaneWave*>(dev + o_lw);
             g.counters = b->d_count;
             HIP_TRY(launch_prepare_grid(g, s));

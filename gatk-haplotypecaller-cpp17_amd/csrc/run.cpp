@@ -118,6 +118,7 @@ int run_part(Part* b, hipStream_t s)
             g.waves = b->d_lane_waves;
             g.n_waves = b->n_seg_waves;
             g.n_waves_dev = b->d_nwaves;
+            g.sdesc = b->d_sdesc;
             // Persistent waves fetching from per-XCD queues
             // (HC_PHMM_SEG_PERSIST=1) or one queue (=2); default 0: one wave
             // per launched slot, the hardware dispatching them in order (the
@@ -133,8 +134,14 @@ int run_part(Part* b, hipStream_t s)
                 HIP_TRY(hipEventRecord(b->fork, s));
                 HIP_TRY(hipStreamWaitEvent(b->side, b->fork, 0));
             }
-            g.rec = b->d_rec;
-            r.rec = b->d_rec;   // the fp64 launch gathers the seg slots' records
+            // Per-slot records (gathered by the fp64 launch) pay off in HBM
+            // writes on large parts; on small ones the gather's two dependent
+            // loads sit on the pass's critical path, and the scattered stores
+            // they replace are a few MB: parts below HC_PHMM_REC_MIN_PAIRS
+            // write their results in place.
+            const bool rec = b->d_rec && b->n >= env_i64("HC_PHMM_REC_MIN_PAIRS", 200000);
+            g.rec = rec ? b->d_rec : nullptr;
+            r.rec = g.rec;   // the fp64 launch gathers the seg slots' records
             r.slot_of = b->d_slot_of;
             HIP_TRY(launch_lane_seg_f32(g, max_blocks, persist == 2 ? 1 : 8, fork ? b->side : s));
             if (fork) HIP_TRY(hipEventRecord(b->join, b->side));

@@ -162,11 +162,14 @@ __device__ __forceinline__ T row0_t(const T* __restrict__ lut, uint32_t w1, int 
     return (T(0) * mm1 + T(0) * g1) + initY * g1;
 }
 
+__device__ __forceinline__ LaneCtx desc_ctx(const PairDesc pd, const uint32_t* rows, const uint32_t* hapw)
+{
+    return LaneCtx{rows - kRowPadBefore, unsigned(pd.x + kRowPadBefore) * 4u, hapw, unsigned(pd.z) * 4u, pd.y, pd.w};
+}
 __device__ __forceinline__ LaneCtx pair_ctx(const PairDesc* pairs, const uint32_t* rows, const uint32_t* hapw,
                                             int pid)
 {
-    const PairDesc pd = pairs[pid];
-    return LaneCtx{rows - kRowPadBefore, unsigned(pd.x + kRowPadBefore) * 4u, hapw, unsigned(pd.z) * 4u, pd.y, pd.w};
+    return desc_ctx(pairs[pid], rows, hapw);
 }
 
 // Constant-gap tag of a read: bit 31 of its first row word (pack_reads_kernel).
@@ -440,7 +443,7 @@ __device__ __forceinline__ void run_seg_bc(const T* __restrict__ lut, const T* _
 // lanes of 8 columns), raw f64 sum to raw64_zero[rp].
 __device__ __forceinline__ void rescue_one(const LaneArgs& a, int rp, int rs, int lane, uint2* __restrict__ mt)
 {
-    const PairDesc pd = a.pairs[rp];
+    const PairDesc pd = a.sdesc[rs];   // = pairs[rp]
     const int R = __builtin_amdgcn_readfirstlane(pd.y), H = __builtin_amdgcn_readfirstlane(pd.w);
     const int rx = __builtin_amdgcn_readfirstlane(pd.x);
     const LaneCtx cx{a.rows - kRowPadBefore, unsigned(rx + kRowPadBefore) * 4u, a.hapw,
@@ -471,7 +474,7 @@ __device__ __forceinline__ void rescue_one(const LaneArgs& a, int rp, int rs, in
 __device__ __forceinline__ void rescue_or_defer(const LaneArgs& a, bool few, int rp, int rs, int lane,
                                                 int owner_lane, uint2* __restrict__ mt)
 {
-    bool here = few && __builtin_amdgcn_readfirstlane(a.pairs[rp].w) <= kInWaveRescueMaxH;
+    bool here = few && __builtin_amdgcn_readfirstlane(a.sdesc[rs].w) <= kInWaveRescueMaxH;
     if (here) {
         int c = 0;
         if (lane == 0) c = atomicAdd(a.inker_count, 1);
@@ -487,6 +490,9 @@ __device__ __forceinline__ void rescue_in_wave(const LaneArgs& a, uint64_t todo,
                                                uint2* __restrict__ mt)
 {
     const bool few = a.inker_count != nullptr && __popcll(todo) <= 2;
+    // The owners' result records are complete before a rescue rewrites part
+    // of one (the same address from another lane of this wave).
+    if (a.rec) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     while (todo) {
         const int l = __builtin_ctzll(todo);
         todo &= todo - 1;

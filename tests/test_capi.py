@@ -144,3 +144,18 @@ def test_init_rejects_unknown_flags(built):
     assert L.hc_phmm_init(2, 0) == hcphmm.EINVAL
     assert b"flags" in L.hc_phmm_last_error()
     assert L.hc_phmm_init_devices(0x80, None, 0) == hcphmm.EINVAL
+
+
+def test_stale_binary_is_refused(built, monkeypatch):
+    """A library whose compiled-in source hashes differ from the tree's is
+    refused (bench.py, smoke() and the GPU tests call check_build_id), and the
+    content check that ensure_built uses to decide on a rebuild sees it."""
+    real = hcphmm.tree_hashes()
+    monkeypatch.setattr(hcphmm, "tree_hashes", lambda: {"kernel": "0" * 16, "lib": real["lib"]})
+    with pytest.raises(hcphmm.PairHMMError) as e:
+        hcphmm.check_build_id()
+    assert "stale" in str(e.value)
+    assert hcphmm._stale_by_content()
+    monkeypatch.setattr(hcphmm, "tree_hashes", lambda: real)
+    assert not hcphmm._stale_by_content()
+    assert hcphmm.check_build_id()["kernel"] == real["kernel"]

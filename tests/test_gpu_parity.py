@@ -426,3 +426,71 @@ def test_use_double_every_golden_pair(engine, golden, golden_batch):
     # and the default mode is back: the fp32 pass decides again
     res = engine.pairs(golden_batch)
     assert np.array_equal(res["rescued"], golden["rescued"])
+
+
+@pytest.mark.parametrize("variant", ["persist-xcd", "persist-one", "prio32", "prio64-off", "records"])
+def test_schedule_variants_are_bit_identical(engine, golden, golden_batch, variant, monkeypatch):
+    """How waves are scheduled never changes a result: the persistent fp32
+    pass (per-XCD queues / one queue, HC_PHMM_SEG_PERSIST=1/2)
+    and the issue-priority switches give the default's bits on a 125k-pair S2
+    shard (more waves than wave slots, so the persistent kernel really fetches)
+    run twice (the counters it zeroes for the next run), and on the golden set."""
+    env = {"persist-xcd": ("HC_PHMM_SEG_PERSIST", "1"), "persist-one": ("HC_PHMM_SEG_PERSIST", "2"),
+           "prio32": ("HC_PHMM_PRIO", "1"), "prio64-off": ("HC_PHMM_PRIO64", "0"),
+           "records": ("HC_PHMM_REC_MIN_PAIRS", "0")}[variant]
+    b = W.config("S2", 125_000)
+    ref = engine.pairs(b)
+    bt_ref = engine.Batch(b)
+    bt_ref.run()
+    rb = bt_ref.results()
+    bt_ref.close()
+    monkeypatch.setenv(*env)
+    bt = engine.Batch(b)
+    for _ in range(2):   # the second run checks the counters the first one left
+        bt.run()
+        got = bt.results()
+        for k in ("raw_f32", "raw_f64", "rescued", "loglik"):
+            assert np.array_equal(bits(got[k]), bits(rb[k])), f"{variant}: {k}"
+    bt.close()
+    assert_same(engine.pairs(b), ref, f"{variant} flat")
+    res = engine.pairs(golden_batch)
+    assert_same(res, dict(raw_f32=golden["raw_f32"], rescued=golden["rescued"],
+                          raw_f64=golden["raw_f64_all"], loglik=golden["loglik"]), f"{variant} golden")
+
+
+@pytest.mark.parametrize("mode", ["auto", "lane"])
+def test_seg_records_and_gather_with_mixed_kernels(engine, oracle_lib, monkeypatch, mode):
+    """The fp32 seg waves write per-slot records that the fp64 launch gathers
+    into the per-pair outputs (slot_of); pairs of the one-lane and anti-
+    diagonal kernels write theirs in place (slot_of = -1). A batch of haps up
+    to 6 000 bases (some rescued) split between the seg waves and the anti-
+    diagonal kernel (auto: haps past 64 x 64 columns) or the one-lane kernel
+    (lane: past the seg reach), against the oracle, with outputs bound to
+    caller buffers and run twice."""
+    import torch
+    if mode == "lane":
+        monkeypatch.setenv("HC_PHMM_KERNEL", "lane")
+        monkeypatch.setenv("HC_PHMM_LANE_SEG", "auto")
+    monkeypatch.setenv("HC_PHMM_REC_MIN_PAIRS", "0")   # records at any size (default: large parts only)
+    b = W.generate(600, (100, 6000), (60, 250), 0.03, seed=91)
+    ref = oracle_lib.pairs(b, nthreads=16)
+    bt = engine.Batch(b)
+    n = len(b["R"])
+    out32 = torch.full((n,), float("nan"), dtype=torch.float32, device="cuda")
+    out64 = torch.full((n,), float("nan"), dtype=torch.float64, device="cuda")
+    outfl = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    bt.bind_outputs(out32.data_ptr(), out64.data_ptr(), outfl.data_ptr())
+    for _ in range(2):
+        bt.run()
+        torch.cuda.synchronize()
+        got = dict(raw_f32=out32.cpu().numpy(), raw_f64=out64.cpu().numpy(), rescued=outfl.cpu().numpy())
+        r32 = got["raw_f32"].view(np.uint32) != ref["raw_f32"].view(np.uint32)
+        assert not r32.any(), f"{r32.sum()} raw_f32 mismatches"
+        assert np.array_equal(got["rescued"], ref["rescued"])
+        m = ref["rescued"].astype(bool)
+        assert np.array_equal(bits(got["raw_f64"][m]), bits(ref["raw_f64"][m]))
+        assert (got["raw_f64"][~m] == 0).all()
+    st = bt.stats()
+    assert 0 < st.n_seg_waves   # seg waves ran ...
+    assert st.n_lane_pairs < st.n_pairs if mode == "auto" else st.n_launch_waves > st.n_seg_waves   # ... and another kernel
+    bt.close()
