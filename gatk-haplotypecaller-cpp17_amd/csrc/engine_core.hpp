@@ -250,7 +250,6 @@ struct Part {
     float* own_raw32 = nullptr;   // outputs in the part's allocation: [raw32 | raw64 | flag]
     double* own_raw64 = nullptr;
     uint8_t* own_flag = nullptr;
-    double* d_spec64 = nullptr;   // speculative fp64 results (small batches, run.cpp)
     size_t res_bytes = 0;         // bytes of that contiguous output block
     size_t res_o64 = 0, res_ofl = 0;
     uint4* d_rec = nullptr;       // seg slot result records (LaneArgs::rec), gathered by the fp64 launch
@@ -267,7 +266,6 @@ struct Part {
     int* d_count = nullptr;
     int inker_limit = 0;   // in-wave rescues allowed in the last run
     int parity = 0;
-    bool speculate = false;       // fp64 over every pair beside the fp32 pass (run.cpp)
     char* dev_base = nullptr;
     Slot* slot = nullptr;         // borrowed workspace (jobs), else dev_base is owned
     char* host_res = nullptr;     // pinned results image (slot) after the D2H
@@ -275,6 +273,7 @@ struct Part {
     hipEvent_t pack_ev[2] = {nullptr, nullptr};
     hipEvent_t done = nullptr;    // jobs: D2H complete
     std::vector<std::array<hipEvent_t, 3>> ev_pool;
+    std::vector<uint8_t> ev_solo;   // per pooled run: no fp64 launch, ev[2] not recorded (ev[1] ends the run)
     size_t ev_used = 0;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     bool slot_ev = false;         // pack_ev / ev / done are the slot's (not destroyed here)

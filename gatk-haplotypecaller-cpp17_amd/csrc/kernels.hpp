@@ -179,6 +179,13 @@ struct LaneArgs {
     uint4* rec;
     int prio;   // 1: issue priority by remaining steps (seg_common.hpp set_prio_by_remaining)
     const PairDesc* sdesc;   // seg slots' pair descriptors in slot order (pairs[order[slot]])
+    // No fp64 launch after this pass (run.cpp: small parts of seg waves only,
+    // every hap within kInWaveRescueMaxH): each flagged pair is rescued in its
+    // own wave, however many the wave has, and workgroup 0 zeroes the other
+    // run parity's counters, which the fp64 launch zeroes otherwise. null = an
+    // fp64 launch follows.
+    int* solo_counters;   // the part's counter block
+    int solo_other;       // the other run parity
 };
 // Result record of one seg slot: {raw f32 bits, state, raw f64 low word, high
 // word}; state 0 = not rescued, 1 = rescued in the fp32 pass (raw f64 here),

@@ -344,12 +344,15 @@ __device__ void plan_rescue(const Seg64Args& a, int n, PlanLds& L)
 // One column-segmented wave (wid) of the fp32 pass.
 __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float* __restrict__ slut)
 {
-    const int lane = threadIdx.x & 63;
+    // Lane id and the wave's LDS tables in forms the compiler can recompute
+    // (mbcnt) or keep in SGPRs (wave-uniform): values live across the step
+    // loop that it would otherwise spill at every wave's start.
+    const int lane = __lane_id();
     const unsigned long long t_start = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
     const LaneWave wv = load_wave(a.waves, wid);
     const int bc = wv.ncols;
     __shared__ uint2 mtab[kSegWPB][5 * 64];
-    uint2* mt = mtab[threadIdx.x >> 6];
+    uint2* mt = mtab[__builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6))];
     // Lane -> (group, block): group g's lanes start at the prefix sum of nb.
     int* gmap = reinterpret_cast<int*>(mt);   // 128 ints, used before the match table
     int nb_g = 0;
@@ -453,10 +456,21 @@ __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
     // waves: every wave's start-up latency is on the pass's critical path).
     __shared__ float sluts[kSegWPB][kSlutLen];
     const int n_waves = a.n_waves_dev ? __builtin_amdgcn_readfirstlane(*a.n_waves_dev) : a.n_waves;
-    const int wid = blockIdx.x * kSegWPB + (threadIdx.x >> 6);
+    const int wib = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+    const int wid = blockIdx.x * kSegWPB + wib;
+    if (a.solo_counters && blockIdx.x == 0 && threadIdx.x == 0) {
+        // No fp64 launch follows: the other parity's counters for the next run
+        // (its last run's kernels are complete: stream order).
+        int* c = a.solo_counters;
+        const int o = a.solo_other;
+        c[o] = 0;                 // rescue list length
+        c[2 + o] = 0;             // in-wave rescues
+        c[kPlanTicket + o] = 0;
+        c[kPlanReady + o] = 0;
+    }
     if (wid >= n_waves) return;   // wave-uniform (device-planned parts launch an upper bound)
-    float* slut = sluts[threadIdx.x >> 6];
-    for (int t = threadIdx.x & 63; t < kSlutLen; t += 64) slut[t] = a.lut[t];
+    float* slut = sluts[wib];
+    for (int t = __lane_id(); t < kSlutLen; t += 64) slut[t] = a.lut[t];
     __builtin_amdgcn_wave_barrier();
     seg_wave(a, wid, slut);
 }

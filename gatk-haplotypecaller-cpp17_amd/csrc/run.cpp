@@ -4,6 +4,7 @@
 // pass recomputes the flagged pairs; then the host log10 finish.
 #include <algorithm>
 #include <cmath>
+#include <limits>
 
 #include "engine_core.hpp"
 #include "luts.hpp"
@@ -64,6 +65,7 @@ int run_part(Part* b, hipStream_t s)
     // initNative(use_double = true): no fp32 pass, every pair to the fp64 one
     // (intel_pairhmm.hpp:71,81,135-140).
     const bool all_f64 = (g_flags.load(std::memory_order_relaxed) & HC_PHMM_FLAG_F64) != 0;
+    bool solo = false;   // no fp64 launch after the fp32 pass (below)
     if (all_f64) HIP_TRY(launch_all_f64_list(int(b->n), b->d_raw32, b->d_flag, b->d_list, count, s));
     if (b->n_lane > 0 && !all_f64) {
         LaneArgs a{};
@@ -143,6 +145,20 @@ int run_part(Part* b, hipStream_t s)
             g.rec = rec ? b->d_rec : nullptr;
             r.rec = g.rec;   // the fp64 launch gathers the seg slots' records
             r.slot_of = b->d_slot_of;
+            // Small parts of seg waves only, every hap within one wave's fp64
+            // reach: each wave rescues all its flagged pairs itself and no fp64
+            // launch follows (S1: that launch was ~6 us of a 73 us pass, for an
+            // empty list). Larger parts keep the list: a region whose reads miss
+            // many haps would serialise hundreds of rescues in its waves.
+            solo = !rec && persist == 0 && n_one == 0 && b->n_wide == 0 && b->cls[0].n == 0 && b->cls[1].n == 0 &&
+                   a.inker_count != nullptr && b->Hmax <= kInWaveRescueMaxH &&
+                   b->n <= env_i64("HC_PHMM_SOLO_MAX_PAIRS", 32768);
+            if (solo) {
+                g.solo_counters = b->d_count;
+                g.solo_other = par ^ 1;
+                g.inker_limit = std::numeric_limits<int>::max();
+                b->inker_limit = g.inker_limit;
+            }
             HIP_TRY(launch_lane_seg_f32(g, max_blocks, persist == 2 ? 1 : 8, fork ? b->side : s));
             if (fork) HIP_TRY(hipEventRecord(b->join, b->side));
         }
@@ -175,7 +191,7 @@ int run_part(Part* b, hipStream_t s)
         HIP_TRY(launch_diag_f32(c.W, a, grid, s));
     }
     HIP_TRY(hipEventRecord(b->ev[1], s));
-    if (b->n > 0) {
+    if (b->n > 0 && !solo) {
         // fp64 rescue (intel_pairhmm.hpp:137-139) over the device-built list, no
         // host round trip for its length: device planning + column-segmented
         // fp64 waves (grid-stride), then the anti-diagonal fp64 kernel for haps
@@ -199,7 +215,12 @@ int run_part(Part* b, hipStream_t s)
             HIP_TRY(launch_diag_f64(64, a, int(std::max<int64_t>(1, std::min<int64_t>(b->n_wide, cap))), s));
         }
     }
-    HIP_TRY(hipEventRecord(b->ev[2], s));
+    // A solo run's end is ev[1]: recording ev[2] right behind it would only add
+    // the marker's own stream time (~5 us measured on S1, as much as the fp64
+    // launch it replaces).
+    if (!solo) HIP_TRY(hipEventRecord(b->ev[2], s));
+    if (b->ev_solo.size() < b->ev_pool.size()) b->ev_solo.resize(b->ev_pool.size());
+    b->ev_solo[b->ev_used - 1] = solo;
     b->ran = true;
     return HC_PHMM_OK;
 }

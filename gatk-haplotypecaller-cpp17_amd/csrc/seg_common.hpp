@@ -157,7 +157,12 @@ template <typename T>
 __device__ __forceinline__ T row0_t(const T* __restrict__ lut, uint32_t w1, int H)
 {
     const T mm1 = lut[kOffMM + mm_idx(row_i(w1), row_d(w1))];
-    const T g1 = lut[kOffGapm + row_c(w1)];
+    // Opaque offset: otherwise the address lut + 4 * row_c is shared with row
+    // 1's ph2pr[row_c] load in the step loop's set-up, and that 64-bit address,
+    // live across the wave's whole prologue, is spilled to scratch.
+    unsigned go = unsigned(kOffGapm + row_c(w1)) * unsigned(sizeof(T));
+    asm volatile("" : "+v"(go));
+    const T g1 = *reinterpret_cast<const T*>(reinterpret_cast<const char*>(lut) + go);
     const T initY = initial_value<T>() / T(H);
     return (T(0) * mm1 + T(0) * g1) + initY * g1;
 }
@@ -489,7 +494,8 @@ __device__ __forceinline__ void rescue_or_defer(const LaneArgs& a, bool few, int
 __device__ __forceinline__ void rescue_in_wave(const LaneArgs& a, uint64_t todo, int pid, int slot, int lane,
                                                uint2* __restrict__ mt)
 {
-    const bool few = a.inker_count != nullptr && __popcll(todo) <= 2;
+    // (No fp64 launch after this pass: every one, the list would go unread.)
+    const bool few = a.inker_count != nullptr && (a.solo_counters != nullptr || __popcll(todo) <= 2);
     // The owners' result records are complete before a rescue rewrites part
     // of one (the same address from another lane of this wave).
     if (a.rec) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -458,6 +458,31 @@ def test_schedule_variants_are_bit_identical(engine, golden, golden_batch, varia
                           raw_f64=golden["raw_f64_all"], loglik=golden["loglik"]), f"{variant} golden")
 
 
+@pytest.mark.parametrize("solo", ["on", "off"])
+def test_small_part_rescues_in_its_waves(engine, oracle_lib, monkeypatch, solo):
+    """A small part of seg waves whose haps all fit one wave's fp64 reach
+    (H <= 512) launches no fp64 pass: each wave rescues every pair it flagged
+    (run.cpp `solo`, HC_PHMM_SOLO_MAX_PAIRS). A rescue-heavy batch (most pairs,
+    many per wave) against the oracle, flat and through one prepared batch run
+    three times (the seg kernel zeroes the other run parity's counters in
+    place of the fp64 launch); off: the same batch through the list."""
+    if solo == "off":
+        monkeypatch.setenv("HC_PHMM_SOLO_MAX_PAIRS", "0")
+    b = W.generate(3000, (100, 500), (60, 200), 0.08, seed=23)
+    ref = oracle_lib.pairs(b, nthreads=16)
+    n_resc = int(ref["rescued"].sum())
+    assert n_resc > 1000
+    assert_same(engine.pairs(b), ref, f"solo {solo} flat")
+    bt = engine.Batch(b)
+    for k in range(3):
+        bt.run()
+        got = bt.results()
+        assert_same(got, ref, f"solo {solo} run {k}")
+        assert (got["raw_f64"][~ref["rescued"].astype(bool)] == 0).all()
+    assert bt.stats().n_rescued == n_resc
+    bt.close()
+
+
 @pytest.mark.parametrize("mode", ["auto", "lane"])
 def test_seg_records_and_gather_with_mixed_kernels(engine, oracle_lib, monkeypatch, mode):
     """The fp32 seg waves write per-slot records that the fp64 launch gathers
