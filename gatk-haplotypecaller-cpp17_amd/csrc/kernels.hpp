@@ -203,10 +203,10 @@ const LaneVariant& lane_variant(int id);
 hipError_t launch_lane_f32(int variant, const LaneArgs& a, hipStream_t s);
 // Column-segmented waves only (lane_kernel.hip run_seg): a pair of hap length H
 // takes ceil(H / BC) lanes; BC per wave, one of the compiled block widths.
-// max_blocks > 0: at most that many workgroups (4 waves each), persistent
-// waves fetching the rest (a.seg_counters must be set).
+// max_waves > 0: at most that many resident waves, persistent waves fetching
+// the rest (a.seg_counters must be set).
 // queues: 8 = per-XCD queues + tail queue, 1 = one queue (persistent only).
-hipError_t launch_lane_seg_f32(const LaneArgs& a, int max_blocks, int queues, hipStream_t s);
+hipError_t launch_lane_seg_f32(const LaneArgs& a, int max_waves, int queues, hipStream_t s);
 bool seg_width_ok(int bc);
 int seg_width_ceil(int bc);   // narrowest compiled width >= bc (-1: none)
 constexpr int kSegMaxBC = 64;

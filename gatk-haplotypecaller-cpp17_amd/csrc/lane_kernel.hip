@@ -180,9 +180,16 @@ __global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
 // Column-segmented fp32 waves (host-planned). The wave's npairs pairs are the
 // slots slot0 .. slot0+npairs-1; pair g takes nb_g = ceil(H_g / BC) consecutive
 // lanes in slot order. Lanes past the last group idle (s = 0, no output).
-// Seg waves per workgroup: 1, 2 and 4 time the same (profiles/
-// r02_seg_waves_per_workgroup_ab.txt); 4 shares the LDS prior table.
-constexpr int kSegWPB = 4;
+// Seg waves per workgroup (HC_SEG_WPB, A/B builds: EXTRA_DEV_FLAGS=-DHC_SEG_WPB=n).
+// A workgroup is dispatched when a CU has room for all its waves, so with 4
+// the slot a finished wave frees can wait for its workgroup's others (a 125k
+// pass spent 18 % of its SIMD time at 2 resident waves). One wave per
+// workgroup (each wave has its own LDS tables): S2 8.64 -> 8.59 ms, S1 and
+// the shard sizes unchanged (profiles/r04_wpb_ab.txt).
+#ifndef HC_SEG_WPB
+#define HC_SEG_WPB 1
+#endif
+constexpr int kSegWPB = HC_SEG_WPB;
 // ---------------------------------------------------------------------------
 // fp64 rescue pass (intel_pairhmm.hpp:137-139) in column-segmented form.
 //
@@ -716,10 +723,11 @@ int seg_width_ceil(int bc)
     return -1;
 }
 
-hipError_t launch_lane_seg_f32(const LaneArgs& a, int max_blocks, int queues, hipStream_t s)
+hipError_t launch_lane_seg_f32(const LaneArgs& a, int max_waves, int queues, hipStream_t s)
 {
     if (a.n_waves <= 0) return hipSuccess;
     const int grid = (a.n_waves + kSegWPB - 1) / kSegWPB;
+    const int max_blocks = max_waves / kSegWPB;
     // Persistent only when the waves outnumber the launch's slots (device-
     // planned parts: their upper bound does; the kernel re-reads the count).
     if (max_blocks > 0 && a.seg_counters && grid > max_blocks) {

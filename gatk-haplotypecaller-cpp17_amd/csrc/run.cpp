@@ -125,12 +125,12 @@ int run_part(Part* b, hipStream_t s)
             // (HC_PHMM_SEG_PERSIST=1) or one queue (=2); default 0: one wave
             // per launched slot, the hardware dispatching them in order (the
             // persistent forms measured no faster).
-            int max_blocks = 0;
+            int max_waves = 0;
             const int persist = int(env_i64("HC_PHMM_SEG_PERSIST", 0));
             if (persist != 0) {
                 g.seg_counters = b->d_count;
                 g.n_tail = b->seg_tail;
-                max_blocks = int(std::max<int64_t>(1, env_i64("HC_PHMM_SEG_BLOCKS_PER_CU", 3))) * dv.n_cu;
+                max_waves = int(std::max<int64_t>(1, env_i64("HC_PHMM_SEG_WAVES_PER_SIMD", 3))) * 4 * dv.n_cu;
             }
             if (fork) {
                 HIP_TRY(hipEventRecord(b->fork, s));
@@ -159,7 +159,7 @@ int run_part(Part* b, hipStream_t s)
                 g.inker_limit = std::numeric_limits<int>::max();
                 b->inker_limit = g.inker_limit;
             }
-            HIP_TRY(launch_lane_seg_f32(g, max_blocks, persist == 2 ? 1 : 8, fork ? b->side : s));
+            HIP_TRY(launch_lane_seg_f32(g, max_waves, persist == 2 ? 1 : 8, fork ? b->side : s));
             if (fork) HIP_TRY(hipEventRecord(b->join, b->side));
         }
         if (n_one > 0) {
