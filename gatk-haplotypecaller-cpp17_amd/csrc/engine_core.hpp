@@ -255,6 +255,7 @@ struct Part {
     uint4* d_rec = nullptr;       // seg slot result records (LaneArgs::rec), gathered by the fp64 launch
     int* d_slot_of = nullptr;     // pair -> seg slot (-1: one-lane / anti-diagonal pair)
     PairDesc* d_sdesc = nullptr;  // seg slot -> pair descriptor (pairs[order[slot]])
+    int* d_steal = nullptr;       // stealable rescue list (LaneArgs::steal_list; host-planned parts)
     int* d_list = nullptr;
     int* d_sorted = nullptr;
     int* d_worder = nullptr;      // fp64 pass: dispatch position -> wave

@@ -42,13 +42,16 @@ constexpr long long kMaxRowWords = (1ll << 30) - 1024;
 // Run counters of a part (zeroed when the part is prepared): [0, 1] rescue
 // list lengths and [2, 3] in-wave rescue counts, by run parity (a run zeroes
 // the other parity's for the next run: no memset per run); [4] the fp64
-// pass's wave counter (zeroed by its plan each run); from kSegHeads the
+// pass's wave counter (zeroed by its plan each run); [5..10] the fp64
+// planner's ticket and flag and the stealable list's length, by parity
+// likewise; from kSegHeads the
 // persistent fp32 pass's queue heads (8 XCD queues + the tail queue, one
 // 64-byte line each) and its finished-wave count, which the last wave to
 // finish zeroes again for the next run (lane_kernel.hip phmm_seg_kernel).
 constexpr int kNextWave = 4;
 constexpr int kPlanTicket = 5;   // [5, 6] fp64 planner ticket, [7, 8] plan-published flag, by run parity
 constexpr int kPlanReady = 7;
+constexpr int kStealCount = 9;    // [9, 10] stealable rescue list length, by parity
 constexpr int kSegHeads = 16;
 constexpr int kSegQueues = 9;          // 8 XCD queues + the tail queue
 constexpr int kSegHeadStride = 16;     // ints: one 64-byte line per head
@@ -99,7 +102,8 @@ struct Seg64Args {
     const uint32_t* rows;
     const uint32_t* hapw;
     const double* lut;
-    const int* list;          // rescue list (fp32 pass, arbitrary order)
+    int* list;                // rescue list (fp32 pass, arbitrary order); the planner appends the
+                              // stealable list's untaken entries to it
     const int* count;         // its length
     int* count_reset;         // the other run parity's counter, zeroed for the next run
     int* inker_reset;         // the other run parity's in-wave rescue counter, likewise
@@ -125,6 +129,13 @@ struct Seg64Args {
     float* raw32;
     uint8_t* flag;
     int prio;   // as LaneArgs::prio
+    // The fp32 pass's stealable rescues (LaneArgs::steal_list): entries of
+    // [0, steal_count) still holding a pair id + 1 were not taken by a seg
+    // wave and are planned here with the list's; every entry is zeroed again
+    // for the next run.
+    int* steal_list;          // null: no stealable list this run
+    const int* steal_count;
+    int* steal_count_reset;   // the other run parity's, zeroed for the next run
 };
 // Lane-per-pair kernel (large batches): one lane owns one pair and sweeps it
 // row by row over register-resident blocks of kLaneBlock columns. A wave holds
@@ -186,6 +197,15 @@ struct LaneArgs {
     // fp64 launch follows.
     int* solo_counters;   // the part's counter block
     int solo_other;       // the other run parity
+    // Stealable rescues (seg waves, with an fp64 launch after the pass): a
+    // flagged pair of H <= kInWaveRescueMaxH its wave does not rescue goes to
+    // steal_list as pid + 1 (entries zero before the run); a seg wave done with
+    // its own pairs takes entries (seg_common.hpp steal_rescues) and rescues
+    // them in fp64 itself, so rescues listed while the pass drains run beside
+    // it instead of after it. The fp64 launch plans the entries left untaken.
+    // null = off (every deferred rescue to rescue_list).
+    int* steal_list;
+    int* steal_count;
 };
 // Result record of one seg slot: {raw f32 bits, state, raw f64 low word, high
 // word}; state 0 = not rescued, 1 = rescued in the fp32 pass (raw f64 here),
@@ -259,6 +279,8 @@ struct PackArgs {
     const int* order;
     int nslots;
     int4* sdesc;
+    int* steal;   // the part's stealable rescue list, zeroed here (n_steal entries)
+    int n_steal;
 };
 hipError_t launch_pack_batch(const PackArgs& a, hipStream_t s);
 // Pair descriptors of a structured (cross-product) plan, built on the device

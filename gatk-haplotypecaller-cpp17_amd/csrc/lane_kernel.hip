@@ -420,7 +420,7 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
         }
     }
     const uint64_t todo = __builtin_amdgcn_ballot_w64(resc);
-    if (todo) rescue_in_wave(a, todo, pid, slot, lane, mt);
+    if (todo) rescue_in_wave(a, todo, pid, slot, cx.H, lane, mt);
     if (a.timeline && lane == 0) {
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
         a.timeline[3 * size_t(wid)] = t_start;
@@ -429,6 +429,7 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
         a.timeline[3 * size_t(wid) + 2] = (unsigned long long)unsigned(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))) |
                                           ((unsigned long long)unsigned(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11))) << 32);
     }
+    if (a.steal_list) steal_rescues(a, wid, lane, mt);
 }
 
 
@@ -474,6 +475,7 @@ __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
         c[2 + o] = 0;             // in-wave rescues
         c[kPlanTicket + o] = 0;
         c[kPlanReady + o] = 0;
+        c[kStealCount + o] = 0;
     }
     if (wid >= n_waves) return;   // wave-uniform (device-planned parts launch an upper bound)
     float* slut = sluts[wib];
@@ -554,18 +556,35 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
     // none, and otherwise the first workgroup to arrive plans while the others
     // gather the seg records, then wait for its flag (they never wait on a
     // workgroup that is not running: the planner is the first one running).
-    const int n = __builtin_amdgcn_readfirstlane(*a.count);
+    const int n_list = __builtin_amdgcn_readfirstlane(*a.count);
+    // Stealable rescues no seg wave took join the list: the planner keeps the
+    // entries [0, s_count) still holding a pair id + 1. Until it has, n is an
+    // upper bound (an all-taken list plans zero waves).
+    const int s_count = a.steal_list ? __builtin_amdgcn_readfirstlane(*a.steal_count) : 0;
+    int n = n_list + s_count;
     if (blockIdx.x == 0 && t == 0) {   // the other run parity's counters, zeroed for the next run
         *a.count_reset = 0;
         *a.inker_reset = 0;
         *a.ticket_reset = 0;
         *a.ready_reset = 0;
+        *a.steal_count_reset = 0;
         if (n == 0) *a.big_count = 0;   // the wide fp64 kernel's list (the plan writes it otherwise)
     }
     if (t == 0) role = n > 0 ? atomicAdd(a.ticket, 1) : 1;
     __syncthreads();
     const bool planner = role == 0;
     if (planner) {
+        if (s_count > 0) {
+            if (t == 0) plan_lds.lanes = 0;
+            __syncthreads();
+            for (int i = t; i < s_count; i += 256) {   // untaken into the list; every entry zeroed for the next run
+                const int v = a.steal_list[i];
+                a.steal_list[i] = 0;
+                if (v > 0) a.list[n_list + int(atomicAdd(&plan_lds.lanes, 1ull))] = v - 1;
+            }
+            __syncthreads();
+            n = n_list + int(plan_lds.lanes);
+        }
         plan_rescue(a, n, plan_lds);
         // Publish (MI355X_MICROARCH.md, inter-workgroup visibility): every
         // storing wave drains its stores, then one lane releases and flags.

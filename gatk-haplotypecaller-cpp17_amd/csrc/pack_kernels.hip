@@ -90,6 +90,8 @@ __device__ __forceinline__ uint4 rows_rec4(uint32_t q4, uint32_t c4, uint32_t i4
 // several HBM requests in flight instead of one dependent chain per read.
 __device__ __forceinline__ void pack_items(const PackArgs& a)
 {
+    // The stealable rescue list starts each part zeroed (its runs zero what they use).
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < a.n_steal; k += gridDim.x * blockDim.x) a.steal[k] = 0;
     const int lane = threadIdx.x & 63;
     const int n = max(a.nreads, a.nhaps);
     const int stride = gridDim.x * 4;

@@ -969,6 +969,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const size_t o_rec = L.take(sizeof(uint4) * std::max<size_t>(size_t(n_seg_slots), 1));   // seg slot records
     const size_t o_sdesc = L.take(sizeof(PairDesc) * std::max<size_t>(size_t(n_seg_slots), 1));   // slot -> descriptor
     const size_t o_list = L.take(sizeof(int) * n1);
+    const size_t o_steal = L.take(sizeof(int) * std::max<size_t>(size_t(n_seg_slots), 1));   // stealable rescues (seg pairs)
     const size_t o_count = L.take(kNumCounters * sizeof(int));   // run counters (kernels.hpp kNumCounters)
     const size_t o_sorted = L.take(sizeof(int) * n1);
     const size_t o_worder = L.take(sizeof(int) * n1);
@@ -1059,6 +1060,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     b->d_rec = n_seg_slots > 0 ? reinterpret_cast<uint4*>(dev + o_rec) : nullptr;
     b->d_slot_of = reinterpret_cast<int*>(dev + o_slotof);
     b->d_sdesc = reinterpret_cast<PairDesc*>(dev + o_sdesc);
+    b->d_steal = n_seg_slots > 0 ? reinterpret_cast<int*>(dev + o_steal) : nullptr;
     b->n_wide = wide_a.load();
     b->wide_ring_blocks = wide_ring_blocks;
     b->d_carry = carry_rows ? reinterpret_cast<float2*>(dev + o_carry) : nullptr;
@@ -1097,6 +1099,8 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     pack.order = d_ord;
     pack.nslots = dev_pairs ? 0 : n_seg_slots;   // structured plans: grid_waves writes them
     pack.sdesc = b->d_sdesc;
+    pack.steal = b->d_steal;   // zeroed by the prep launch
+    pack.n_steal = b->d_steal ? int(n_seg_slots) : 0;
     auto enqueue = [&]() -> int {
         if (!b->slot_ev)
             for (auto& e : b->pack_ev) HIP_TRY(hipEventCreate(&e));

@@ -44,6 +44,7 @@ int run_part(Part* b, hipStream_t s)
     r.ticket_reset = b->d_count + kPlanTicket + (par ^ 1);
     r.ready = b->d_count + kPlanReady + par;
     r.ready_reset = b->d_count + kPlanReady + (par ^ 1);
+    r.steal_count_reset = b->d_count + kStealCount + (par ^ 1);
     r.sorted = b->d_sorted;
     r.big = b->d_big;
     r.big_count = b->d_big_count;
@@ -158,6 +159,16 @@ int run_part(Part* b, hipStream_t s)
                 g.solo_other = par ^ 1;
                 g.inker_limit = std::numeric_limits<int>::max();
                 b->inker_limit = g.inker_limit;
+            } else if (b->d_steal && a.inker_count != nullptr && env_i64("HC_PHMM_STEAL", 0) != 0) {
+                // Rescues a wave defers are taken by seg waves done with their
+                // own pairs before the fp64 launch plans the rest. Opt-in: the
+                // 415 x 128 region call measured 1.07 -> 1.18 ms with it (a
+                // stolen fp64 rescue holds a slot the pass's next fp32 wave
+                // needs, and the rescues of the last waves still leave the
+                // fp64 launch its one-rescue latency).
+                g.steal_list = r.steal_list = b->d_steal;
+                g.steal_count = b->d_count + kStealCount + par;
+                r.steal_count = g.steal_count;
             }
             HIP_TRY(launch_lane_seg_f32(g, max_waves, persist == 2 ? 1 : 8, fork ? b->side : s));
             if (fork) HIP_TRY(hipEventRecord(b->join, b->side));

@@ -446,9 +446,12 @@ __device__ __forceinline__ void run_seg_bc(const T* __restrict__ lut, const T* _
 // others are appended to the rescue list for that pass.
 // fp64 recompute of pair rp by the whole wave (H <= kInWaveRescueMaxH: 64
 // lanes of 8 columns), raw f64 sum to raw64_zero[rp].
-__device__ __forceinline__ void rescue_one(const LaneArgs& a, int rp, int rs, int lane, uint2* __restrict__ mt)
+// rs < 0 (a stolen rescue, another wave's pair): the raw f64 goes to
+// raw64_zero[rp] even with records (its record says kRecListed, which the
+// gather leaves to the rescue's own store).
+__device__ __forceinline__ void rescue_one(const LaneArgs& a, const PairDesc pd, int rp, int rs, int lane,
+                                           uint2* __restrict__ mt)
 {
-    const PairDesc pd = a.sdesc[rs];   // = pairs[rp]
     const int R = __builtin_amdgcn_readfirstlane(pd.y), H = __builtin_amdgcn_readfirstlane(pd.w);
     const int rx = __builtin_amdgcn_readfirstlane(pd.x);
     const LaneCtx cx{a.rows - kRowPadBefore, unsigned(rx + kRowPadBefore) * 4u, a.hapw,
@@ -462,7 +465,7 @@ __device__ __forceinline__ void rescue_one(const LaneArgs& a, int rp, int rs, in
     run_seg_bc<double, 8>(a.lut64, a.lut64, st, lane, lane, cx, T0, sM, sX, mt, eq);
     if (lane == nb - 1) {
         const double r = sM + sX;
-        if (a.rec) {   // record of slot rs: state and raw f64 (after the owner's store: same wave, program order)
+        if (a.rec && rs >= 0) {   // record of slot rs: state and raw f64 (after the owner's store: same wave, program order)
             const unsigned long long b = (unsigned long long)__double_as_longlong(r);
             uint4* q = a.rec + rs;
             q->y = kRecInWave;
@@ -474,24 +477,32 @@ __device__ __forceinline__ void rescue_one(const LaneArgs& a, int rp, int rs, in
     __builtin_amdgcn_wave_barrier();   // the next pair rewrites mt
 }
 
-// Rescue pair rp in this wave if it qualifies and the run's in-wave budget
-// allows (wave-uniform), else append it to the rescue list (lane `owner_lane`).
-__device__ __forceinline__ void rescue_or_defer(const LaneArgs& a, bool few, int rp, int rs, int lane,
+// Rescue pair rp (slot rs, hap length H) in this wave if it qualifies and the
+// run's in-wave budget allows (wave-uniform), else append it to a list (lane
+// `owner_lane`): the stealable list if a wave can take it (H within reach),
+// else the fp64 launch's.
+__device__ __forceinline__ void rescue_or_defer(const LaneArgs& a, bool few, int rp, int rs, int H, int lane,
                                                 int owner_lane, uint2* __restrict__ mt)
 {
-    bool here = few && __builtin_amdgcn_readfirstlane(a.sdesc[rs].w) <= kInWaveRescueMaxH;
+    const bool fits = H <= kInWaveRescueMaxH;
+    bool here = few && fits;
     if (here) {
         int c = 0;
         if (lane == 0) c = atomicAdd(a.inker_count, 1);
         here = __builtin_amdgcn_readfirstlane(c) < a.inker_limit;
     }
-    if (here)
-        rescue_one(a, rp, rs, lane, mt);
-    else if (lane == owner_lane)
-        a.rescue_list[atomicAdd(a.rescue_count, 1)] = rp;
+    if (here) {
+        rescue_one(a, a.sdesc[rs], rp, rs, lane, mt);   // sdesc[rs] = pairs[rp]
+    } else if (lane == owner_lane) {
+        if (a.steal_list && fits)
+            __hip_atomic_store(a.steal_list + atomicAdd(a.steal_count, 1), rp + 1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        else
+            a.rescue_list[atomicAdd(a.rescue_count, 1)] = rp;
+    }
 }
 
-__device__ __forceinline__ void rescue_in_wave(const LaneArgs& a, uint64_t todo, int pid, int slot, int lane,
+__device__ __forceinline__ void rescue_in_wave(const LaneArgs& a, uint64_t todo, int pid, int slot, int H, int lane,
                                                uint2* __restrict__ mt)
 {
     // (No fp64 launch after this pass: every one, the list would go unread.)
@@ -502,7 +513,40 @@ __device__ __forceinline__ void rescue_in_wave(const LaneArgs& a, uint64_t todo,
     while (todo) {
         const int l = __builtin_ctzll(todo);
         todo &= todo - 1;
-        rescue_or_defer(a, few, __builtin_amdgcn_readlane(pid, l), __builtin_amdgcn_readlane(slot, l), lane, l, mt);
+        rescue_or_defer(a, few, __builtin_amdgcn_readlane(pid, l), __builtin_amdgcn_readlane(slot, l),
+                        __builtin_amdgcn_readlane(H, l), lane, l, mt);
+    }
+}
+
+// A seg wave done with its own pairs rescues deferred pairs of other waves
+// (LaneArgs::steal_list). Lane 0 probes up to kStealProbes entries from a
+// per-wave pseudo-random start, swapping in kStealTaken: a pair id + 1 back
+// means the pair is this wave's to rescue; kStealTaken, another wave's; 0, a
+// slot reserved but not yet stored, whose writer's store then stands and the
+// fp64 launch plans it. No shared head, so waves finishing together do not
+// serialise on one atomic (a CAS-on-head first form made a 415 x 128 region
+// call 1.1 -> 9 ms).
+constexpr int kStealTaken = -1;
+constexpr int kStealProbes = 4;
+__device__ __forceinline__ void steal_rescues(const LaneArgs& a, int wid, int lane, uint2* __restrict__ mt)
+{
+    unsigned seed = unsigned(wid) * 2654435761u + 12345u;
+    for (;;) {
+        int v = 0;
+        if (lane == 0) {
+            const int c = __hip_atomic_load(a.steal_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (c > 0) {
+                int i = int(seed % unsigned(c));
+                for (int p = 0; p < kStealProbes && v <= 0; ++p) {
+                    v = __hip_atomic_exchange(a.steal_list + i, kStealTaken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (++i == c) i = 0;
+                }
+            }
+        }
+        v = __builtin_amdgcn_readfirstlane(v);
+        if (v <= 0) return;
+        rescue_one(a, a.pairs[v - 1], v - 1, -1, lane, mt);   // (uniform: rescue_one reads it with readfirstlane)
+        seed = seed * 1664525u + 1013904223u;
     }
 }
 

@@ -483,6 +483,34 @@ def test_small_part_rescues_in_its_waves(engine, oracle_lib, monkeypatch, solo):
     bt.close()
 
 
+@pytest.mark.parametrize("mode", ["steal", "steal-records", "no-steal"])
+def test_stolen_rescues(engine, oracle_lib, monkeypatch, mode):
+    """Rescues a seg wave defers (past the in-wave limits) with H <= 512 go to
+    the stealable list; seg waves done with their own pairs take entries and
+    rescue them in fp64, the fp64 launch plans the untaken ones with the
+    list's (haps past 512). A batch above the solo size with most pairs
+    rescued (H 100-900), three runs through one prepared batch (the list is
+    zeroed for the next run, its counters by run parity), against the oracle;
+    with per-slot records (a stolen rescue writes its pair's raw f64 itself)
+    and with stealing off."""
+    monkeypatch.setenv("HC_PHMM_STEAL", "0" if mode == "no-steal" else "1")
+    if mode == "steal-records":
+        monkeypatch.setenv("HC_PHMM_REC_MIN_PAIRS", "0")
+    b = W.generate(40000, (100, 900), (60, 200), 0.08, seed=29)
+    ref = oracle_lib.pairs(b, nthreads=16)
+    n_resc = int(ref["rescued"].sum())
+    assert n_resc > 15000
+    bt = engine.Batch(b)
+    for k in range(3):
+        bt.run()
+        got = bt.results()
+        assert_same(got, ref, f"{mode} run {k}")
+        assert (got["raw_f64"][~ref["rescued"].astype(bool)] == 0).all()
+    assert bt.stats().n_rescued == n_resc
+    bt.close()
+    assert_same(engine.pairs(b), ref, f"{mode} flat")
+
+
 @pytest.mark.parametrize("mode", ["auto", "lane"])
 def test_seg_records_and_gather_with_mixed_kernels(engine, oracle_lib, monkeypatch, mode):
     """The fp32 seg waves write per-slot records that the fp64 launch gathers
