@@ -268,16 +268,18 @@ FP64_PEAK_TOPS = 39.3   # AMD MI355X FP64 vector 78.6 TFLOPS (FMA = 2) -> 39.3 T
 
 
 def resident_pass(hcphmm, W, name, npairs, prof, batch=None):
-    """One BASELINE config as a device-resident batch: 5 timed device passes
-    (HIP events). S4 also prices its fp64 rescue pass (intel_pairhmm.hpp:
+    """One BASELINE config as a device-resident batch: 10 timed device passes
+    (HIP events) after 5 untimed ones (a new batch's first passes touch fresh
+    pages: a 125k-pair shard measured 1.32 ms over 5 passes after 2, 1.22 ms
+    warm). S4 also prices its fp64 rescue pass (intel_pairhmm.hpp:
     137-139): 12 f64 ops per rescued cell / fp64 pass time vs the fp64 peak.
     `batch`: a given batch (a shard) instead of the config's."""
     b = W.config(name, npairs) if batch is None else batch
     bb = hcphmm.Batch(b)
-    for _ in range(2):
+    for _ in range(5):
         bb.run()
     bb.stats()
-    for _ in range(5):
+    for _ in range(10):
         bb.run()
     s2 = bb.stats()
     cells = W.cells(b)
