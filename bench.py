@@ -269,15 +269,21 @@ FP64_PEAK_TOPS = 39.3   # AMD MI355X FP64 vector 78.6 TFLOPS (FMA = 2) -> 39.3 T
 
 def resident_pass(hcphmm, W, name, npairs, prof, batch=None):
     """One BASELINE config as a device-resident batch: 10 timed device passes
-    (HIP events) after 5 untimed ones (a new batch's first passes touch fresh
-    pages: a 125k-pair shard measured 1.32 ms over 5 passes after 2, 1.22 ms
-    warm). S4 also prices its fp64 rescue pass (intel_pairhmm.hpp:
-    137-139): 12 f64 ops per rescued cell / fp64 pass time vs the fp64 peak.
-    `batch`: a given batch (a shard) instead of the config's."""
+    (HIP events, back to back) after at least 5 untimed ones and 0.2 s of
+    them: the GPU's clocks rise over the first tens of ms of work after an idle
+    spell (rank 0's 125k-pair shard: 1.29 ms on the first pass of a sequence,
+    1.18 ms on the tenth, tools/shard_state_probe.py), and the bench's other
+    steps leave it idle between configs. S4 also prices its fp64 rescue pass
+    (intel_pairhmm.hpp:137-139): 12 f64 ops per rescued cell / fp64 pass time
+    vs the fp64 peak. `batch`: a given batch (a shard) instead of the config's."""
     b = W.config(name, npairs) if batch is None else batch
     bb = hcphmm.Batch(b)
-    for _ in range(5):
+    t0, k = time.perf_counter(), 0
+    while k < 5 or time.perf_counter() - t0 < 0.2:
         bb.run()
+        k += 1
+        if k % 4 == 0:
+            bb.stats()   # (synchronises: bounds the queued passes)
     bb.stats()
     for _ in range(10):
         bb.run()
