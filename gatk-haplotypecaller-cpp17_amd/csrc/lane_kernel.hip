@@ -237,8 +237,12 @@ struct PlanLds {
     unsigned cost[kMaxSortWaves];
 };
 
-// Cost of wave w (class order) of the plan in L.
-__device__ __forceinline__ unsigned wave_cost(const Seg64Args& a, const PlanLds& L, int w)
+// Entries [e0, e1) of `sorted` and the class shape of wave w (class order)
+// of the plan in L.
+struct WaveSpan {
+    int e0, e1, kk, bc;
+};
+__device__ __forceinline__ WaveSpan wave_span(const PlanLds& L, int w)
 {
     constexpr int NC = kSeg64Classes;
     int lo = 0, hi = NC - 1;   // the last class whose first wave is <= w
@@ -249,13 +253,62 @@ __device__ __forceinline__ unsigned wave_cost(const Seg64Args& a, const PlanLds&
     }
     const int c = lo;
     const int kk = 6 - c / kSeg64Widths, per = 64 >> kk;
-    const int bc = seg64_width(kSeg64Widths - 1 - c % kSeg64Widths);
     const int off = L.fill[c] - L.cnt[c];   // the class's first entry (fill ran past it)
     const int e0 = off + (w - L.wbase[c]) * per;
-    const int e1 = min(off + L.cnt[c], e0 + per);
-    int rmax = 0;
-    for (int e = e0; e < e1; ++e) rmax = max(rmax, a.pairs[a.sorted[e]].y);
-    return unsigned(rmax + (1 << kk) - 1) * unsigned(bc * 14 + 40);
+    return WaveSpan{e0, min(off + L.cnt[c], e0 + per), kk, seg64_width(kSeg64Widths - 1 - c % kSeg64Widths)};
+}
+
+// The planner is one workgroup walking the list, so its time is load
+// latency: each thread takes kPlanBatch entries at a time and issues their
+// independent loads together (the list entries, then their pairs' H) instead
+// of one dependent pair per step (S4's 1 861 rescues: one round of loads).
+constexpr int kPlanBatch = 8;
+template <typename F>
+__device__ __forceinline__ void plan_walk(const Seg64Args& a, int n, F&& f)
+{
+    for (int b = threadIdx.x; b < n; b += kPlanBatch * kPlanThreads) {
+        int pid[kPlanBatch], h[kPlanBatch];
+#pragma unroll
+        for (int k = 0; k < kPlanBatch; ++k) {
+            const int i = b + k * kPlanThreads;
+            pid[k] = i < n ? a.list[i] : -1;
+        }
+#pragma unroll
+        for (int k = 0; k < kPlanBatch; ++k) h[k] = pid[k] >= 0 ? a.pairs[pid[k]].w : 0;
+#pragma unroll
+        for (int k = 0; k < kPlanBatch; ++k)
+            if (pid[k] >= 0) f(pid[k], h[k]);
+    }
+}
+
+// Modelled costs of waves [0, W) into L.cost (and their maximum into L.cmax):
+// (rows + skew) steps x (14 ops per column + ~40 per step); batched like
+// plan_walk (the first pair of kPlanBatch waves at once, then the rest).
+__device__ __forceinline__ void wave_costs(const Seg64Args& a, PlanLds& L, int W)
+{
+    for (int b = threadIdx.x; b < W; b += kPlanBatch * kPlanThreads) {
+        WaveSpan sp[kPlanBatch];
+        int s0[kPlanBatch], r[kPlanBatch];
+#pragma unroll
+        for (int k = 0; k < kPlanBatch; ++k) {
+            const int w = b + k * kPlanThreads;
+            sp[k] = w < W ? wave_span(L, w) : WaveSpan{0, 0, 0, 0};
+            s0[k] = sp[k].e0 < sp[k].e1 ? a.sorted[sp[k].e0] : -1;
+        }
+#pragma unroll
+        for (int k = 0; k < kPlanBatch; ++k) r[k] = s0[k] >= 0 ? a.pairs[s0[k]].y : 0;
+#pragma unroll
+        for (int k = 0; k < kPlanBatch; ++k) {
+#pragma unroll 4
+            for (int e = sp[k].e0 + 1; e < sp[k].e1; ++e) r[k] = max(r[k], a.pairs[a.sorted[e]].y);
+            const int w = b + k * kPlanThreads;
+            if (w < W) {
+                const unsigned c = unsigned(r[k] + (1 << sp[k].kk) - 1) * unsigned(sp[k].bc * 14 + 40);
+                L.cost[w] = c;
+                atomicMax(&L.cmax, c);
+            }
+        }
+    }
 }
 
 // The fp64 pass's plan over the n > 0 listed pairs, by one workgroup of the
@@ -275,12 +328,12 @@ __device__ void plan_rescue(const Seg64Args& a, int n, PlanLds& L)
     }
     __syncthreads();
     unsigned long long mine = 0;
-    for (int i = t; i < n; i += kPlanThreads) mine += (a.pairs[a.list[i]].w + 31) / 32;
+    plan_walk(a, n, [&](int, int H) { mine += (H + 31) / 32; });
     if (mine) atomicAdd(&L.lanes, mine);
     __syncthreads();
     const long long l32 = (long long)L.lanes;
     const int bc0 = l32 >= a.min_lanes ? 32 : (2 * l32 >= a.min_lanes ? 16 : 8);
-    for (int i = t; i < n; i += kPlanThreads) atomicAdd(&L.cnt[rescue_class(a.pairs[a.list[i]].w, bc0)], 1);
+    plan_walk(a, n, [&](int, int H) { atomicAdd(&L.cnt[rescue_class(H, bc0)], 1); });
     __syncthreads();
     if (t == 0) {
         Seg64Plan* __restrict__ p = a.plan;   // written in place (a local copy would live in registers)
@@ -302,15 +355,14 @@ __device__ void plan_rescue(const Seg64Args& a, int n, PlanLds& L)
         *a.big_count = L.cnt[NC - 1];
     }
     __syncthreads();
-    for (int i = t; i < n; i += kPlanThreads) {
-        const int pid = a.list[i];
-        const int c = rescue_class(a.pairs[pid].w, bc0);
+    plan_walk(a, n, [&](int pid, int H) {
+        const int c = rescue_class(H, bc0);
         const int pos = atomicAdd(&L.fill[c], 1);
         if (c < NC - 1)
             a.sorted[pos] = pid;
         else
             a.big[pos - (n - L.cnt[NC - 1])] = pid;
-    }
+    });
     __syncthreads();
     const int W = L.wbase[NC - 1];   // segmented waves
     if (W <= 1 || !a.wave_order) return;
@@ -319,11 +371,7 @@ __device__ void plan_rescue(const Seg64Args& a, int n, PlanLds& L)
         return;
     }
     // Costs, then a counting sort by cost descending over 256 buckets.
-    for (int w = t; w < W; w += kPlanThreads) {
-        const unsigned c = wave_cost(a, L, w);
-        L.cost[w] = c;
-        atomicMax(&L.cmax, c);
-    }
+    wave_costs(a, L, W);
     L.hist[t] = 0;
     __syncthreads();
     const unsigned cmax = L.cmax;

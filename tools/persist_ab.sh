@@ -8,7 +8,7 @@ mkdir -p gpurun_out/pab
 WL=${WL:-S2}
 run() {  # tag n env...
   local tag=$1 n=$2; shift 2
-  env "$@" timeout -k 10 120 python3 bench.py --workload $WL --pairs $n --steps 20 --warmup 5 --no-cpu --no-extra \
+  env "$@" timeout -k 10 120 python3 bench.py --workload $WL --pairs $n --steps ${STEPS:-20} --warmup ${WARM:-5} --no-cpu --no-extra \
       > gpurun_out/pab/b_${WL}_${n}_${tag}.json 2> gpurun_out/pab/b_${WL}_${n}_${tag}.err || return 1
   python3 -c "import json; d=json.load(open('gpurun_out/pab/b_${WL}_${n}_${tag}.json')); print('$WL', '$tag', $n, d['roofline']['kernel_ms'], d['kernel_ms_f64'], d['device_pass_ms'], d['roofline']['frac'])"
 }
