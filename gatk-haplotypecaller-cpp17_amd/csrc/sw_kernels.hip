@@ -657,18 +657,22 @@ __global__ __launch_bounds__(64 * WPG) void sw_dp_kernel(SwDpArgs a)
             L.acc = 0;
             uint32_t* btw = bt + int64_t(s) * nw * kStripe;
             const bool lastw = s == nstripes - 1 && (n1 % kStripe) != 0;
+            // A partial last stripe of r rows is done after n2 + r - 1 steps
+            // (lane r - 1 leaves column n2), not n2 + 63: its unwritten
+            // backtrack words lie past every cell the trace reads.
+            const int Ts = lastw ? std::min(T, (n2 + (n1 - s * kStripe) + kGroup - 1) & ~(kGroup - 1)) : T;
             if (use_prof) {
                 const int code = row_ok ? int(codeOf[s1[i - 1]]) : 0;
                 sr.prow = prof + code * PS + 64 - lane;
                 if (lastw)
-                    pstripe<true, true>(L, lane, n2, row_ok, T, btw, open_v, extend_v, rowH, rowF, sr);
+                    pstripe<true, true>(L, lane, n2, row_ok, Ts, btw, open_v, extend_v, rowH, rowF, sr);
                 else
                     pstripe<false, true>(L, lane, n2, row_ok, T, btw, open_v, extend_v, rowH, rowF, sr);
             } else {
                 sr.rb = row_ok ? int(s1[i - 1]) : -1;   // never equals a byte
                 sr.arow = altB + 64 - lane;
                 if (lastw)
-                    pstripe<true, false>(L, lane, n2, row_ok, T, btw, open_v, extend_v, rowH, rowF, sr);
+                    pstripe<true, false>(L, lane, n2, row_ok, Ts, btw, open_v, extend_v, rowH, rowF, sr);
                 else
                     pstripe<false, false>(L, lane, n2, row_ok, T, btw, open_v, extend_v, rowH, rowF, sr);
             }
