@@ -121,8 +121,9 @@ extern std::mutex g_mu;
 extern std::vector<Device*> g_devs;
 extern int64_t g_live_parts;
 extern int64_t g_active_calls;
-// hc_phmm_init flags of the most recent successful init (HC_PHMM_FLAG_*),
-// read by every run: HC_PHMM_FLAG_F64 = initNative(use_double = true).
+// hc_phmm_init flags of the most recent successful init (HC_PHMM_FLAG_*): the
+// default mode of later calls and batches (HC_PHMM_FLAG_F64 = initNative(
+// use_double = true)), captured into each PartSpec when the call is made.
 extern std::atomic<uint32_t> g_flags;
 
 int init_devices_locked(const int32_t* devices, int32_t n, bool any_ok);
@@ -209,11 +210,33 @@ struct PartSpec {
     bool flat = true;
     int64_t lo = 0, hi = 0;
     std::vector<Block> blocks;
+    // hc_phmm_init flags of the call (HC_PHMM_FLAG_F64 = initNative's
+    // use_double), fixed when the call is made: the reference's g_use_double
+    // is per IntelPairHMM instance (intel_pairhmm.hpp:58,81), so a later init
+    // from another thread must not switch the mode of work already submitted.
+    uint32_t flags = 0;
 };
 
 // Planning modes: a real part (device calls), or a dry run that plans on the
 // host only and keeps the plan for the host-logic tests (hcx_* hooks).
 enum class PlanMode { Real, Dry };
+
+// A part's results block, one contiguous device range returned to the host by
+// one store (enqueue_results): [raw32 | raw64 | flag | run counters]. The run
+// counters (kNumCounters ints, kernels.hpp) ride along so the host sees the
+// device error word (kErrWord) with the results, at no extra transfer.
+struct ResLayout {
+    size_t o64, ofl, ocnt, bytes;
+};
+inline ResLayout res_layout(size_t n1)
+{
+    ResLayout r;
+    r.o64 = (sizeof(float) * n1 + 255) & ~size_t(255);
+    r.ofl = r.o64 + ((sizeof(double) * n1 + 255) & ~size_t(255));
+    r.ocnt = (r.ofl + n1 + 255) & ~size_t(255);
+    r.bytes = (r.ocnt + kNumCounters * sizeof(int) + 15) & ~size_t(15);   // whole 16-byte stores (launch_store_to_host)
+    return r;
+}
 
 // ---------------------------------------------------------------------------
 // A part prepared on one device: every device array lives in one allocation,
@@ -250,8 +273,8 @@ struct Part {
     float* own_raw32 = nullptr;   // outputs in the part's allocation: [raw32 | raw64 | flag]
     double* own_raw64 = nullptr;
     uint8_t* own_flag = nullptr;
-    size_t res_bytes = 0;         // bytes of that contiguous output block
-    size_t res_o64 = 0, res_ofl = 0;
+    size_t res_bytes = 0;         // bytes of that contiguous output block (ResLayout)
+    size_t res_o64 = 0, res_ofl = 0, res_ocnt = 0;
     uint4* d_rec = nullptr;       // seg slot result records (LaneArgs::rec), gathered by the fp64 launch
     int* d_slot_of = nullptr;     // pair -> seg slot (-1: one-lane / anti-diagonal pair)
     PairDesc* d_sdesc = nullptr;  // seg slot -> pair descriptor (pairs[order[slot]])
@@ -338,6 +361,7 @@ void finish_part(const Part& P, const float* f, const double* d, const uint8_t* 
 // has it; flat_plan.cpp).
 void pack_nibbles(const uint8_t* s, int n, uint8_t* d);
 int enqueue_results(Part* b, hipStream_t s);
+int check_device_error(const int* counters);   // run.cpp: counters = a host copy of a part's run counters
 
 // The last dry-run plan (hcx_dump_sizes / hcx_dump_plan).
 struct DryDump {

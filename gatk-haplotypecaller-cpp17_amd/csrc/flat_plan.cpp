@@ -434,9 +434,8 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     // Device layout: the upload image, descriptors and tables, then what the
     // device builds, the outputs and the rescue scratch.
     const size_t n1 = size_t(n);
-    const size_t res_o64 = (sizeof(float) * n1 + 255) & ~size_t(255);
-    const size_t res_ofl = res_o64 + ((sizeof(double) * n1 + 255) & ~size_t(255));
-    const size_t res_bytes = (res_ofl + n1 + 15) & ~size_t(15);   // whole 16-byte stores (launch_store_to_host)
+    const ResLayout RL = res_layout(n1);
+    const size_t res_bytes = RL.bytes;
     struct Lay {
         size_t off = 0;
         size_t take(size_t b)
@@ -453,6 +452,8 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     const size_t row_pad = kRowPadBefore + size_t(rmax) + 256;
     if (int64_t(rows) + int64_t(row_pad) > kMaxRowWords)
         return fail(HC_PHMM_EINVAL, "batch too large (read bases of one part exceed 2^30)");
+    if (int64_t(hapw) + 16 > kMaxHapWords)
+        return fail(HC_PHMM_EINVAL, "batch too large (hap match tables of one part exceed 2^30 words)");
     const size_t o_rows = L.take(sizeof(uint32_t) * (size_t(rows) + row_pad));
     const size_t o_hapw = L.take(sizeof(uint32_t) * (size_t(hapw) + 16));
     const size_t o_pairs = L.take(sizeof(PairDesc) * n1);
@@ -471,7 +472,6 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     const size_t o_rec = L.take(sizeof(uint4) * n1);   // seg slot records (every pair is a seg pair)
     const size_t o_slotof = L.take(sizeof(int) * n1);
     const size_t o_sdesc = L.take(sizeof(PairDesc) * n1);
-    const size_t o_count = L.take(kNumCounters * sizeof(int));
     const size_t o_sorted = L.take(sizeof(int) * n1);
     const size_t o_worder = L.take(sizeof(int) * n1);
     const size_t o_big = L.take(sizeof(int) * n1);
@@ -540,13 +540,14 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     b->d_lane_order = reinterpret_cast<int*>(dev + o_order);
     b->d_lane_waves = reinterpret_cast<LaneWave*>(dev + o_waves);
     b->res_bytes = res_bytes;
-    b->res_o64 = res_o64;
-    b->res_ofl = res_ofl;
+    b->res_o64 = RL.o64;
+    b->res_ofl = RL.ofl;
+    b->res_ocnt = RL.ocnt;
     b->own_raw32 = b->d_raw32 = reinterpret_cast<float*>(dev + o_res);
-    b->own_raw64 = b->d_raw64 = reinterpret_cast<double*>(dev + o_res + res_o64);
-    b->own_flag = b->d_flag = reinterpret_cast<uint8_t*>(dev + o_res + res_ofl);
+    b->own_raw64 = b->d_raw64 = reinterpret_cast<double*>(dev + o_res + RL.o64);
+    b->own_flag = b->d_flag = reinterpret_cast<uint8_t*>(dev + o_res + RL.ofl);
     b->d_list = reinterpret_cast<int*>(dev + o_list);
-    b->d_count = reinterpret_cast<int*>(dev + o_count);
+    b->d_count = reinterpret_cast<int*>(dev + o_res + RL.ocnt);   // run counters: the results block's tail
     b->d_sorted = reinterpret_cast<int*>(dev + o_sorted);
     b->d_worder = reinterpret_cast<int*>(dev + o_worder);
     b->d_big = reinterpret_cast<int*>(dev + o_big);

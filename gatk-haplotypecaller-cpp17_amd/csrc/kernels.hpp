@@ -38,6 +38,10 @@ using PairDesc = int4;
 // base in SGPRs), so a part's rows + slack stay below kMaxRowWords.
 constexpr long long kRowPadBefore = 256;
 constexpr long long kMaxRowWords = (1ll << 30) - 1024;
+// Hap match tables are addressed the same way (32-bit byte offsets from the
+// part's table base, seg_common.hpp LaneCtx::hbyte): a part's tables stay
+// below 2^30 words too (advisor round 4).
+constexpr long long kMaxHapWords = (1ll << 30) - 1024;
 
 // Run counters of a part (zeroed when the part is prepared): [0, 1] rescue
 // list lengths and [2, 3] in-wave rescue counts, by run parity (a run zeroes
@@ -52,6 +56,13 @@ constexpr int kNextWave = 4;
 constexpr int kPlanTicket = 5;   // [5, 6] fp64 planner ticket, [7, 8] plan-published flag, by run parity
 constexpr int kPlanReady = 7;
 constexpr int kStealCount = 9;    // [9, 10] stealable rescue list length, by parity
+// [12] device error word (sticky, not by parity): a kernel that cannot finish
+// its share sets a bit here instead of leaving results silently undone; the
+// host reads it with the results (the counters are the last field of a part's
+// results block, so the D2H of a call brings them along) and fails the call
+// with HC_PHMM_EHIP. Batches clear it when they report it.
+constexpr int kErrWord = 12;
+constexpr int kErrPlanWait = 1;   // fp64 pass: a workgroup gave up waiting for the rescue plan
 constexpr int kSegHeads = 16;
 constexpr int kSegQueues = 9;          // 8 XCD queues + the tail queue
 constexpr int kSegHeadStride = 16;     // ints: one 64-byte line per head
@@ -136,6 +147,8 @@ struct Seg64Args {
     int* steal_list;          // null: no stealable list this run
     const int* steal_count;
     int* steal_count_reset;   // the other run parity's, zeroed for the next run
+    int* err;                 // the part's error word (kErrWord): kErrPlanWait on a plan-wait timeout
+    int force_plan_timeout;   // test hook (HC_PHMM_TEST_PLAN_TIMEOUT=1): non-planner workgroups time out at once
 };
 // Lane-per-pair kernel (large batches): one lane owns one pair and sweeps it
 // row by row over register-resident blocks of kLaneBlock columns. A wave holds

@@ -632,6 +632,10 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
             }
             __syncthreads();
             n = n_list + int(plan_lds.lanes);
+            // Every thread holds n before plan_rescue reuses plan_lds.lanes
+            // (its thread 0 resets it first thing): without this barrier a
+            // slower wave could read the reset value (advisor round 4).
+            __syncthreads();
         }
         plan_rescue(a, n, plan_lds);
         // Publish (MI355X_MICROARCH.md, inter-workgroup visibility): every
@@ -662,7 +666,8 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
     if (!planner) {
         if (t == 0) {
             int ok = 0;
-            for (int it = 0; it < (1 << 24); ++it) {   // bounded: a wave never waits forever
+            const int limit = a.force_plan_timeout ? 0 : (1 << 24);
+            for (int it = 0; it < limit; ++it) {   // bounded: a wave never waits forever
                 if (__hip_atomic_load(a.ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
                     ok = 1;
                     break;
@@ -671,10 +676,14 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // (Not expected.) No plan: this workgroup's share of the rescue is
+            // not done, so the run must not return results: the error word
+            // makes the host fail the call with HC_PHMM_EHIP (verdict round 4).
+            if (!ok) __hip_atomic_fetch_or(a.err, kErrPlanWait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             role = ok ? 1 : -1;
         }
         __syncthreads();
-        if (role < 0) return;   // (not expected) no plan: leave the rescue undone rather than read a stale one
+        if (role < 0) return;   // never read a stale plan
     }
     const Seg64Plan* __restrict__ p = a.plan;
     const int total = __builtin_amdgcn_readfirstlane(p->wave_base[kSeg64Classes - 1]);

@@ -459,9 +459,8 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const size_t waves_max = sizeof(LaneWave) * (size_t(npairs) + 1) + sizeof(GridBlock) * spec.blocks.size() +
                              sizeof(GridSeg) * size_t(nh) + sizeof(int) * size_t(nr + nh) + 1024;
     const size_t n1 = size_t(std::max<int64_t>(npairs, 1));
-    const size_t res_o64 = (sizeof(float) * n1 + 255) & ~size_t(255);
-    const size_t res_ofl = res_o64 + ((sizeof(double) * n1 + 255) & ~size_t(255));
-    const size_t res_bytes = (res_ofl + n1 + 15) & ~size_t(15);   // whole 16-byte stores (launch_store_to_host)
+    const ResLayout RL = res_layout(n1);
+    const size_t res_bytes = RL.bytes;
     const size_t host_upload_cap = o_lw + waves_max;
     const size_t host_res_off = (host_upload_cap + 255) & ~size_t(255);
     char* host = nullptr;
@@ -963,6 +962,8 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const size_t row_pad = kRowPadBefore + size_t(rlen_max.load()) + 256;
     if (int64_t(nrows) + int64_t(row_pad) > kMaxRowWords)
         return fail(HC_PHMM_EINVAL, "batch too large (read bases of one part exceed 2^30)");
+    if (int64_t(hap_w[size_t(nh)]) + 16 > kMaxHapWords)
+        return fail(HC_PHMM_EINVAL, "batch too large (hap match tables of one part exceed 2^30 words)");
     const size_t o_rows = L.take(sizeof(uint32_t) * (size_t(nrows) + row_pad));
     const size_t o_hapw = L.take(sizeof(uint32_t) * (size_t(hap_w[size_t(nh)]) + 16));
     const size_t o_res = L.take(res_bytes);
@@ -970,7 +971,6 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const size_t o_sdesc = L.take(sizeof(PairDesc) * std::max<size_t>(size_t(n_seg_slots), 1));   // slot -> descriptor
     const size_t o_list = L.take(sizeof(int) * n1);
     const size_t o_steal = L.take(sizeof(int) * std::max<size_t>(size_t(n_seg_slots), 1));   // stealable rescues (seg pairs)
-    const size_t o_count = L.take(kNumCounters * sizeof(int));   // run counters (kernels.hpp kNumCounters)
     const size_t o_sorted = L.take(sizeof(int) * n1);
     const size_t o_worder = L.take(sizeof(int) * n1);
     const size_t o_big = L.take(sizeof(int) * n1);
@@ -1045,13 +1045,14 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     b->d_ring = ring_bytes ? dev + o_ring : nullptr;
     b->d_lane_waves = reinterpret_cast<LaneWave*>(dev + o_lw);
     b->res_bytes = res_bytes;
-    b->res_o64 = res_o64;
-    b->res_ofl = res_ofl;
+    b->res_o64 = RL.o64;
+    b->res_ofl = RL.ofl;
+    b->res_ocnt = RL.ocnt;
     b->own_raw32 = b->d_raw32 = reinterpret_cast<float*>(dev + o_res);
-    b->own_raw64 = b->d_raw64 = reinterpret_cast<double*>(dev + o_res + res_o64);
-    b->own_flag = b->d_flag = reinterpret_cast<uint8_t*>(dev + o_res + res_ofl);
+    b->own_raw64 = b->d_raw64 = reinterpret_cast<double*>(dev + o_res + RL.o64);
+    b->own_flag = b->d_flag = reinterpret_cast<uint8_t*>(dev + o_res + RL.ofl);
     b->d_list = reinterpret_cast<int*>(dev + o_list);
-    b->d_count = reinterpret_cast<int*>(dev + o_count);
+    b->d_count = reinterpret_cast<int*>(dev + o_res + RL.ocnt);   // run counters (kNumCounters): the results block's tail
     b->d_sorted = reinterpret_cast<int*>(dev + o_sorted);
     b->d_worder = reinterpret_cast<int*>(dev + o_worder);
     b->d_big = reinterpret_cast<int*>(dev + o_big);

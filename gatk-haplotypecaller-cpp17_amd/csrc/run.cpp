@@ -63,9 +63,11 @@ int run_part(Part* b, hipStream_t s)
     r.prio = int(env_i64("HC_PHMM_PRIO64", 1));
     r.raw32 = b->d_raw32;
     r.flag = b->d_flag;
+    r.err = b->d_count + kErrWord;
+    r.force_plan_timeout = env_i64("HC_PHMM_TEST_PLAN_TIMEOUT", 0) != 0 ? 1 : 0;   // test hook
     // initNative(use_double = true): no fp32 pass, every pair to the fp64 one
     // (intel_pairhmm.hpp:71,81,135-140).
-    const bool all_f64 = (g_flags.load(std::memory_order_relaxed) & HC_PHMM_FLAG_F64) != 0;
+    const bool all_f64 = (b->spec.flags & HC_PHMM_FLAG_F64) != 0;   // the call's mode (PartSpec::flags)
     bool solo = false;   // no fp64 launch after the fp32 pass (below)
     if (all_f64) HIP_TRY(launch_all_f64_list(int(b->n), b->d_raw32, b->d_flag, b->d_list, count, s));
     if (b->n_lane > 0 && !all_f64) {
@@ -234,6 +236,17 @@ int run_part(Part* b, hipStream_t s)
     b->ev_solo[b->ev_used - 1] = solo;
     b->ran = true;
     return HC_PHMM_OK;
+}
+
+// The device error word of a part's last runs (kErrWord) from a host copy of
+// its counters: HC_PHMM_EHIP with a message if any kernel gave up.
+int check_device_error(const int* counters)
+{
+    const int e = counters[kErrWord];
+    if (e == 0) return HC_PHMM_OK;
+    std::string m = "device pass incomplete (error word " + std::to_string(e) + ")";
+    if (e & kErrPlanWait) m += ": fp64 rescue workgroups timed out waiting for the rescue plan";
+    return fail(HC_PHMM_EHIP, m);
 }
 
 int enqueue_results(Part* b, hipStream_t s)

@@ -28,7 +28,9 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# HC_PHMM_LIB: load another build of the library (A/B experiments only).
+# HC_PHMM_LIB: load another build of the library (A/B experiments only). The
+# binding refuses it unless HC_PHMM_AB=1 says the caller means it (an A/B run
+# is reported as such by check_build_id; a product run never loads it).
 LIB_PATH = os.environ.get("HC_PHMM_LIB") or os.path.join(HERE, "libhcpairhmm.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "hc_pairhmm.h")
 
@@ -105,6 +107,9 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    if os.environ.get("HC_PHMM_LIB") and os.environ.get("HC_PHMM_AB") != "1":
+        raise PairHMMError(EINVAL, f"HC_PHMM_LIB={LIB_PATH} names an A/B build: set HC_PHMM_AB=1 to load it "
+                                   "(its build id is then reported, not checked against the tree)")
     if not os.path.exists(LIB_PATH):
         raise PairHMMError(ENODEV, f"{LIB_PATH} missing: run `make -C {HERE}` (no fallback path exists)")
     L = C.CDLL(LIB_PATH)
@@ -121,9 +126,12 @@ def lib():
     flat = [C.c_int64, _i64p, _i32p, _i64p, _i32p] + [_u8p] * 6
     L.hc_phmm_pairs_flat.argtypes = flat + [_f64p, _f32p, _f64p, _u8p]
     L.hc_phmm_cross.argtypes = [C.POINTER(Read), C.c_int32, C.POINTER(Hap), C.c_int32, _f64p]
+    L.hc_phmm_cross_ex.argtypes = [C.POINTER(Read), C.c_int32, C.POINTER(Hap), C.c_int32, _f64p, C.c_uint32]
     L.hc_phmm_cross_regions.argtypes = [C.POINTER(Region), C.c_int32]
     L.hc_phmm_compute_likelihoods.argtypes = [C.POINTER(Read), C.c_int32, C.POINTER(Hap), C.c_int32,
                                               _f64p, _u8p, _i32p]
+    L.hc_phmm_compute_likelihoods_ex.argtypes = [C.POINTER(Read), C.c_int32, C.POINTER(Hap), C.c_int32,
+                                                 _f64p, _u8p, _i32p, C.c_uint32]
     L.hc_phmm_batch_create.argtypes = flat + [C.POINTER(C.c_void_p)]
     L.hc_phmm_batch_run.argtypes = [C.c_void_p, C.c_void_p]
     L.hc_phmm_batch_results.argtypes = [C.c_void_p, _f64p, _f32p, _f64p, _u8p]
@@ -190,7 +198,8 @@ def _p(a, t):
     return None if a is None else a.ctypes.data_as(t)
 
 
-FLAG_F64 = 1   # HC_PHMM_FLAG_F64: initNative(use_double = true), every pair in fp64 only
+FLAG_F64 = 1         # HC_PHMM_FLAG_F64: initNative(use_double = true), every pair in fp64 only
+FLAG_KEEP_MODE = 2   # HC_PHMM_FLAG_KEEP_MODE: hc_phmm_init selects the device, the default mode stays
 
 
 def init(device: int = -1, use_double: bool = False) -> None:
@@ -274,11 +283,17 @@ def _structs(reads, haps):
     return ra, ha, keep
 
 
-def cross(reads, haps):
-    """All reads x all haps -> (n_reads, n_haps) log10 likelihoods (unnormalised)."""
+def cross(reads, haps, use_double=None):
+    """All reads x all haps -> (n_reads, n_haps) log10 likelihoods (unnormalised).
+    use_double: None = the process default (init); True / False = this call's
+    mode (hc_phmm_cross_ex)."""
     ra, ha, _keep = _structs(reads, haps)
     out = np.zeros((len(reads), len(haps)), np.float64)
-    _check(lib().hc_phmm_cross(ra, len(reads), ha, len(haps), _p(out, _f64p)))
+    if use_double is None:
+        _check(lib().hc_phmm_cross(ra, len(reads), ha, len(haps), _p(out, _f64p)))
+    else:
+        _check(lib().hc_phmm_cross_ex(ra, len(reads), ha, len(haps), _p(out, _f64p),
+                                      FLAG_F64 if use_double else 0))
     return out
 
 
@@ -386,15 +401,20 @@ def submit_regions(regions) -> Job:
     return Job(h, outs, None)
 
 
-def compute_likelihoods(haps, reads):
+def compute_likelihoods(haps, reads, use_double=None):
     """IntelPairHMM::compute_likelihoods(haplotypes, reads): returns (L, kept_reads)
-    where L has one row per surviving read (intel_pairhmm.hpp:48-56, 24-46)."""
+    where L has one row per surviving read (intel_pairhmm.hpp:48-56, 24-46).
+    use_double as in :func:`cross` (the reference's per-instance mode)."""
     ra, ha, _keep = _structs(reads, haps)
     out = np.zeros((len(reads), len(haps)), np.float64)
     keep = np.zeros(max(len(reads), 1), np.uint8)
     nk = C.c_int32(0)
-    _check(lib().hc_phmm_compute_likelihoods(ra, len(reads), ha, len(haps), _p(out, _f64p),
-                                             _p(keep, _u8p), C.byref(nk)))
+    if use_double is None:
+        _check(lib().hc_phmm_compute_likelihoods(ra, len(reads), ha, len(haps), _p(out, _f64p),
+                                                 _p(keep, _u8p), C.byref(nk)))
+    else:
+        _check(lib().hc_phmm_compute_likelihoods_ex(ra, len(reads), ha, len(haps), _p(out, _f64p),
+                                                    _p(keep, _u8p), C.byref(nk), FLAG_F64 if use_double else 0))
     mask = keep[:len(reads)].astype(bool)
     return out[mask], [r for r, k in zip(reads, mask) if k]
 

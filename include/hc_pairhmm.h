@@ -42,7 +42,9 @@
  * handles may be used concurrently). All entry points return 0 on success
  * or a negative HC_PHMM_E* code; the message of the calling thread's last
  * error is available from hc_phmm_last_error(). There is no CPU fallback:
- * without a usable MI355X the calls fail with HC_PHMM_ENODEV.
+ * without a usable MI355X the calls fail with HC_PHMM_ENODEV, and a device
+ * pass that could not complete (a kernel reports it in the part's device
+ * error word) fails with HC_PHMM_EHIP instead of returning partial results.
  */
 #ifndef HC_PAIRHMM_H
 #define HC_PAIRHMM_H
@@ -100,14 +102,22 @@ typedef struct hc_phmm_stats {
                                  result_float = 0 for every pair, so every pair is computed
                                  in fp64 only: raw_f32 = 0, rescued = 1, raw_f64 = the fp64
                                  sum, loglik = log10(raw_f64) - log10(2^1020) */
+#define HC_PHMM_FLAG_KEEP_MODE 2u /* hc_phmm_init only: select / initialise the device and leave the
+                                     process's default mode as it is (callers that pass their mode
+                                     per call, e.g. hc::MI355XPairHMM through *_ex) */
 
 /* Select the device (HIP ordinal; -1 = current) and build the device LUTs
- * (intel_pairhmm.hpp:77-113 initNative). flags: 0 or HC_PHMM_FLAG_F64; other
- * bits are HC_PHMM_EINVAL. The flags of the latest successful init apply to
- * every later run in the process (batches included) until the next init or
- * hc_phmm_shutdown (which resets them to 0). Calling it again is a no-op for
- * the same device or for -1 (apart from the flags); naming a different device
- * than the engine runs on is HC_PHMM_EINVAL (hc_phmm_shutdown first). */
+ * (intel_pairhmm.hpp:77-113 initNative). flags: 0, HC_PHMM_FLAG_F64 and/or
+ * HC_PHMM_FLAG_KEEP_MODE; other bits are HC_PHMM_EINVAL. The mode of the
+ * latest successful init (HC_PHMM_FLAG_F64 or not, unless KEEP_MODE) is the
+ * default of every later call and batch until the next init or
+ * hc_phmm_shutdown (which resets it to 0); each call or batch fixes its mode
+ * when it is made (hc_phmm_batch_create, submit), so a later init does not
+ * change work already submitted. The *_ex calls take their mode explicitly
+ * (the reference's use_double is per IntelPairHMM instance,
+ * intel_pairhmm.hpp:58,81). Calling it again is a no-op for the same device
+ * or for -1 (apart from the mode); naming a different device than the engine
+ * runs on is HC_PHMM_EINVAL (hc_phmm_shutdown first). */
 int hc_phmm_init(uint32_t flags, int device);
 /* Several device slots in one process: devices[k] is a HIP ordinal (-1 =
  * current); devices == NULL or n == 0 means every visible device. An ordinal
@@ -130,6 +140,10 @@ const char* hc_phmm_build_id(void);
  * n_reads == 0 or n_haps == 0 is a no-op. */
 int hc_phmm_cross(const hc_phmm_read* reads, int32_t n_reads,
                   const hc_phmm_hap* haps, int32_t n_haps, double* out);
+/* The same with this call's mode: mode = 0 or HC_PHMM_FLAG_F64 (other bits:
+ * HC_PHMM_EINVAL), independent of the process default set by hc_phmm_init. */
+int hc_phmm_cross_ex(const hc_phmm_read* reads, int32_t n_reads,
+                     const hc_phmm_hap* haps, int32_t n_haps, double* out, uint32_t mode);
 
 /* Many active regions in one device pass (cross-region batching, SURVEY §8(f)
  * row 2): region k is the cross product reads x haps of regions[k], written
@@ -153,6 +167,10 @@ int hc_phmm_cross_regions(const hc_phmm_region* regions, int32_t n_regions);
 int hc_phmm_compute_likelihoods(const hc_phmm_read* reads, int32_t n_reads,
                                 const hc_phmm_hap* haps, int32_t n_haps,
                                 double* out, uint8_t* keep, int32_t* n_kept);
+/* The same with this call's mode (as hc_phmm_cross_ex). */
+int hc_phmm_compute_likelihoods_ex(const hc_phmm_read* reads, int32_t n_reads,
+                                   const hc_phmm_hap* haps, int32_t n_haps,
+                                   double* out, uint8_t* keep, int32_t* n_kept, uint32_t mode);
 
 /* Independent pairs over flat byte pools: pair p uses rs/q/ins/del/gcp rows
  * [read_off[p], read_off[p]+R[p]) and hap bytes [hap_off[p], hap_off[p]+H[p]).

@@ -29,15 +29,16 @@ namespace hc {
 class MI355XPairHMM {
 public:
     // use_double: initNative(use_double) (intel_pairhmm.hpp:71,81): every pair
-    // in fp64 only. The mode is process-wide in the engine (hc_phmm_init
-    // flags), set again by each compute_likelihoods call.
+    // in fp64 only. Per instance, as the reference's g_use_double: each call
+    // passes it (hc_phmm_compute_likelihoods_ex), so instances with different
+    // modes in different threads do not interfere.
     explicit MI355XPairHMM(int device = -1, bool use_double = false) : device_(device), use_double_(use_double) {}
 
     template <class HaplotypeT, class SAMRecordT>
     std::vector<std::vector<double>> compute_likelihoods(const std::vector<HaplotypeT>& haplotypes,
                                                          std::vector<SAMRecordT>& reads)
     {
-        check(hc_phmm_init(use_double_ ? HC_PHMM_FLAG_F64 : 0u, device_));
+        check(hc_phmm_init(HC_PHMM_FLAG_KEEP_MODE, device_));   // device only: the mode goes with the call
         const int nr = static_cast<int>(reads.size()), nh = static_cast<int>(haplotypes.size());
         std::vector<std::string> gaps;   // owned i/d/c strings where the record's are short
         gaps.reserve(3 * reads.size());
@@ -65,7 +66,8 @@ public:
         std::vector<double> flat(static_cast<size_t>(nr) * nh);
         std::vector<uint8_t> keep(reads.size());
         int32_t kept = 0;
-        check(hc_phmm_compute_likelihoods(rv.data(), nr, hv.data(), nh, flat.data(), keep.data(), &kept));
+        check(hc_phmm_compute_likelihoods_ex(rv.data(), nr, hv.data(), nh, flat.data(), keep.data(), &kept,
+                                             use_double_ ? HC_PHMM_FLAG_F64 : 0u));
         std::vector<std::vector<double>> out;
         out.reserve(kept);
         std::vector<SAMRecordT> survivors;

@@ -138,12 +138,17 @@ def test_flat_record_nibble_packing():
 
 
 def test_init_rejects_unknown_flags(built):
-    """hc_phmm_init flags: 0 or HC_PHMM_FLAG_F64 (initNative's use_double);
-    any other bit is refused before a device is touched."""
+    """hc_phmm_init flags: HC_PHMM_FLAG_F64 (initNative's use_double) and
+    HC_PHMM_FLAG_KEEP_MODE; any other bit is refused before a device is
+    touched, and so is an unknown mode of the per-call *_ex entry points."""
     L = hcphmm.lib()
-    assert L.hc_phmm_init(2, 0) == hcphmm.EINVAL
+    assert L.hc_phmm_init(4, 0) == hcphmm.EINVAL
     assert b"flags" in L.hc_phmm_last_error()
     assert L.hc_phmm_init_devices(0x80, None, 0) == hcphmm.EINVAL
+    L.hc_phmm_cross_ex.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
+                                   ctypes.c_void_p, ctypes.c_uint32]
+    assert L.hc_phmm_cross_ex(None, 1, None, 1, None, 2) == hcphmm.EINVAL
+    assert b"mode" in L.hc_phmm_last_error()
 
 
 def test_stale_binary_is_refused(built, monkeypatch):

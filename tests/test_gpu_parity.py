@@ -84,6 +84,21 @@ def test_s1_full_vs_oracle(engine, kernel, oracle_lib):
     assert_same(res, ref, "S1")
 
 
+def test_s1w_full_vs_oracle(engine, oracle_lib):
+    """The north star's 101 x 250 shape (S1w: configs[1]'s 10k pairs with the
+    250-base haps BASELINE.json's north_star names), the whole batch against
+    the oracle, flat call and a prepared batch run twice."""
+    b = W.config("S1w")
+    assert (b["R"] == 101).all() and (b["H"] == 250).all() and len(b["R"]) == 10_000
+    ref = oracle_lib.pairs(b, nthreads=16)
+    assert_same(engine.pairs(b), ref, "S1w flat")
+    bt = engine.Batch(b)
+    for k in range(2):
+        bt.run()
+        assert_same(bt.results(), ref, f"S1w batch run {k}")
+    bt.close()
+
+
 def test_s2_sample_vs_oracle(engine, kernel, oracle_lib):
     b = W.config("S2", 20_000)
     res = engine.pairs(b)
@@ -547,3 +562,65 @@ def test_seg_records_and_gather_with_mixed_kernels(engine, oracle_lib, monkeypat
     assert 0 < st.n_seg_waves   # seg waves ran ...
     assert st.n_lane_pairs < st.n_pairs if mode == "auto" else st.n_launch_waves > st.n_seg_waves   # ... and another kernel
     bt.close()
+
+
+@pytest.mark.parametrize("plan", ["static", "dynamic"])
+def test_rescue_plan_timeout_is_an_error(engine, oracle_lib, monkeypatch, plan):
+    """A fp64 workgroup that gives up waiting for the device-made rescue plan
+    (lane_kernel.hip phmm_seg64_kernel, bounded wait) sets the part's device
+    error word, and the call fails with HC_PHMM_EHIP instead of returning
+    results (verdict round 4). HC_PHMM_TEST_PLAN_TIMEOUT=1 makes every
+    non-planner workgroup time out at once: a static plan (S4-200: fewer waves
+    than two per SIMD) and a dynamic one (thousands of long rescued pairs),
+    through a flat call and a prepared batch; the batch then runs correctly
+    once the hook is off (the error word is cleared when reported)."""
+    import hcphmm
+    if plan == "static":
+        b = W.subset(W.config("S4"), np.arange(200))
+    else:
+        b = W.generate(4000, (1000, 1500), (150, 250), 0.08, seed=71)
+    ref = oracle_lib.pairs(b, nthreads=16)
+    assert ref["rescued"].sum() > (100 if plan == "static" else 3000)
+    bt = engine.Batch(b)
+    monkeypatch.setenv("HC_PHMM_TEST_PLAN_TIMEOUT", "1")
+    with pytest.raises(hcphmm.PairHMMError) as e:
+        engine.pairs(b)
+    assert e.value.code == hcphmm.EHIP and "rescue plan" in str(e.value)
+    bt.run()
+    with pytest.raises(hcphmm.PairHMMError) as e:
+        bt.results()
+    assert e.value.code == hcphmm.EHIP
+    monkeypatch.delenv("HC_PHMM_TEST_PLAN_TIMEOUT")
+    bt.run()
+    assert_same(bt.results(), ref, f"{plan}: after the hook")
+    bt.close()
+    assert_same(engine.pairs(b), ref, f"{plan}: flat after the hook")
+
+
+def test_mode_is_per_call_and_fixed_at_submit(engine, golden, golden_batch):
+    """initNative's use_double is per IntelPairHMM instance in the reference
+    (intel_pairhmm.hpp:58,81): hc_phmm_cross_ex / compute_likelihoods_ex take
+    the mode per call whatever the process default is, and a batch keeps the
+    mode it was created with when the default changes later (advisor round 4)."""
+    # a small region of S1-shaped reads x haps: the fp32 / fp64 modes differ
+    b = W.config("S1", 64)
+    reads = [(bytes(b["rs"][o:o + r]), bytes(b["q"][o:o + r]), bytes(b["ins"][o:o + r]),
+              bytes(b["dels"][o:o + r]), bytes(b["gcp"][o:o + r])) for o, r in zip(b["read_off"][:8], b["R"][:8])]
+    haps = [bytes(b["hap"][o:o + h]) for o, h in zip(b["hap_off"][:4], b["H"][:4])]
+    f32 = engine.cross(reads, haps)
+    bt = engine.Batch(golden_batch)   # created in fp32 mode
+    engine.init(0, use_double=True)
+    try:
+        assert np.array_equal(bits(engine.cross(reads, haps, use_double=False)), bits(f32))
+        f64 = engine.cross(reads, haps)   # process default: fp64 only
+        assert not np.array_equal(bits(f64), bits(f32))
+        bt.run()
+        got = bt.results()
+        assert np.array_equal(got["rescued"], golden["rescued"])   # still the fp32 pass deciding
+        assert np.array_equal(bits(got["raw_f32"]), bits(golden["raw_f32"]))
+    finally:
+        engine.init(0, use_double=False)
+        bt.close()
+    assert np.array_equal(bits(engine.cross(reads, haps, use_double=True)), bits(f64))
+    L, kept = engine.compute_likelihoods(haps, reads, use_double=True)
+    assert L.shape[1] == len(haps) and len(kept) == L.shape[0]

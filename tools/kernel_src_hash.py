@@ -8,12 +8,16 @@ lib_src_hash(): every source of libhcpairhmm.so (csrc/, include/, the
 Makefile's flag lines, the Jacobian table generator).
 
     python tools/kernel_src_hash.py                  # kernel hash
-    python tools/kernel_src_hash.py --header OUT.h   # both hashes + git HEAD as C macros
+    python tools/kernel_src_hash.py --header OUT.h [--extra "FLAGS"]
+                                                     # both hashes + git HEAD as C macros
 
 The Makefile compiles that header into the library (hc_phmm_build_id()), so a
 run can prove which sources the binary it loaded was built from: bench.py and
 __graft_entry__.smoke() compare the library's hashes with the tree's and
-refuse a stale binary."""
+refuse a stale binary. The Makefile passes its EXTRA_DEV_FLAGS (A/B builds,
+e.g. -DHC_SEG_WPB=4) with --extra: a non-empty value enters both hashes, so
+such a build never matches the tree and is loaded only as an A/B build
+(hcphmm.py: HC_PHMM_LIB with HC_PHMM_AB=1)."""
 import hashlib
 import os
 import subprocess
@@ -31,16 +35,18 @@ def _flag_lines(prefixes):
     return "".join(ln for ln in mk.splitlines() if ln.startswith(prefixes)).encode()
 
 
-def kernel_src_hash() -> str:
+def kernel_src_hash(extra: str = "") -> str:
     h = hashlib.sha256()
     for f in FILES:
         h.update(f.encode())
         h.update(open(os.path.join(SRC, f), "rb").read())
     h.update(_flag_lines(("DEV_FLAGS",)))
+    if extra.strip():
+        h.update(b"EXTRA_DEV_FLAGS=" + extra.strip().encode())
     return h.hexdigest()[:16]
 
 
-def lib_src_hash() -> str:
+def lib_src_hash(extra: str = "") -> str:
     h = hashlib.sha256()
     files = [os.path.join(SRC, f) for f in sorted(os.listdir(SRC))]
     inc = os.path.join(ROOT, "include")
@@ -52,6 +58,8 @@ def lib_src_hash() -> str:
         h.update(os.path.relpath(p, ROOT).encode())
         h.update(open(p, "rb").read())
     h.update(_flag_lines(("DEV_FLAGS", "HOST_FLAGS")))
+    if extra.strip():
+        h.update(b"EXTRA_DEV_FLAGS=" + extra.strip().encode())
     return h.hexdigest()[:16]
 
 
@@ -66,9 +74,9 @@ def git_head() -> str:
         return "unknown"
 
 
-def write_header(path: str) -> None:
-    txt = (f'#define HC_KERNEL_SRC_HASH "{kernel_src_hash()}"\n'
-           f'#define HC_LIB_SRC_HASH "{lib_src_hash()}"\n'
+def write_header(path: str, extra: str = "") -> None:
+    txt = (f'#define HC_KERNEL_SRC_HASH "{kernel_src_hash(extra)}"\n'
+           f'#define HC_LIB_SRC_HASH "{lib_src_hash(extra)}"\n'
            f'#define HC_GIT_HEAD "{git_head()}"\n')
     try:
         if open(path).read() == txt:
@@ -80,8 +88,8 @@ def write_header(path: str) -> None:
 
 
 if __name__ == "__main__":
-    if len(sys.argv) == 3 and sys.argv[1] == "--header":
-        write_header(sys.argv[2])
+    if len(sys.argv) in (3, 5) and sys.argv[1] == "--header":
+        write_header(sys.argv[2], sys.argv[4] if len(sys.argv) == 5 and sys.argv[3] == "--extra" else "")
     elif len(sys.argv) == 2 and sys.argv[1] == "--lib":
         print(lib_src_hash())
     else:
