@@ -633,6 +633,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
         a.max_waves = int(max_waves);
         a.nwaves = reinterpret_cast<int*>(dev + o_nw);
         a.counters = b->d_count;
+        a.list = b->d_list;
         HIP_TRY(launch_flat_plan(a, s));
         HIP_TRY(hipEventRecord(b->pack_ev[1], s));
         if (with_run) {

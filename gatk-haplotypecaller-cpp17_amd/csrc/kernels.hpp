@@ -63,11 +63,18 @@ constexpr int kStealCount = 9;    // [9, 10] stealable rescue list length, by pa
 // with HC_PHMM_EHIP. Batches clear it when they report it.
 constexpr int kErrWord = 12;
 constexpr int kErrPlanWait = 1;   // fp64 pass: a workgroup gave up waiting for the rescue plan
-constexpr int kSegHeads = 16;
+constexpr int kErrFusedWait = 2;  // fused pass: a wave gave up waiting for a listed rescue's entry
+// [16..21] the fused pass's rescue queue (LaneArgs::fz_*), by run parity:
+// waves started, waves done with their fp32 pairs, queue head.
+constexpr int kFusedStarted = 16;
+constexpr int kFusedDone = 18;
+constexpr int kFusedHead = 20;
+constexpr int kSegHeads = 24;
 constexpr int kSegQueues = 9;          // 8 XCD queues + the tail queue
 constexpr int kSegHeadStride = 16;     // ints: one 64-byte line per head
 constexpr int kSegDone = kSegHeads + kSegQueues * kSegHeadStride;
 constexpr int kNumCounters = kSegDone + 16;
+static_assert(kNumCounters <= 256, "the prep kernels zero the counters with one 256-thread block");
 
 struct DiagArgs {
     const PairDesc* pairs;
@@ -219,7 +226,25 @@ struct LaneArgs {
     // null = off (every deferred rescue to rescue_list).
     int* steal_list;
     int* steal_count;
+    // Fused pass (phmm_seg_kernel<kFusedOcc, true>; run.cpp: small parts of
+    // seg pairs with H <= kSeg64MaxH, every wave resident at once): no fp64
+    // launch. A wave appends its flagged pairs to rescue_list (pid + 1; the
+    // entries are zero before the run and the consumer zeroes them again),
+    // counts itself done, then takes listed rescues from the queue head and
+    // recomputes each in fp64 over its 64 lanes (seg_common.hpp
+    // fused_rescues). It waits for more only while every wave of the launch
+    // has started and some are still in their fp32 pairs, so a waiting wave
+    // never holds a slot an undispatched wave needs. null = off.
+    int* fz_started;      // launched as phmm_seg_kernel<kFusedOcc, true> when set
+    int* fz_done;
+    int* fz_head;
+    int* err;             // the part's error word (kErrWord)
+    int prio64;           // the fused pass's fp64 rescues: issue priority by remaining steps (as Seg64Args::prio)
 };
+// Waves per SIMD of the fused pass (fp64 blocks up to 32 columns in the same
+// waves: 256 VGPRs); run.cpp takes it only when every wave of a part is
+// resident at once at this occupancy.
+constexpr int kFusedOcc = 2;
 // Result record of one seg slot: {raw f32 bits, state, raw f64 low word, high
 // word}; state 0 = not rescued, 1 = rescued in the fp32 pass (raw f64 here),
 // 2 = rescued by the fp64 pass (raw f64 written there, by pair id).
@@ -294,6 +319,8 @@ struct PackArgs {
     int4* sdesc;
     int* steal;   // the part's stealable rescue list, zeroed here (n_steal entries)
     int n_steal;
+    int* list;    // the part's rescue list, zeroed here (n_list entries; the fused pass's queue)
+    int n_list;
 };
 hipError_t launch_pack_batch(const PackArgs& a, hipStream_t s);
 // Pair descriptors of a structured (cross-product) plan, built on the device
@@ -377,6 +404,7 @@ struct FlatPlanArgs {
     int* nwaves;           // the plan's wave count
     int tail;              // waves dispatched last, longest first (0: packing order)
     int* counters;         // kNumCounters run counters, zeroed
+    int* list;             // the rescue list (n entries), zeroed (the fused pass's queue)
 };
 hipError_t launch_flat_plan(const FlatPlanArgs& a, hipStream_t s);
 // bytes (a multiple of 16, both 16-byte aligned) from device memory to mapped

@@ -396,14 +396,18 @@ __device__ void plan_rescue(const Seg64Args& a, int n, PlanLds& L)
     }
 }
 
-// One column-segmented wave (wid) of the fp32 pass.
-__device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float* __restrict__ slut)
+// One column-segmented wave (wid) of the fp32 pass. FUSED: the fused pass
+// (LaneArgs::fz_*): flagged pairs go to the queue, then the wave takes queued
+// rescues (seg_common.hpp fused_rescues); nw = the launch's waves.
+template <bool FUSED = false>
+__device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float* __restrict__ slut, int nw = 0)
 {
     // Lane id and the wave's LDS tables in forms the compiler can recompute
     // (mbcnt) or keep in SGPRs (wave-uniform): values live across the step
     // loop that it would otherwise spill at every wave's start.
     const int lane = __lane_id();
     const unsigned long long t_start = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (FUSED && lane == 0) __hip_atomic_fetch_add(a.fz_started, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const LaneWave wv = load_wave(a.waves, wid);
     const int bc = wv.ncols;
     __shared__ uint2 mtab[kSegWPB][5 * 64];
@@ -467,8 +471,14 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
             if (!resc) a.raw64_zero[pid] = 0.0;
         }
     }
-    const uint64_t todo = __builtin_amdgcn_ballot_w64(resc);
-    if (todo) rescue_in_wave(a, todo, pid, slot, cx.H, lane, mt);
+    if constexpr (FUSED) {
+        // pair id + 1: a zero entry is one whose store has not landed yet
+        if (resc) __hip_atomic_store(a.rescue_list + atomicAdd(a.rescue_count, 1), pid + 1, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        const uint64_t todo = __builtin_amdgcn_ballot_w64(resc);
+        if (todo) rescue_in_wave(a, todo, pid, slot, cx.H, lane, mt);
+    }
     if (a.timeline && lane == 0) {
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
         a.timeline[3 * size_t(wid)] = t_start;
@@ -477,7 +487,12 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
         a.timeline[3 * size_t(wid) + 2] = (unsigned long long)unsigned(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))) |
                                           ((unsigned long long)unsigned(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11))) << 32);
     }
-    if (a.steal_list) steal_rescues(a, wid, lane, mt);
+    if constexpr (FUSED) {
+        __builtin_amdgcn_wave_barrier();   // the rescues below rewrite mt
+        fused_rescues<kSeg64Widths - 1>(a, nw, lane, mt);
+    } else if (a.steal_list) {
+        steal_rescues(a, wid, lane, mt);
+    }
 }
 
 
@@ -503,7 +518,7 @@ __device__ __forceinline__ int seg_fetch(int* head)
     return __builtin_amdgcn_readfirstlane(v);
 }
 
-template <int OCC>
+template <int OCC, bool FUSED = false>
 __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
 {
     // Each wave fills its own copy of the prior tables: no workgroup barrier
@@ -524,12 +539,15 @@ __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
         c[kPlanTicket + o] = 0;
         c[kPlanReady + o] = 0;
         c[kStealCount + o] = 0;
+        c[kFusedStarted + o] = 0;
+        c[kFusedDone + o] = 0;
+        c[kFusedHead + o] = 0;
     }
     if (wid >= n_waves) return;   // wave-uniform (device-planned parts launch an upper bound)
     float* slut = sluts[wib];
     for (int t = __lane_id(); t < kSlutLen; t += 64) slut[t] = a.lut[t];
     __builtin_amdgcn_wave_barrier();
-    seg_wave(a, wid, slut);
+    seg_wave<FUSED>(a, wid, slut, n_waves);
 }
 
 // The persistent form (a separate instance: its fetch loop around the width
@@ -803,6 +821,10 @@ hipError_t launch_lane_seg_f32(const LaneArgs& a, int max_waves, int queues, hip
 {
     if (a.n_waves <= 0) return hipSuccess;
     const int grid = (a.n_waves + kSegWPB - 1) / kSegWPB;
+    if (a.fz_started) {
+        hipLaunchKernelGGL((phmm_seg_kernel<kFusedOcc, true>), dim3(grid), dim3(64 * kSegWPB), 0, s, a);
+        return hipGetLastError();
+    }
     const int max_blocks = max_waves / kSegWPB;
     // Persistent only when the waves outnumber the launch's slots (device-
     // planned parts: their upper bound does; the kernel re-reads the count).

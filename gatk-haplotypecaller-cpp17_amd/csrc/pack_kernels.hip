@@ -92,6 +92,9 @@ __device__ __forceinline__ void pack_items(const PackArgs& a)
 {
     // The stealable rescue list starts each part zeroed (its runs zero what they use).
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < a.n_steal; k += gridDim.x * blockDim.x) a.steal[k] = 0;
+    // the rescue list starts zeroed: the fused pass's entries are pair id + 1
+    // (its consumers zero them again after each run)
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < a.n_list; k += gridDim.x * blockDim.x) a.list[k] = 0;
     const int lane = threadIdx.x & 63;
     const int n = max(a.nreads, a.nhaps);
     const int stride = gridDim.x * 4;
@@ -256,6 +259,7 @@ __host__ __device__ constexpr int align4(int x) { return (x + 3) & ~3; }
 __global__ __launch_bounds__(256) void flat_prep_kernel(FlatPlanArgs a)
 {
     if (blockIdx.x == 0 && threadIdx.x < kNumCounters) a.counters[threadIdx.x] = 0;
+    for (int k = blockIdx.x * 256 + threadIdx.x; k < a.n; k += gridDim.x * 256) a.list[k] = 0;   // as pack_items
     const int lane = threadIdx.x & 63;
     const int stride = gridDim.x * 4;
     int p = blockIdx.x * 4 + (threadIdx.x >> 6);

@@ -1102,6 +1102,8 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     pack.sdesc = b->d_sdesc;
     pack.steal = b->d_steal;   // zeroed by the prep launch
     pack.n_steal = b->d_steal ? int(n_seg_slots) : 0;
+    pack.list = b->d_list;   // zeroed by the prep launch (the fused pass's queue)
+    pack.n_list = int(npairs);
     auto enqueue = [&]() -> int {
         if (!b->slot_ev)
             for (auto& e : b->pack_ev) HIP_TRY(hipEventCreate(&e));

@@ -156,7 +156,31 @@ int run_part(Part* b, hipStream_t s)
             solo = !rec && persist == 0 && n_one == 0 && b->n_wide == 0 && b->cls[0].n == 0 && b->cls[1].n == 0 &&
                    a.inker_count != nullptr && b->Hmax <= kInWaveRescueMaxH &&
                    b->n <= env_i64("HC_PHMM_SOLO_MAX_PAIRS", 32768);
-            if (solo) {
+            // Fused pass (kernels.hpp LaneArgs::fz_*): a part whose waves are
+            // all resident at once at kFusedOcc and whose haps are all within a
+            // 64-lane fp64 rescue (H <= kSeg64MaxH) lists its rescues on a
+            // queue that the waves done with their fp32 pairs drain while the
+            // others still run — no fp64 launch, no wait for the slowest fp32
+            // wave (S4: 2 000 pairs of 1-2 kb, 93 % rescued). HC_PHMM_FUSED: 0 off,
+            // 1 (default) when the haps are past the in-wave rescue's reach
+            // (solo covers the rest), 2 whenever it applies.
+            const int64_t fz = env_i64("HC_PHMM_FUSED", 1);
+            const bool fused = fz != 0 && !rec && persist == 0 && n_one == 0 && b->n_wide == 0 && b->cls[0].n == 0 &&
+                               b->cls[1].n == 0 && b->Hmax <= kSeg64MaxH &&
+                               int64_t(b->n_seg_waves) <= int64_t(kFusedOcc) * 4 * dv.n_cu &&
+                               (fz == 2 || b->Hmax > kInWaveRescueMaxH);
+            if (fused) {
+                solo = true;
+                g.solo_counters = b->d_count;
+                g.solo_other = par ^ 1;
+                g.fz_started = b->d_count + kFusedStarted + par;
+                g.fz_done = b->d_count + kFusedDone + par;
+                g.fz_head = b->d_count + kFusedHead + par;
+                g.err = b->d_count + kErrWord;
+                g.prio64 = r.prio;
+                g.inker_count = nullptr;
+                b->inker_limit = 0;
+            } else if (solo) {
                 g.solo_counters = b->d_count;
                 g.solo_other = par ^ 1;
                 g.inker_limit = std::numeric_limits<int>::max();

@@ -449,6 +449,17 @@ __device__ __forceinline__ void run_seg_bc(const T* __restrict__ lut, const T* _
 // rs < 0 (a stolen rescue, another wave's pair): the raw f64 goes to
 // raw64_zero[rp] even with records (its record says kRecListed, which the
 // gather leaves to the rescue's own store).
+// MAXWI: the widest fp64 block width compiled in (seg64_width(MAXWI)): 0 =
+// 8 columns, H <= 512 (the in-wave rescue of the occupancy-3 fp32 kernel);
+// kSeg64Widths - 1 = 32 columns, H <= kSeg64MaxH (the fused pass). A pair
+// takes the narrowest width that covers its hap on 64 lanes.
+__device__ __forceinline__ int rescue_width_index(int H)
+{
+    const int need = (H + 63) >> 6;   // columns per lane on 64 lanes
+    return need <= 8 ? 0 : (need - 8 + 3) >> 2;
+}
+
+template <int MAXWI = 0>
 __device__ __forceinline__ void rescue_one(const LaneArgs& a, const PairDesc pd, int rp, int rs, int lane,
                                            uint2* __restrict__ mt)
 {
@@ -456,13 +467,24 @@ __device__ __forceinline__ void rescue_one(const LaneArgs& a, const PairDesc pd,
     const int rx = __builtin_amdgcn_readfirstlane(pd.x);
     const LaneCtx cx{a.rows - kRowPadBefore, unsigned(rx + kRowPadBefore) * 4u, a.hapw,
                      unsigned(__builtin_amdgcn_readfirstlane(pd.z)) * 4u, R, H};
-    const int nb = (H + 7) / 8;
-    const SegSteps st{R, R, R + nb - 1};
+    const int wi = MAXWI == 0 ? 0 : rescue_width_index(H);
+    const int bc = seg64_width(wi);
+    const int nb = (H + bc - 1) / bc;
+    const SegSteps st{R, R, R + nb - 1, MAXWI == 0 ? 0 : a.prio64};
     const uint32_t w1 = row_word(cx, 0);
     const double T0 = row0_t<double>(a.lut64, w1, H);
     const bool eq = read_eq(w1);
     double sM = 0.0, sX = 0.0;
-    run_seg_bc<double, 8>(a.lut64, a.lut64, st, lane, lane, cx, T0, sM, sX, mt, eq);
+    switch (wi) {
+#define HC_RESCUE_CASE(WI) \
+    case WI: \
+        if constexpr (WI <= MAXWI) run_seg_bc<double, seg64_width(WI)>(a.lut64, a.lut64, st, lane, lane, cx, T0, sM, sX, mt, eq); \
+        break;
+        HC_RESCUE_CASE(0) HC_RESCUE_CASE(1) HC_RESCUE_CASE(2) HC_RESCUE_CASE(3) HC_RESCUE_CASE(4) HC_RESCUE_CASE(5)
+        HC_RESCUE_CASE(6)
+#undef HC_RESCUE_CASE
+    default: break;
+    }
     if (lane == nb - 1) {
         const double r = sM + sX;
         if (a.rec && rs >= 0) {   // record of slot rs: state and raw f64 (after the owner's store: same wave, program order)
@@ -547,6 +569,71 @@ __device__ __forceinline__ void steal_rescues(const LaneArgs& a, int wid, int la
         if (v <= 0) return;
         rescue_one(a, a.pairs[v - 1], v - 1, -1, lane, mt);   // (uniform: rescue_one reads it with readfirstlane)
         seed = seed * 1664525u + 1013904223u;
+    }
+}
+
+// The fused pass's rescue queue (LaneArgs::fz_*): this wave has appended its
+// flagged pairs; it counts itself done (after a release, so the entries are
+// visible first), then takes listed rescues from the head, oldest first, each
+// recomputed in fp64 over its 64 lanes (rescue_one: the rescue of
+// intel_pairhmm.hpp:137-139, as the fp64 launch would). With nothing listed it
+// waits only while every one of the launch's nw waves has started and some are
+// still in their fp32 pairs (they may still list rescues): a waiting wave never
+// holds a slot an undispatched wave needs, and the waves it waits for are
+// running. Claims go by compare-and-swap on the head, never past the count, so
+// no wave holds a claim nobody will fill. Both waits are bounded; giving up
+// sets the part's error word (the host fails the call).
+constexpr int kFusedWaitIters = 1 << 24;
+template <int MAXWI>
+__device__ __forceinline__ void fused_rescues(const LaneArgs& a, int nw, int lane, uint2* __restrict__ mt)
+{
+    constexpr auto AG = __HIP_MEMORY_SCOPE_AGENT;
+    if (lane == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_fetch_add(a.fz_done, 1, __ATOMIC_RELAXED, AG);
+    }
+    int idle = 0;
+    for (;;) {
+        int v = 0;   // > 0: a claimed pair id + 1; 0: done; -1: wait; -2: lost a race, retry
+        if (lane == 0) {
+            const int h = __hip_atomic_load(a.fz_head, __ATOMIC_RELAXED, AG);
+            const int c = __hip_atomic_load(a.rescue_count, __ATOMIC_RELAXED, AG);
+            if (h < c) {
+                int hh = h;
+                if (__hip_atomic_compare_exchange_strong(a.fz_head, &hh, h + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED, AG)) {
+                    // the appender has its index; its store of the entry follows
+                    int e = 0;
+                    for (int it = 0; it < kFusedWaitIters; ++it) {
+                        e = __hip_atomic_load(a.rescue_list + h, __ATOMIC_RELAXED, AG);
+                        if (e != 0) break;
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    if (e == 0) __hip_atomic_fetch_or(a.err, kErrFusedWait, __ATOMIC_RELAXED, AG);
+                    else __hip_atomic_store(a.rescue_list + h, 0, __ATOMIC_RELAXED, AG);   // clean for the next run
+                    v = e;
+                } else {
+                    v = -2;
+                }
+            } else {
+                const int st = __hip_atomic_load(a.fz_started, __ATOMIC_RELAXED, AG);
+                const int dn = __hip_atomic_load(a.fz_done, __ATOMIC_ACQUIRE, AG);
+                v = (st >= nw && dn < nw) ? -1 : 0;
+            }
+        }
+        v = __builtin_amdgcn_readfirstlane(v);
+        if (v == 0) return;
+        if (v == -2) continue;
+        if (v == -1) {
+            if (++idle >= kFusedWaitIters) {
+                if (lane == 0) __hip_atomic_fetch_or(a.err, kErrFusedWait, __ATOMIC_RELAXED, AG);
+                return;
+            }
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        idle = 0;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        rescue_one<MAXWI>(a, a.pairs[v - 1], v - 1, -1, lane, mt);
     }
 }
 

@@ -304,7 +304,7 @@ def test_repeated_runs_reuse_rescue_counters(engine, oracle_lib):
     bt.close()
 
 
-@pytest.mark.parametrize("in_wave", ["on", "off"])
+@pytest.mark.parametrize("in_wave", ["on", "off", "fused-off"])
 @pytest.mark.parametrize("shape", ["short_list", "mid_list", "long_list", "wide_haps"])
 def test_fp64_rescue_tiers(engine, oracle_lib, monkeypatch, shape, in_wave):
     """The fp64 rescue pass is planned on the device: block width 8 / 16 / 32
@@ -312,8 +312,12 @@ def test_fp64_rescue_tiers(engine, oracle_lib, monkeypatch, shape, in_wave):
     2^k-lane classes, haps too wide for 64 blocks of 32 on the anti-diagonal
     fp64 kernel. High substitution rates force most pairs into rescue. With
     in_wave on, fp32 waves holding one or two rescued pairs (H <= 1024)
-    recompute them themselves (short_list is mostly that path)."""
-    monkeypatch.setenv("HC_PHMM_RESCUE_IN_WAVE", "1" if in_wave == "on" else "0")
+    recompute them themselves (short_list is mostly that path). Small parts
+    with haps past 512 take the fused pass by default (short / mid lists);
+    fused-off sends them through the fp64 launch's tiers as well."""
+    monkeypatch.setenv("HC_PHMM_RESCUE_IN_WAVE", "0" if in_wave == "off" else "1")
+    if in_wave == "fused-off":
+        monkeypatch.setenv("HC_PHMM_FUSED", "0")
     n, h, r = {"short_list": (40, (300, 900), (100, 250)),
                "mid_list": (1500, (600, 1100), (150, 250)),
                "long_list": (4500, (1000, 1200), (150, 250)),
@@ -624,3 +628,37 @@ def test_mode_is_per_call_and_fixed_at_submit(engine, golden, golden_batch):
     assert np.array_equal(bits(engine.cross(reads, haps, use_double=True)), bits(f64))
     L, kept = engine.compute_likelihoods(haps, reads, use_double=True)
     assert L.shape[1] == len(haps) and len(kept) == L.shape[0]
+
+
+@pytest.mark.parametrize("mode", ["auto", "forced", "off"])
+@pytest.mark.parametrize("shape", ["S4", "S4-300", "many-per-wave", "short-haps"])
+def test_fused_pass(engine, oracle_lib, monkeypatch, shape, mode):
+    """The fused pass (run.cpp, kernels.hpp LaneArgs::fz_*): a small part's
+    waves list their rescues on a queue and drain it themselves, no fp64
+    launch (HC_PHMM_FUSED: auto = haps past 512, forced = whenever it applies,
+    off = the fp64 launch). configs[4] (S4, 2 000 pairs, 93 % rescued) and a
+    subset; 8 000 pairs of 520-700 bases four to a wave, most rescued (a wave
+    lists several, other waves take them); short haps (the solo path's domain
+    unless forced). Flat call and a prepared batch run three times (the queue
+    counters go by run parity, the entries are zeroed by their consumers),
+    against the oracle; the rescued count is the oracle's."""
+    monkeypatch.setenv("HC_PHMM_FUSED", {"auto": "1", "forced": "2", "off": "0"}[mode])
+    b = {"S4": lambda: W.config("S4"),
+         "S4-300": lambda: W.subset(W.config("S4"), np.arange(300)),
+         "many-per-wave": lambda: W.generate(8000, (520, 700), (60, 200), 0.08, seed=41),
+         "short-haps": lambda: W.generate(3000, (100, 500), (60, 200), 0.08, seed=23)}[shape]()
+    ref = oracle_lib.pairs(b, nthreads=16)
+    n_resc = int(ref["rescued"].sum())
+    assert n_resc > len(b["R"]) // 3
+    assert_same(engine.pairs(b), ref, f"{shape}/{mode} flat")
+    bt = engine.Batch(b)
+    for k in range(3):
+        bt.run()
+        got = bt.results()
+        assert_same(got, ref, f"{shape}/{mode} run {k}")
+        assert (got["raw_f64"][~ref["rescued"].astype(bool)] == 0).all()
+    st = bt.stats()
+    assert st.n_rescued == n_resc
+    if mode != "off":
+        assert st.kernel_ms_f64 == 0   # no fp64 launch: the fused (or solo) pass did every rescue
+    bt.close()
