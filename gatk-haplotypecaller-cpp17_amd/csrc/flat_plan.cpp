@@ -46,6 +46,7 @@ struct Mini {
 
 struct FlatScratch {
     std::vector<int32_t> gapw;
+    std::vector<uint8_t> fmtw;   // scanning pass 1: each pair's record format (kFmt* bits)
     std::vector<Mini> mini;
     std::vector<int32_t> hsamp;
 };
@@ -113,11 +114,14 @@ bool constant_gaps(const uint8_t* i, const uint8_t* d, const uint8_t* c, int len
 
 constexpr int align4(int x) { return (x + 3) & ~3; }
 
-// Record of a pair (pack_kernels.hip flat_prep_kernel): qualities, read code
-// nibbles, [i, d, c planes], hap code nibbles, each field 4-byte aligned.
-inline int64_t record_bytes(int R, int H, bool planes)
+// Record of a pair (pack_kernels.hip flat_prep_kernel), each field 4-byte
+// aligned: the read — one byte per base (kFmtRead1B: quality delta and 2-bit
+// code) or its qualities then its code nibbles —, [i, d, c planes], the hap —
+// 2-bit codes (kFmtHap2b) or nibbles.
+inline int64_t record_bytes(int R, int H, bool planes, int fmt)
 {
-    return align4(R) + align4((R + 1) / 2) + (planes ? 3 * int64_t(align4(R)) : 0) + align4((H + 1) / 2);
+    return align4(R) + ((fmt & kFmtRead1B) ? 0 : align4((R + 1) / 2)) + (planes ? 3 * int64_t(align4(R)) : 0) +
+           ((fmt & kFmtHap2b) ? align4((H + 3) / 4) : align4((H + 1) / 2));
 }
 
 // ConvertChar (pairhmm_common.h:26-44): A0 C1 T2 G3 N4, every other byte -> 0.
@@ -216,12 +220,159 @@ void pack_nibbles(const uint8_t* s, int n, uint8_t* d)
 
 namespace {
 
+// ---- compact record fields (kernels.hpp kFmtRead1B / kFmtHap2b)
+
+// A read fits one byte per base when no base is 'N' and its qualities (& 127)
+// span less than 64; qbase = their minimum.
+bool read_1b_scalar(const uint8_t* q, const uint8_t* b, int R, int& qbase)
+{
+    int mn = 127, mx = 0;
+    bool n = false;
+    for (int k = 0; k < R; ++k) {
+        const int v = q[k] & 127;
+        mn = std::min(mn, v);
+        mx = std::max(mx, v);
+        n |= b[k] == 'N';
+    }
+    qbase = mn;
+    return !n && mx - mn < 64;
+}
+
+__attribute__((target("avx2"))) inline void read_1b_step(const uint8_t* q, const uint8_t* b, __m256i& vmn,
+                                                          __m256i& vmx, __m256i& vn)
+{
+    const __m256i v = _mm256_and_si256(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(q)), _mm256_set1_epi8(0x7f));
+    vmn = _mm256_min_epu8(vmn, v);
+    vmx = _mm256_max_epu8(vmx, v);
+    vn = _mm256_or_si256(vn, _mm256_cmpeq_epi8(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(b)),
+                                               _mm256_set1_epi8('N')));
+}
+
+__attribute__((target("avx2"))) bool read_1b_avx2(const uint8_t* q, const uint8_t* b, int R, int& qbase)
+{
+    if (R < 32) return read_1b_scalar(q, b, R, qbase);
+    __m256i vmn = _mm256_set1_epi8(0x7f), vmx = _mm256_setzero_si256(), vn = _mm256_setzero_si256();
+    int k = 0;
+    for (; k + 32 <= R; k += 32) read_1b_step(q + k, b + k, vmn, vmx, vn);
+    if (k < R) read_1b_step(q + R - 32, b + R - 32, vmn, vmx, vn);   // overlapping: min / max / any are idempotent
+    alignas(32) uint8_t mn[32], mx[32];
+    _mm256_store_si256(reinterpret_cast<__m256i*>(mn), vmn);
+    _mm256_store_si256(reinterpret_cast<__m256i*>(mx), vmx);
+    int a = 127, z = 0;
+    for (int j = 0; j < 32; ++j) {
+        a = std::min(a, int(mn[j]));
+        z = std::max(z, int(mx[j]));
+    }
+    qbase = a;
+    return _mm256_testz_si256(vn, vn) && z - a < 64;
+}
+
+bool read_1b(const uint8_t* q, const uint8_t* b, int R, int& qbase)
+{
+    return has_avx2() ? read_1b_avx2(q, b, R, qbase) : read_1b_scalar(q, b, R, qbase);
+}
+
+// d[k] = ((q[k] & 127) - qbase) << 2 | code(b[k]) (codes A0 C1 T2 G3, others 0;
+// no 'N' here).
+void pack_read_1b_scalar(const uint8_t* q, const uint8_t* b, int R, int qbase, uint8_t* d)
+{
+    const auto& ct = code_table();
+    for (int k = 0; k < R; ++k) d[k] = uint8_t((((q[k] & 127) - qbase) << 2) | (ct[b[k]] & 3));
+}
+
+__attribute__((target("avx2"))) inline __m256i read_1b32(const uint8_t* q, const uint8_t* b, __m256i vqb)
+{
+    const __m256i v = _mm256_sub_epi8(
+        _mm256_and_si256(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(q)), _mm256_set1_epi8(0x7f)), vqb);
+    // v < 64: the 16-bit shift carries only zero bits across bytes
+    return _mm256_or_si256(_mm256_slli_epi16(v, 2),
+                           codes32(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(b))));
+}
+
+__attribute__((target("avx2"))) void pack_read_1b_avx2(const uint8_t* q, const uint8_t* b, int R, int qbase,
+                                                       uint8_t* d)
+{
+    if (R < 32) {
+        pack_read_1b_scalar(q, b, R, qbase, d);
+        return;
+    }
+    const __m256i vqb = _mm256_set1_epi8(char(qbase));
+    int k = 0;
+    for (; k + 32 <= R; k += 32) _mm256_storeu_si256(reinterpret_cast<__m256i*>(d + k), read_1b32(q + k, b + k, vqb));
+    if (k < R) _mm256_storeu_si256(reinterpret_cast<__m256i*>(d + R - 32), read_1b32(q + R - 32, b + R - 32, vqb));
+}
+
+void pack_read_1b(const uint8_t* q, const uint8_t* b, int R, int qbase, uint8_t* d)
+{
+    if (has_avx2())
+        pack_read_1b_avx2(q, b, R, qbase, d);
+    else
+        pack_read_1b_scalar(q, b, R, qbase, d);
+}
+
+// Hap codes 2 bits each (a hap with no 'N'): false if it has one.
+bool pack_hap_2b_scalar(const uint8_t* s, int n, uint8_t* d)
+{
+    const auto& ct = code_table();
+    bool ok = true;
+    for (int k = 0; k < n; k += 4) {
+        uint8_t x = 0;
+        for (int j = 0; j < 4 && k + j < n; ++j) {
+            const uint8_t c = ct[s[k + j]];
+            ok &= c != 4;
+            x |= uint8_t((c & 3) << (2 * j));
+        }
+        d[k >> 2] = x;
+    }
+    return ok;
+}
+
+__attribute__((target("avx2"))) bool pack_hap_2b_avx2(const uint8_t* s, int n, uint8_t* d)
+{
+    const __m256i kN = _mm256_set1_epi8('N');
+    const __m256i gather = _mm256_setr_epi8(0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
+                                            0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1);
+    __m256i vn = _mm256_setzero_si256();
+    int k = 0;
+    for (; k + 32 <= n; k += 32) {
+        const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + k));
+        vn = _mm256_or_si256(vn, _mm256_cmpeq_epi8(v, kN));
+        // codes c0 + 4 c1 per 16 bits, then (c0 + 4 c1) + 16 (c2 + 4 c3) per 32 bits
+        const __m256i t = _mm256_maddubs_epi16(codes32(v), _mm256_set1_epi16(0x0401));
+        const __m256i u = _mm256_madd_epi16(t, _mm256_set1_epi32(0x00100001));
+        const __m256i g = _mm256_shuffle_epi8(u, gather);
+        const uint64_t w = uint64_t(uint32_t(_mm256_extract_epi32(g, 0))) |
+                           (uint64_t(uint32_t(_mm256_extract_epi32(g, 4))) << 32);
+        std::memcpy(d + (k >> 2), &w, 8);
+    }
+    const bool ok = k < n ? pack_hap_2b_scalar(s + k, n - k, d + (k >> 2)) : true;
+    return ok && _mm256_testz_si256(vn, vn);
+}
+
+bool pack_hap_2b(const uint8_t* s, int n, uint8_t* d)
+{
+    return has_avx2() ? pack_hap_2b_avx2(s, n, d) : pack_hap_2b_scalar(s, n, d);
+}
+
+bool has_n(const uint8_t* s, int n) { return std::memchr(s, 'N', size_t(n)) != nullptr; }
+
+}  // namespace
+
+// (test hooks below)
+bool read_1b_hook(const uint8_t* q, const uint8_t* b, int R, int& qbase) { return read_1b(q, b, R, qbase); }
+void pack_read_1b_hook(const uint8_t* q, const uint8_t* b, int R, int qbase, uint8_t* d) { pack_read_1b(q, b, R, qbase, d); }
+bool pack_hap_2b_hook(const uint8_t* s, int n, uint8_t* d) { return pack_hap_2b(s, n, d); }
+
+namespace {
+
 // Pass 2 over mini-tasks [m0, m1): each pair's record at buf + (its offset
-// - r0) and its descriptor at dd[k - p0]. With scan_gaps false, a read whose
-// gap qualities vary sets `varying` (the part is planned again with planes).
+// - r0) and its descriptor at dd[k - p0]. With scan_gaps false (pass 1 assumed
+// constant gap qualities and compact fields everywhere), a read whose gap
+// qualities vary or that does not fit one byte per base, or a hap with an 'N',
+// sets `varying` (the part is planned again with pass 1 scanning: fmtw[k]).
 void fill_chunk(const Src& src, int64_t lo, int64_t n, int64_t m0, int64_t m1, const Mini* mini,
-                const int32_t* gapw, bool scan_gaps, char* buf, int64_t r0, FlatDesc* dd, int64_t p0,
-                std::atomic<bool>& varying)
+                const int32_t* gapw, const uint8_t* fmtw, bool scan_gaps, char* buf, int64_t r0, FlatDesc* dd,
+                int64_t p0, std::atomic<bool>& varying)
 {
     parallel_for(m1 - m0, [&](int64_t a, int64_t e) {
         for (int64_t m = m0 + a; m < m0 + e; ++m) {
@@ -232,8 +383,10 @@ void fill_chunk(const Src& src, int64_t lo, int64_t n, int64_t m0, int64_t m1, c
                 const int R = src.R[p], H = src.H[p];
                 const int64_t o = src.read_off[p];
                 int32_t g;
+                int fmt;
                 if (scan_gaps) {
                     g = gapw[k];
+                    fmt = fmtw[k];
                 } else {
                     const uint8_t *ip = src.ins + o, *dp = src.del + o, *cp = src.gcp + o;
                     if (!constant_gaps(ip, dp, cp, R)) {
@@ -241,21 +394,39 @@ void fill_chunk(const Src& src, int64_t lo, int64_t n, int64_t m0, int64_t m1, c
                         return;
                     }
                     g = int32_t((ip[0] & 127) | ((dp[0] & 127) << 7) | ((cp[0] & 127) << 14));
+                    fmt = kFmtRead1B | kFmtHap2b;
                 }
                 const int qa = align4(R);
                 uint8_t* d = reinterpret_cast<uint8_t*>(buf + (ro - r0));
-                copy_bytes(src.q + o, R, d);
-                pack_nibbles(src.rs + o, R, d + qa);
-                size_t at = size_t(qa) + size_t(align4((R + 1) / 2));
+                size_t at = size_t(qa);
+                int qbase = 0;
+                if (fmt & kFmtRead1B) {
+                    if (!read_1b(src.q + o, src.rs + o, R, qbase)) {
+                        varying.store(true, std::memory_order_relaxed);   // (scan mode never lists such a read)
+                        return;
+                    }
+                    pack_read_1b(src.q + o, src.rs + o, R, qbase, d);
+                } else {
+                    copy_bytes(src.q + o, R, d);
+                    pack_nibbles(src.rs + o, R, d + qa);
+                    at += size_t(align4((R + 1) / 2));
+                }
                 if (g < 0) {
                     std::memcpy(d + at, src.ins + o, size_t(R));
                     std::memcpy(d + at + qa, src.del + o, size_t(R));
                     std::memcpy(d + at + 2 * qa, src.gcp + o, size_t(R));
                     at += 3 * size_t(qa);
                 }
-                pack_nibbles(src.hap + src.hap_off[p], H, d + at);
-                dd[k - p0] = FlatDesc{ro, int(rw), R, H, int(hw), g, 0};
-                ro += record_bytes(R, H, g < 0);
+                if (fmt & kFmtHap2b) {
+                    if (!pack_hap_2b(src.hap + src.hap_off[p], H, d + at)) {
+                        varying.store(true, std::memory_order_relaxed);
+                        return;
+                    }
+                } else {
+                    pack_nibbles(src.hap + src.hap_off[p], H, d + at);
+                }
+                dd[k - p0] = FlatDesc{ro, int(rw), R, H, int(hw), g, fmt | (qbase << 8)};
+                ro += record_bytes(R, H, g < 0, fmt);
                 rw += qa;
                 hw += hap_table_words(H);
             }
@@ -266,8 +437,8 @@ void fill_chunk(const Src& src, int64_t lo, int64_t n, int64_t m0, int64_t m1, c
 // Pass 1 over pairs [lo, lo + n): per mini-task sums and bounds; with
 // scan_gaps, each read's constant gap triple (or -1) in gapw; every stride-th
 // hap length in hsamp.
-void scan_pass(const Src& src, int64_t lo, int64_t n, bool scan_gaps, Mini* mini, int32_t* gapw, int32_t* hsamp,
-               int64_t stride)
+void scan_pass(const Src& src, int64_t lo, int64_t n, bool scan_gaps, Mini* mini, int32_t* gapw, uint8_t* fmtw,
+               int32_t* hsamp, int64_t stride)
 {
     const int64_t nmini = (n + kMini - 1) / kMini;
     parallel_for(nmini, [&](int64_t m0, int64_t m1) {
@@ -283,6 +454,7 @@ void scan_pass(const Src& src, int64_t lo, int64_t n, bool scan_gaps, Mini* mini
                     continue;
                 }
                 int32_t g = 0;
+                int fmt = kFmtRead1B | kFmtHap2b;   // assumed (checked by pass 2) unless scanning
                 if (scan_gaps) {
                     const int64_t o = src.read_off[p];
                     const uint8_t *ip = src.ins + o, *dp = src.del + o, *cp = src.gcp + o;
@@ -290,8 +462,12 @@ void scan_pass(const Src& src, int64_t lo, int64_t n, bool scan_gaps, Mini* mini
                             ? int32_t((ip[0] & 127) | ((dp[0] & 127) << 7) | ((cp[0] & 127) << 14))
                             : -1;
                     gapw[k] = g;
+                    int qb;
+                    fmt = (read_1b(src.q + o, src.rs + o, R, qb) ? kFmtRead1B : 0) |
+                          (has_n(src.hap + src.hap_off[p], H) ? 0 : kFmtHap2b);
+                    fmtw[k] = uint8_t(fmt);
                 }
-                M.rec += record_bytes(R, H, g < 0);
+                M.rec += record_bytes(R, H, g < 0, fmt);
                 M.rows += align4(R);
                 M.hapw += hap_table_words(H);
                 M.rmax = std::max(M.rmax, R);
@@ -305,7 +481,7 @@ void scan_pass(const Src& src, int64_t lo, int64_t n, bool scan_gaps, Mini* mini
     }, 8);
 }
 
-constexpr int kRetryWithPlanes = 1;   // plan_flat_try: a read's gap qualities vary
+constexpr int kRetryWithPlanes = 1;   // plan_flat_try: a read's gap qualities vary, or a field is not compact
 
 bool default_policies()
 {
@@ -321,8 +497,9 @@ bool default_policies()
 
 namespace {
 
-// One attempt: scan_gaps = false assumes constant gap qualities (checked in
-// pass 2; kRetryWithPlanes if one varies), true finds them in pass 1.
+// One attempt: scan_gaps = false assumes constant gap qualities and compact
+// read / hap fields (checked in pass 2; kRetryWithPlanes if one is not), true
+// finds each pair's in pass 1.
 int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool with_run, bool scan_gaps,
                   Part** out)
 {
@@ -332,16 +509,18 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     if (n <= 0 || n > (int64_t(1) << 31) - 1) return HC_PHMM_OK;
     FlatScratch& S = t_fs;
     grow(S.gapw, size_t(n));
+    grow(S.fmtw, size_t(n));
     const int64_t nmini = (n + kMini - 1) / kMini;
     S.mini.assign(size_t(nmini), Mini{});
     const int64_t stride = std::max<int64_t>(1, n / 8192);   // cap-model sample of hap lengths
     const int64_t nsamp = (n + stride - 1) / stride;
     grow(S.hsamp, size_t(nsamp));
     int32_t* gapw = S.gapw.data();
+    uint8_t* fmtw = S.fmtw.data();
     Mini* mini = S.mini.data();
     int32_t* hsamp = S.hsamp.data();
 
-    scan_pass(src, lo, n, scan_gaps, mini, gapw, hsamp, stride);
+    scan_pass(src, lo, n, scan_gaps, mini, gapw, fmtw, hsamp, stride);
     tm.mark("flat: scan");
 
     int rmax = 0, rmin = INT32_MAX, hmax = 0, hmin = INT32_MAX;
@@ -592,7 +771,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
                 char* buf = dv.ring.buf[ri];
                 const size_t dbase = (size_t(r1 - r0) + 255) & ~size_t(255);
                 FlatDesc* dd = reinterpret_cast<FlatDesc*>(buf + dbase);
-                fill_chunk(src, lo, n, m0, m1, mini, gapw, scan_gaps, buf, r0, dd, p0, varying);
+                fill_chunk(src, lo, n, m0, m1, mini, gapw, fmtw, scan_gaps, buf, r0, dd, p0, varying);
                 if (varying.load()) return kRetryWithPlanes;
                 HIP_TRY(hipMemcpyAsync(dev + o_img + r0, buf, size_t(r1 - r0), hipMemcpyHostToDevice, s));
                 HIP_TRY(hipMemcpyAsync(dev + o_desc + sizeof(FlatDesc) * size_t(p0), dd,
@@ -667,6 +846,18 @@ int plan_flat_device(Device& dv, const Src& src, const PartSpec& spec, Slot* slo
 
 // Host-logic test hook (not part of the ABI): the record's nibble packing.
 extern "C" void hcx_pack_nibbles(const uint8_t* s, int n, uint8_t* d) { hcphmm::eng::pack_nibbles(s, n, d); }
+// Host-logic test hooks (not part of the ABI): the compact record fields.
+// Returns 1 (and writes d, *qbase) if the read fits one byte per base, else 0.
+extern "C" int hcx_pack_read_1b(const uint8_t* q, const uint8_t* b, int n, uint8_t* d, int* qbase)
+{
+    int qb = 0;
+    if (!hcphmm::eng::read_1b_hook(q, b, n, qb)) return 0;
+    hcphmm::eng::pack_read_1b_hook(q, b, n, qb, d);
+    *qbase = qb;
+    return 1;
+}
+// Returns 1 if the hap has no 'N' (d holds its 2-bit codes), else 0.
+extern "C" int hcx_pack_hap_2b(const uint8_t* s, int n, uint8_t* d) { return hcphmm::eng::pack_hap_2b_hook(s, n, d) ? 1 : 0; }
 
 // Host-pass timing without a GPU (not part of the ABI: tools/flat_host_bench.py):
 // pass 1 and pass 2 of a flat call over pairs [0, n) into host memory, `reps`
@@ -691,13 +882,14 @@ extern "C" void hcx_flat_host_passes(int64_t n, const int64_t* read_off, const i
     const int64_t nmini = (n + kMini - 1) / kMini;
     std::vector<Mini> mini;
     std::vector<int32_t> gapw(static_cast<size_t>(n)), hsamp(static_cast<size_t>(n));
+    std::vector<uint8_t> fmtw(static_cast<size_t>(n));
     std::vector<char> buf;
     std::vector<FlatDesc> dd(static_cast<size_t>(n));
     ms[0] = ms[1] = 0;
     for (int r = 0; r <= reps; ++r) {   // rep 0 sizes the buffers (untimed)
         auto t0 = std::chrono::steady_clock::now();
         mini.assign(size_t(nmini), Mini{});
-        scan_pass(src, 0, n, false, mini.data(), gapw.data(), hsamp.data(), std::max<int64_t>(1, n / 8192));
+        scan_pass(src, 0, n, false, mini.data(), gapw.data(), fmtw.data(), hsamp.data(), std::max<int64_t>(1, n / 8192));
         int64_t rec = 0;
         for (auto& M : mini) {
             const int64_t x = M.rec;
@@ -707,7 +899,8 @@ extern "C" void hcx_flat_host_passes(int64_t n, const int64_t* read_off, const i
         if (buf.size() < size_t(rec)) buf.resize(size_t(rec));
         auto t1 = std::chrono::steady_clock::now();
         std::atomic<bool> varying{false};
-        fill_chunk(src, 0, n, 0, nmini, mini.data(), gapw.data(), false, buf.data(), 0, dd.data(), 0, varying);
+        fill_chunk(src, 0, n, 0, nmini, mini.data(), gapw.data(), fmtw.data(), false, buf.data(), 0, dd.data(), 0,
+                   varying);
         auto t2 = std::chrono::steady_clock::now();
         if (r == 0) continue;
         ms[0] += std::chrono::duration<double, std::milli>(t1 - t0).count() / reps;

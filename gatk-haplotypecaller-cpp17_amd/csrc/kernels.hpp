@@ -235,14 +235,17 @@ struct LaneArgs {
     // fused_rescues). It waits for more only while every wave of the launch
     // has started and some are still in their fp32 pairs, so a waiting wave
     // never holds a slot an undispatched wave needs. null = off.
-    int* fz_started;      // launched as phmm_seg_kernel<kFusedOcc, true> when set
+    int* fz_started;      // launches the fused form of phmm_seg_kernel when set
     int* fz_done;
     int* fz_head;
+    int fz_wide;          // 1: fp64 blocks up to 32 columns (H <= kSeg64MaxH) at kFusedOcc waves per
+                          // SIMD; 0: 8 columns (H <= kInWaveRescueMaxH) at the fp32 pass's 3
     int* err;             // the part's error word (kErrWord)
+    int force_wait_timeout;   // test hook (HC_PHMM_TEST_PLAN_TIMEOUT=1): a wave reaching the queue gives up at once
     int prio64;           // the fused pass's fp64 rescues: issue priority by remaining steps (as Seg64Args::prio)
 };
-// Waves per SIMD of the fused pass (fp64 blocks up to 32 columns in the same
-// waves: 256 VGPRs); run.cpp takes it only when every wave of a part is
+// Waves per SIMD of the wide fused pass (fp64 blocks up to 32 columns in the
+// same waves: 256 VGPRs); run.cpp takes it only when every wave of a part is
 // resident at once at this occupancy.
 constexpr int kFusedOcc = 2;
 // Result record of one seg slot: {raw f32 bits, state, raw f64 low word, high
@@ -377,8 +380,16 @@ struct FlatDesc {
     int R, H;
     int hapw_off;    // first word of the hap's match table
     int gapw;        // constant gap qualities i | d << 7 | c << 14, or -1 (planes in the record)
-    int pad;
+    int fmt;         // record format: kFmt* bits, the read's quality base in bits 8-14
 };
+// Compact record fields (flat_plan.cpp): a read with no 'N' whose qualities
+// (& 127) span less than 64 sends one byte per base, (q - qbase) << 2 | code
+// (codes A0 C1 T2 G3, every other byte 0 as ConvertChar), instead of its
+// quality byte and code nibble; a hap with no 'N' sends its codes 2 bits each
+// (base k in bits 2(k % 4) of byte k / 4) instead of nibbles. The S2 batch
+// uploads ~250 instead of ~416 bytes per pair.
+constexpr int kFmtRead1B = 1;
+constexpr int kFmtHap2b = 2;
 struct FlatPlanArgs {
     const uint8_t* img;
     const FlatDesc* desc;

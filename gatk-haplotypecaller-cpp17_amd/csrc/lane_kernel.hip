@@ -399,7 +399,7 @@ __device__ void plan_rescue(const Seg64Args& a, int n, PlanLds& L)
 // One column-segmented wave (wid) of the fp32 pass. FUSED: the fused pass
 // (LaneArgs::fz_*): flagged pairs go to the queue, then the wave takes queued
 // rescues (seg_common.hpp fused_rescues); nw = the launch's waves.
-template <bool FUSED = false>
+template <bool FUSED = false, int MAXWI = 0>
 __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float* __restrict__ slut, int nw = 0)
 {
     // Lane id and the wave's LDS tables in forms the compiler can recompute
@@ -489,7 +489,7 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
     }
     if constexpr (FUSED) {
         __builtin_amdgcn_wave_barrier();   // the rescues below rewrite mt
-        fused_rescues<kSeg64Widths - 1>(a, nw, lane, mt);
+        fused_rescues<MAXWI>(a, nw, lane, mt);
     } else if (a.steal_list) {
         steal_rescues(a, wid, lane, mt);
     }
@@ -518,7 +518,10 @@ __device__ __forceinline__ int seg_fetch(int* head)
     return __builtin_amdgcn_readfirstlane(v);
 }
 
-template <int OCC, bool FUSED = false>
+// FUSED: the fused pass (LaneArgs::fz_*); its rescues take fp64 blocks up to
+// seg64_width(MAXWI) columns: 32 at 2 waves per SIMD (haps up to 2 048), 8 at
+// the fp32 pass's 3 (haps up to 512, the in-wave rescue's registers).
+template <int OCC, bool FUSED = false, int MAXWI = 0>
 __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
 {
     // Each wave fills its own copy of the prior tables: no workgroup barrier
@@ -547,7 +550,7 @@ __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
     float* slut = sluts[wib];
     for (int t = __lane_id(); t < kSlutLen; t += 64) slut[t] = a.lut[t];
     __builtin_amdgcn_wave_barrier();
-    seg_wave<FUSED>(a, wid, slut, n_waves);
+    seg_wave<FUSED, MAXWI>(a, wid, slut, n_waves);
 }
 
 // The persistent form (a separate instance: its fetch loop around the width
@@ -822,7 +825,11 @@ hipError_t launch_lane_seg_f32(const LaneArgs& a, int max_waves, int queues, hip
     if (a.n_waves <= 0) return hipSuccess;
     const int grid = (a.n_waves + kSegWPB - 1) / kSegWPB;
     if (a.fz_started) {
-        hipLaunchKernelGGL((phmm_seg_kernel<kFusedOcc, true>), dim3(grid), dim3(64 * kSegWPB), 0, s, a);
+        if (a.fz_wide)
+            hipLaunchKernelGGL((phmm_seg_kernel<kFusedOcc, true, kSeg64Widths - 1>), dim3(grid), dim3(64 * kSegWPB), 0,
+                               s, a);
+        else
+            hipLaunchKernelGGL((phmm_seg_kernel<kSegOcc, true, 0>), dim3(grid), dim3(64 * kSegWPB), 0, s, a);
         return hipGetLastError();
     }
     const int max_blocks = max_waves / kSegWPB;

@@ -246,11 +246,32 @@ __global__ __launch_bounds__(256) void prepare_grid_kernel(GridPrepArgs a)
 // ---------------------------------------------------------------------------
 // Flat batches planned on the device (kernels.hpp FlatPlanArgs).
 
-// Flat records (flat_plan.cpp, kernels.hpp FlatDesc): the read's base
-// qualities, its base codes as nibbles (ConvertChar, two per byte, row k in
-// the low nibble of byte k/2 when k is even), its i / d / c planes when they
-// vary, then the hap's base codes as nibbles; every field 4-byte aligned.
+// Flat records (flat_plan.cpp, kernels.hpp FlatDesc): the read — one byte per
+// base, (q - qbase) << 2 | code (kFmtRead1B), or its base qualities then its
+// base codes as nibbles (ConvertChar, two per byte, row k in the low nibble of
+// byte k/2 when k is even) —, its i / d / c planes when they vary, then the
+// hap's base codes, 2 bits (kFmtHap2b) or a nibble each; every field 4-byte
+// aligned.
 __host__ __device__ constexpr int align4(int x) { return (x + 3) & ~3; }
+
+// kFmtRead1B: four rows' bytes -> their qualities (bytes) and code nibbles.
+__device__ __forceinline__ void read_1b_unpack(uint32_t b4, uint32_t qbase4, uint32_t& q4, uint32_t& c4)
+{
+    q4 = ((b4 >> 2) & 0x3f3f3f3fu) + qbase4;   // (q & 127) <= 127: no carry between bytes
+    uint32_t c = b4 & 0x03030303u;             // code j in byte j
+    c = (c | (c >> 4)) & 0x00ff00ffu;          // codes 0,1 in the low byte, 2,3 in byte 2
+    c4 = (c | (c >> 8)) & 0xffffu;             // code j in nibble j
+}
+
+// kFmtHap2b: the 2-bit codes of 8 columns -> nibbles (column j in nibble j).
+__device__ __forceinline__ uint32_t hap_2b_nibbles(uint32_t h16)
+{
+    uint32_t x = h16 & 0xffffu;
+    x = (x | (x << 8)) & 0x00ff00ffu;
+    x = (x | (x << 4)) & 0x0f0f0f0fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    return x;
+}
 
 // One wave per pair (grid-stride): its rows, its hap table, its pair
 // descriptor, and its plan key — the cheaper of its two (block width, lanes)
@@ -274,45 +295,53 @@ __global__ __launch_bounds__(256) void flat_prep_kernel(FlatPlanArgs a)
         const int R = __builtin_amdgcn_readfirstlane(dn.R), H = __builtin_amdgcn_readfirstlane(dn.H);
         const int ro = __builtin_amdgcn_readfirstlane(dn.row_off), ho = __builtin_amdgcn_readfirstlane(dn.hapw_off);
         const int gw = __builtin_amdgcn_readfirstlane(dn.gapw);
+        const int fmt = __builtin_amdgcn_readfirstlane(dn.fmt);
         if (p + stride < a.n) dn = a.desc[p + stride];
+        const bool r1b = (fmt & kFmtRead1B) != 0, h2b = (fmt & kFmtHap2b) != 0;
+        const uint32_t qbase4 = uint32_t((fmt >> 8) & 127) * 0x01010101u;
         const int qa = align4(R);
         const uint32_t* __restrict__ q32 = reinterpret_cast<const uint32_t*>(quals);
         const uint16_t* __restrict__ c16 = reinterpret_cast<const uint16_t*>(quals + qa);
-        const uint32_t* __restrict__ g32 = reinterpret_cast<const uint32_t*>(quals + qa + align4((R + 1) / 2));
+        const uint32_t* __restrict__ g32 = reinterpret_cast<const uint32_t*>(quals + qa + (r1b ? 0 : align4((R + 1) / 2)));
         const uint32_t* __restrict__ h32 = g32 + (gw < 0 ? 3 * (qa >> 2) : 0);
+        const uint16_t* __restrict__ h16 = reinterpret_cast<const uint16_t*>(h32);
         const int qa4 = qa >> 2;
         uint32_t q4 = 0, c4 = 0, i4 = 0, d4 = 0, g4 = 0, hx = 0;
         if (4 * lane < R) {
             q4 = q32[lane];
-            c4 = c16[lane];
+            if (!r1b) c4 = c16[lane];
             if (gw < 0) {
                 i4 = g32[lane];
                 d4 = g32[qa4 + lane];
                 g4 = g32[2 * qa4 + lane];
             }
         }
-        if (8 * lane < H) hx = h32[lane];
+        if (8 * lane < H) hx = h2b ? hap_2b_nibbles(h16[lane]) : h32[lane];
         const int2 c = a.ctab[H];
         uint4* __restrict__ rows = reinterpret_cast<uint4*>(a.rows + ro);
         for (int t0 = 0; 4 * t0 < R; t0 += 64) {
             const int t = t0 + lane;
             if (t0 > 0 && 4 * t < R) {
                 q4 = q32[t];
-                c4 = c16[t];
+                if (!r1b) c4 = c16[t];
                 if (gw < 0) {
                     i4 = g32[t];
                     d4 = g32[qa4 + t];
                     g4 = g32[2 * qa4 + t];
                 }
             }
-            if (4 * t < R) rows[t] = rows_rec4(q4, c4, i4, d4, g4, gw, t == 0);
+            if (4 * t < R) {
+                uint32_t qq = q4, cc = c4;
+                if (r1b) read_1b_unpack(q4, qbase4, qq, cc);
+                rows[t] = rows_rec4(qq, cc, i4, d4, g4, gw, t == 0);
+            }
         }
         uint32_t* __restrict__ o = a.hapw + ho;
         const int nw = (H + 31) / 32;
         hap_zero_rows(nw, o, lane);
         for (int base = 0; base < H; base += 512) {
             const int nv = H - base - 8 * lane;   // valid columns of this lane (<= 0: none)
-            if (base > 0) hx = nv > 0 ? h32[base / 8 + lane] : 0u;
+            if (base > 0) hx = nv > 0 ? (h2b ? hap_2b_nibbles(h16[base / 8 + lane]) : h32[base / 8 + lane]) : 0u;
             hap_words(hx, nv, base, nw, o, lane);
         }
         if (lane == 0) {

@@ -156,20 +156,26 @@ int run_part(Part* b, hipStream_t s)
             solo = !rec && persist == 0 && n_one == 0 && b->n_wide == 0 && b->cls[0].n == 0 && b->cls[1].n == 0 &&
                    a.inker_count != nullptr && b->Hmax <= kInWaveRescueMaxH &&
                    b->n <= env_i64("HC_PHMM_SOLO_MAX_PAIRS", 32768);
-            // Fused pass (kernels.hpp LaneArgs::fz_*): a part whose waves are
-            // all resident at once at kFusedOcc and whose haps are all within a
-            // 64-lane fp64 rescue (H <= kSeg64MaxH) lists its rescues on a
+            // Fused pass (kernels.hpp LaneArgs::fz_*): the part's rescues go on a
             // queue that the waves done with their fp32 pairs drain while the
             // others still run — no fp64 launch, no wait for the slowest fp32
-            // wave (S4: 2 000 pairs of 1-2 kb, 93 % rescued). HC_PHMM_FUSED: 0 off,
-            // 1 (default) when the haps are past the in-wave rescue's reach
-            // (solo covers the rest), 2 whenever it applies.
+            // wave. Wide: every wave resident at once at kFusedOcc, haps up to
+            // kSeg64MaxH (S4: 2 000 pairs of 1-2 kb, 93 % rescued). Narrow: haps
+            // up to 512 in the fp32 pass's own registers, any part size (a wave
+            // takes queued rescues only once the launch's last wave has been
+            // dispatched: the 415 x 128 region's ~400 rescues run in its last
+            // round instead of a launch after it). Not with per-slot records
+            // (their gather is the fp64 launch's) or other fp32 kernels.
+            // HC_PHMM_FUSED: 0 off; 1 (default) where solo does not apply;
+            // 2 wide and narrow also where solo would.
             const int64_t fz = env_i64("HC_PHMM_FUSED", 1);
-            const bool fused = fz != 0 && !rec && persist == 0 && n_one == 0 && b->n_wide == 0 && b->cls[0].n == 0 &&
-                               b->cls[1].n == 0 && b->Hmax <= kSeg64MaxH &&
-                               int64_t(b->n_seg_waves) <= int64_t(kFusedOcc) * 4 * dv.n_cu &&
-                               (fz == 2 || b->Hmax > kInWaveRescueMaxH);
-            if (fused) {
+            const bool fz_ok = fz != 0 && !rec && persist == 0 && n_one == 0 && b->n_wide == 0 && b->cls[0].n == 0 &&
+                               b->cls[1].n == 0 && (fz == 2 || !solo);
+            const bool fz_narrow = fz_ok && b->Hmax <= kInWaveRescueMaxH;
+            const bool fz_wide = fz_ok && !fz_narrow && b->Hmax <= kSeg64MaxH &&
+                                 int64_t(b->n_seg_waves) <= int64_t(kFusedOcc) * 4 * dv.n_cu;
+            if (fz_narrow || fz_wide) {
+                g.fz_wide = fz_wide ? 1 : 0;
                 solo = true;
                 g.solo_counters = b->d_count;
                 g.solo_other = par ^ 1;
@@ -178,6 +184,7 @@ int run_part(Part* b, hipStream_t s)
                 g.fz_head = b->d_count + kFusedHead + par;
                 g.err = b->d_count + kErrWord;
                 g.prio64 = r.prio;
+                g.force_wait_timeout = r.force_plan_timeout;
                 g.inker_count = nullptr;
                 b->inker_limit = 0;
             } else if (solo) {
@@ -270,6 +277,7 @@ int check_device_error(const int* counters)
     if (e == 0) return HC_PHMM_OK;
     std::string m = "device pass incomplete (error word " + std::to_string(e) + ")";
     if (e & kErrPlanWait) m += ": fp64 rescue workgroups timed out waiting for the rescue plan";
+    if (e & kErrFusedWait) m += ": fused-pass waves timed out waiting for listed rescues";
     return fail(HC_PHMM_EHIP, m);
 }
 

@@ -591,7 +591,9 @@ __device__ __forceinline__ void fused_rescues(const LaneArgs& a, int nw, int lan
     if (lane == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __hip_atomic_fetch_add(a.fz_done, 1, __ATOMIC_RELAXED, AG);
+        if (a.force_wait_timeout) __hip_atomic_fetch_or(a.err, kErrFusedWait, __ATOMIC_RELAXED, AG);
     }
+    if (a.force_wait_timeout) return;   // (test hook: as a wait that timed out)
     int idle = 0;
     for (;;) {
         int v = 0;   // > 0: a claimed pair id + 1; 0: done; -1: wait; -2: lost a race, retry

@@ -137,6 +137,55 @@ def test_flat_record_nibble_packing():
         assert (got[(n + 1) // 2:] == 0xEE).all(), n   # nothing written past the record field
 
 
+def test_flat_record_compact_fields():
+    """Compact flat records (flat_plan.cpp, kernels.hpp kFmtRead1B /
+    kFmtHap2b): a read with no 'N' whose qualities (& 127) span < 64 goes as
+    ((q & 127) - qbase) << 2 | code per base (codes A0 C1 T2 G3, every other
+    byte 0 as ConvertChar), else it is refused; a hap with no 'N' as 2-bit
+    codes, 4 per byte (base k in bits 2(k % 4) of byte k / 4). Every byte value
+    and the lengths around the 32-byte vector step."""
+    import ctypes as C
+    L = hcphmm.lib()
+    L.hcx_pack_read_1b.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.POINTER(C.c_int)]
+    L.hcx_pack_hap_2b.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+    code = np.zeros(256, np.uint8)
+    for ch, v in ((b"C", 1), (b"T", 2), (b"G", 3), (b"N", 4)):
+        code[ch[0]] = v
+    rng = np.random.default_rng(1)
+    nonN = np.array([x for x in range(256) if x != ord("N")], np.uint8)
+    for n in list(range(1, 100)) + [127, 128, 129, 255, 256, 1000, 2049]:
+        b = rng.choice(nonN, n)
+        if n >= 255:
+            b[:255] = nonN
+        qb = int(rng.integers(0, 64))
+        q = (rng.integers(qb, qb + 64, n) | (rng.integers(0, 2, n) << 7)).astype(np.uint8)   # bit 7 ignored
+        got = np.full(n + 8, 0xEE, np.uint8)
+        qbase = C.c_int(-1)
+        assert L.hcx_pack_read_1b(q.ctypes.data, b.ctypes.data, n, got.ctypes.data, C.byref(qbase)) == 1, n
+        qm = (q & 127).astype(np.int32)
+        assert qbase.value == qm.min(), n
+        exp = (((qm - qm.min()) << 2) | (code[b] & 3)).astype(np.uint8)
+        assert np.array_equal(got[:n], exp), n
+        assert (got[n:] == 0xEE).all(), n
+        if n >= 2:   # refused: an 'N', or a quality span of 64
+            bN = b.copy()
+            bN[n // 2] = ord("N")
+            assert L.hcx_pack_read_1b(q.ctypes.data, bN.ctypes.data, n, got.ctypes.data, C.byref(qbase)) == 0
+            q2 = q.copy()
+            q2[0], q2[-1] = 10, 74
+            assert L.hcx_pack_read_1b(q2.ctypes.data, b.ctypes.data, n, got.ctypes.data, C.byref(qbase)) == 0
+        h = rng.choice(nonN, n)
+        got = np.full((n + 3) // 4 + 8, 0xEE, np.uint8)
+        assert L.hcx_pack_hap_2b(h.ctypes.data, n, got.ctypes.data) == 1, n
+        c = np.zeros((n + 3) // 4 * 4, np.uint8)
+        c[:n] = code[h] & 3
+        exp = (c[0::4] | (c[1::4] << 2) | (c[2::4] << 4) | (c[3::4] << 6)).astype(np.uint8)
+        assert np.array_equal(got[:(n + 3) // 4], exp), n
+        assert (got[(n + 3) // 4:] == 0xEE).all(), n
+        h[n - 1] = ord("N")
+        assert L.hcx_pack_hap_2b(h.ctypes.data, n, got.ctypes.data) == 0, n
+
+
 def test_init_rejects_unknown_flags(built):
     """hc_phmm_init flags: HC_PHMM_FLAG_F64 (initNative's use_double) and
     HC_PHMM_FLAG_KEEP_MODE; any other bit is refused before a device is

@@ -568,7 +568,7 @@ def test_seg_records_and_gather_with_mixed_kernels(engine, oracle_lib, monkeypat
     bt.close()
 
 
-@pytest.mark.parametrize("plan", ["static", "dynamic"])
+@pytest.mark.parametrize("plan", ["static", "dynamic", "fused"])
 def test_rescue_plan_timeout_is_an_error(engine, oracle_lib, monkeypatch, plan):
     """A fp64 workgroup that gives up waiting for the device-made rescue plan
     (lane_kernel.hip phmm_seg64_kernel, bounded wait) sets the part's device
@@ -577,19 +577,23 @@ def test_rescue_plan_timeout_is_an_error(engine, oracle_lib, monkeypatch, plan):
     non-planner workgroup time out at once: a static plan (S4-200: fewer waves
     than two per SIMD) and a dynamic one (thousands of long rescued pairs),
     through a flat call and a prepared batch; the batch then runs correctly
-    once the hook is off (the error word is cleared when reported)."""
+    once the hook is off (the error word is cleared when reported). fused:
+    S4-200 through the fused pass, where the hook makes every wave give up at
+    the rescue queue (a wait that timed out: kErrFusedWait); static: the same
+    pairs through the fp64 launch (HC_PHMM_FUSED=0)."""
     import hcphmm
-    if plan == "static":
+    monkeypatch.setenv("HC_PHMM_FUSED", "1" if plan == "fused" else "0")
+    if plan in ("static", "fused"):
         b = W.subset(W.config("S4"), np.arange(200))
     else:
         b = W.generate(4000, (1000, 1500), (150, 250), 0.08, seed=71)
     ref = oracle_lib.pairs(b, nthreads=16)
-    assert ref["rescued"].sum() > (100 if plan == "static" else 3000)
+    assert ref["rescued"].sum() > (3000 if plan == "dynamic" else 100)
     bt = engine.Batch(b)
     monkeypatch.setenv("HC_PHMM_TEST_PLAN_TIMEOUT", "1")
     with pytest.raises(hcphmm.PairHMMError) as e:
         engine.pairs(b)
-    assert e.value.code == hcphmm.EHIP and "rescue plan" in str(e.value)
+    assert e.value.code == hcphmm.EHIP and ("listed rescues" if plan == "fused" else "rescue plan") in str(e.value)
     bt.run()
     with pytest.raises(hcphmm.PairHMMError) as e:
         bt.results()
@@ -631,7 +635,7 @@ def test_mode_is_per_call_and_fixed_at_submit(engine, golden, golden_batch):
 
 
 @pytest.mark.parametrize("mode", ["auto", "forced", "off"])
-@pytest.mark.parametrize("shape", ["S4", "S4-300", "many-per-wave", "short-haps"])
+@pytest.mark.parametrize("shape", ["S4", "S4-300", "many-per-wave", "short-haps", "big-narrow"])
 def test_fused_pass(engine, oracle_lib, monkeypatch, shape, mode):
     """The fused pass (run.cpp, kernels.hpp LaneArgs::fz_*): a small part's
     waves list their rescues on a queue and drain it themselves, no fp64
@@ -639,17 +643,20 @@ def test_fused_pass(engine, oracle_lib, monkeypatch, shape, mode):
     off = the fp64 launch). configs[4] (S4, 2 000 pairs, 93 % rescued) and a
     subset; 8 000 pairs of 520-700 bases four to a wave, most rescued (a wave
     lists several, other waves take them); short haps (the solo path's domain
-    unless forced). Flat call and a prepared batch run three times (the queue
+    unless forced); a 60k-pair part of 300-500-base haps (the narrow form at
+    the fp32 pass's occupancy: more waves than slots, rescues taken once the
+    last wave is dispatched). Flat call and a prepared batch run three times (the queue
     counters go by run parity, the entries are zeroed by their consumers),
     against the oracle; the rescued count is the oracle's."""
     monkeypatch.setenv("HC_PHMM_FUSED", {"auto": "1", "forced": "2", "off": "0"}[mode])
     b = {"S4": lambda: W.config("S4"),
          "S4-300": lambda: W.subset(W.config("S4"), np.arange(300)),
          "many-per-wave": lambda: W.generate(8000, (520, 700), (60, 200), 0.08, seed=41),
-         "short-haps": lambda: W.generate(3000, (100, 500), (60, 200), 0.08, seed=23)}[shape]()
+         "short-haps": lambda: W.generate(3000, (100, 500), (60, 200), 0.08, seed=23),
+         "big-narrow": lambda: W.generate(60000, (300, 500), (60, 200), 0.035, seed=43)}[shape]()
     ref = oracle_lib.pairs(b, nthreads=16)
     n_resc = int(ref["rescued"].sum())
-    assert n_resc > len(b["R"]) // 3
+    assert n_resc > (500 if shape == "big-narrow" else len(b["R"]) // 3)
     assert_same(engine.pairs(b), ref, f"{shape}/{mode} flat")
     bt = engine.Batch(b)
     for k in range(3):
