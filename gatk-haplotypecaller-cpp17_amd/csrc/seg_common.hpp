@@ -196,13 +196,31 @@ __device__ __forceinline__ double from_left(double v)
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
-// v & mask bitwise (mask all ones or zero): one full-rate v_and per 32 bits.
-__device__ __forceinline__ float masked(float v, uint32_t m) { return __uint_as_float(__float_as_uint(v) & m); }
+// v & mask bitwise (mask all ones or zero, in a VGPR): one full-rate v_and per
+// 32 bits. (Written as C the compiler proves the mask boolean and selects with
+// v_cndmask on an SGPR lane mask instead, a half-rate form.)
+__device__ __forceinline__ uint32_t and_v(uint32_t a, uint32_t m)
+{
+    uint32_t r;
+    asm("v_and_b32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(m));
+    return r;
+}
+// AND: the v_and form (the mask lives in a VGPR: one register more, so only
+// where the block's registers leave room — the widest fp32 blocks spill with it).
+template <bool AND>
+__device__ __forceinline__ float masked(float v, uint32_t m)
+{
+    return __uint_as_float(AND ? and_v(__float_as_uint(v), m) : (__float_as_uint(v) & m));
+}
+template <bool AND>
 __device__ __forceinline__ double masked(double v, uint32_t m)
 {
     const unsigned long long x = (unsigned long long)__double_as_longlong(v);
-    return __longlong_as_double((long long)(x & ((unsigned long long)m << 32 | m)));
+    if (!AND) return __longlong_as_double((long long)(x & ((unsigned long long)m << 32 | m)));
+    return __longlong_as_double(
+        (long long)(((unsigned long long)and_v(uint32_t(x >> 32), m) << 32) | and_v(uint32_t(x), m)));
 }
+
 
 // Step bounds of a column-segmented wave (wave-uniform).
 struct SegSteps {
@@ -335,8 +353,9 @@ __device__ __forceinline__ void run_seg(const T* __restrict__ lut, const T* __re
     // T0 (row 0's diagonal) from its own initial t_hold on row 1. Inside a
     // group, lane s-1's initial t_out is T0: lane s's row-1 diagonal.
     const uint32_t keep = (s + 1) * BC < cx.H ? 0xffffffffu : 0u;
+    constexpr bool AND = BC * int(sizeof(T)) <= 128;   // masked's v_and form: fp32 up to 32 columns, fp64 16
     T y_out = T(0);                      // handed to lane s+1: Y past column c0+BC,
-    T t_out = masked(T0, keep);          //   T[BC-1] of the last row
+    T t_out = masked<AND>(T0, keep);     //   T[BC-1] of the last row
     T t_hold = c0 >= 0 ? T0 : T(0);      // lane s-1's right-edge T of the previous row (row 0: column c0's)
     // Running row sums (sumM, sumX): every lane adds its columns on every
     // sum-variant step and restarts from its left neighbour's at its last row
@@ -390,13 +409,16 @@ __device__ __forceinline__ void run_seg(const T* __restrict__ lut, const T* __re
             T Ml = T(0), Yl = Yl0;
             const T M0 = Tdiag * prior_of<31>(mrow.x, k.pm, k.px);
             cell<T, BC, 0, BC, SUM, EQ>(Tt, X, M0, Ml, Yl, mrow.x, mrow.y, k.pm, k.px, k, 0, sumM, sumX);
-            y_out = masked(y_next<EQ>(Ml, Yl, k.my, k.yy), keep);
-            t_out = masked(Tt[BC - 1], keep);
-            if constexpr (CG) {
-                k.pm = pm_n;
-                k.px = px_n;
-                mrow = m_n;
-            }
+            y_out = masked<AND>(y_next<EQ>(Ml, Yl, k.my, k.yy), keep);
+            t_out = masked<AND>(Tt[BC - 1], keep);
+        }
+        if constexpr (CG) {
+            // Unconditional (no register moves for a conditional update): a
+            // lane before its row 1 takes row i + 1's constants too, and at
+            // i = 0 those are row 1's, what it needs on its first row.
+            k.pm = pm_n;
+            k.px = px_n;
+            mrow = m_n;
         }
         wc = wn;
     };
