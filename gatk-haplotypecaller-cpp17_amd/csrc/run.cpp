@@ -290,7 +290,9 @@ int enqueue_results(Part* b, hipStream_t s)
 }
 
 // log10 finish (intel_pairhmm.hpp:137-143, glibc log10 / log10f as in the
-// reference) of a part's results, scattered into the caller's outputs.
+// reference) of a part's results, scattered into the caller's outputs. Chunks
+// of 2 048 pairs: a 415 x 128 region's 53 120 log10 calls spread over the
+// whole pool (in chunks of 8 192 they took 7 threads, ~0.07 ms).
 void finish_part(const Part& P, const float* f, const double* d, const uint8_t* fl, const Outputs& o)
 {
     const Luts& L = luts();
@@ -306,7 +308,7 @@ void finish_part(const Part& P, const float* f, const double* d, const uint8_t* 
                 if (o.raw64) o.raw64[id0 + k] = d[k];
                 if (o.resc) o.resc[id0 + k] = fl[k];
             }
-        }, 1 << 13);
+        }, 2048);
         return;
     }
     // Blocks: pair k of block b is (r, h) = divmod(k - base, nh).
@@ -329,7 +331,7 @@ void finish_part(const Part& P, const float* f, const double* d, const uint8_t* 
             }
             ++b;
         }
-    }, 1 << 13);
+    }, 2048);
 }
 
 }  // namespace eng

@@ -85,6 +85,15 @@ __device__ __forceinline__ void cell(T (&Tt)[BC], T (&X)[BC], T M, T& Ml, T& Yl,
         if constexpr (J + 1 < NC)
             Mn = Tt[J] * prior_of<31 - ((J + 1) & 31)>(((J + 1) >> 5) ? mw1 : mw0, pm, px);
         const T Xc = X[J];
+        if constexpr (SUM && !MASK) {
+            // The row sums first: they read M and the old X[J] before X[J] is
+            // rewritten (after it, the old value needed a copy per column).
+            // Every column of a block is a hap column or a zero padding column
+            // (run_seg), so the row's sums need no column mask; rows other than
+            // the pair's last accumulate values that run_seg discards.
+            sumM = sumM + M;
+            sumX = sumX + Xc;
+        }
         T Y;
         if constexpr (EQ) {
             const T Mx = M * k.mx;
@@ -102,12 +111,6 @@ __device__ __forceinline__ void cell(T (&Tt)[BC], T (&X)[BC], T M, T& Ml, T& Yl,
             const bool c = J < lim;   // column c0+J+1 <= H on the pair's last row
             sumM = sumM + (c ? M : T(0));
             sumX = sumX + (c ? Xc : T(0));
-        } else if constexpr (SUM) {
-            // Every column of a block is a hap column or a zero padding column
-            // (run_seg), so the row's sums need no column mask; rows other than
-            // the pair's last accumulate values that run_seg discards.
-            sumM = sumM + M;
-            sumX = sumX + Xc;
         }
         Yl = Y;
         cell<T, BC, J + 1, NC, SUM, EQ, MASK>(Tt, X, Mn, Ml, Yl, mw0, mw1, pm, px, k, lim, sumM, sumX);

@@ -10,7 +10,9 @@ for k, v in (d.get("secondary") or {}).items():
     keys = ("device_pass_ms", "device_pass_ms_cold", "kernel_ms_f32", "kernel_ms_f64", "frac_f32_kernel", "call_ms",
             "call_ms_cold", "gcups")
     f64 = (v.get("roofline_f64") or {}).get("frac")
-    print(f"  {k}: " + " ".join(f"{x}={v[x]}" for x in keys if x in v) + (f" f64frac={f64}" if f64 else ""))
+    rp = (v.get("roofline_pass") or {}).get("frac")
+    print(f"  {k}: " + " ".join(f"{x}={v[x]}" for x in keys if x in v) + (f" f64frac={f64}" if f64 else "")
+          + (f" passfrac={rp}" if rp else ""))
 for k in ("end_to_end_gcups", "end_to_end_ms", "end_to_end_first_call_ms"):
     if k in d:
         print(f"  {k}={d[k]}")
