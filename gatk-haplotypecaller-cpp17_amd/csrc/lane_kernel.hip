@@ -778,7 +778,7 @@ __global__ __launch_bounds__(256) void all_f64_list_kernel(int n, float* __restr
 // build at 4 waves per SIMD needs narrower blocks and measured 1-3 % slower,
 // profiles/r02_occ3_vs_occ4_caps.jsonl).
 constexpr int kSegOcc = 3;
-constexpr int kSeg64Occ = 2;   // fp64: 2 VGPRs per value
+constexpr int kSeg64Occ = 3;   // fp64: 2 VGPRs per value
 static const LaneVariant kVariants[] = {
     {1, 64, 3}, {1, 64, 2}, {1, 32, 4},
 };
