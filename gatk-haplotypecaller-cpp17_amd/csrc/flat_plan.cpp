@@ -222,92 +222,72 @@ namespace {
 
 // ---- compact record fields (kernels.hpp kFmtRead1B / kFmtHap2b)
 
-// A read fits one byte per base when no base is 'N' and its qualities (& 127)
-// span less than 64; qbase = their minimum.
-bool read_1b_scalar(const uint8_t* q, const uint8_t* b, int R, int& qbase)
+// The format pass 1 assumes for every pair (pass 2 checks it): compact read and
+// hap fields, or (HC_PHMM_FLAT_COMPACT=0, A/B) the nibble records.
+int assumed_fmt()
 {
-    int mn = 127, mx = 0;
-    bool n = false;
-    for (int k = 0; k < R; ++k) {
-        const int v = q[k] & 127;
-        mn = std::min(mn, v);
-        mx = std::max(mx, v);
-        n |= b[k] == 'N';
-    }
-    qbase = mn;
-    return !n && mx - mn < 64;
+    static const int f = std::getenv("HC_PHMM_FLAT_COMPACT") && std::getenv("HC_PHMM_FLAT_COMPACT")[0] == '0'
+                             ? 0
+                             : (kFmtRead1B | kFmtHap2b);
+    return f;
 }
 
-__attribute__((target("avx2"))) inline void read_1b_step(const uint8_t* q, const uint8_t* b, __m256i& vmn,
-                                                          __m256i& vmx, __m256i& vn)
-{
-    const __m256i v = _mm256_and_si256(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(q)), _mm256_set1_epi8(0x7f));
-    vmn = _mm256_min_epu8(vmn, v);
-    vmx = _mm256_max_epu8(vmx, v);
-    vn = _mm256_or_si256(vn, _mm256_cmpeq_epi8(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(b)),
-                                               _mm256_set1_epi8('N')));
-}
+// A read fits one byte per base, ((q & 127) - 33) << 2 | code, when no base
+// is 'N' and every quality (& 127) is in [33, 97): SAM's ASCII qualities
+// (Phred 0-63 + 33) always are. The quality base is the fixed 33 so the
+// check and the packing are one pass (kernels.hpp kFmtRead1B: qbase in the
+// descriptor).
+constexpr int kQBase = 33;
 
-__attribute__((target("avx2"))) bool read_1b_avx2(const uint8_t* q, const uint8_t* b, int R, int& qbase)
-{
-    if (R < 32) return read_1b_scalar(q, b, R, qbase);
-    __m256i vmn = _mm256_set1_epi8(0x7f), vmx = _mm256_setzero_si256(), vn = _mm256_setzero_si256();
-    int k = 0;
-    for (; k + 32 <= R; k += 32) read_1b_step(q + k, b + k, vmn, vmx, vn);
-    if (k < R) read_1b_step(q + R - 32, b + R - 32, vmn, vmx, vn);   // overlapping: min / max / any are idempotent
-    alignas(32) uint8_t mn[32], mx[32];
-    _mm256_store_si256(reinterpret_cast<__m256i*>(mn), vmn);
-    _mm256_store_si256(reinterpret_cast<__m256i*>(mx), vmx);
-    int a = 127, z = 0;
-    for (int j = 0; j < 32; ++j) {
-        a = std::min(a, int(mn[j]));
-        z = std::max(z, int(mx[j]));
-    }
-    qbase = a;
-    return _mm256_testz_si256(vn, vn) && z - a < 64;
-}
-
-bool read_1b(const uint8_t* q, const uint8_t* b, int R, int& qbase)
-{
-    return has_avx2() ? read_1b_avx2(q, b, R, qbase) : read_1b_scalar(q, b, R, qbase);
-}
-
-// d[k] = ((q[k] & 127) - qbase) << 2 | code(b[k]) (codes A0 C1 T2 G3, others 0;
-// no 'N' here).
-void pack_read_1b_scalar(const uint8_t* q, const uint8_t* b, int R, int qbase, uint8_t* d)
+bool read_1b_scalar(const uint8_t* q, const uint8_t* b, int R, uint8_t* d)
 {
     const auto& ct = code_table();
-    for (int k = 0; k < R; ++k) d[k] = uint8_t((((q[k] & 127) - qbase) << 2) | (ct[b[k]] & 3));
+    bool ok = true;
+    for (int k = 0; k < R; ++k) {
+        const int v = (q[k] & 127) - kQBase;
+        ok &= unsigned(v) < 64u && b[k] != 'N';
+        if (d) d[k] = uint8_t((v << 2) | (ct[b[k]] & 3));
+    }
+    return ok;
 }
 
-__attribute__((target("avx2"))) inline __m256i read_1b32(const uint8_t* q, const uint8_t* b, __m256i vqb)
+// 32 bases: the packed bytes, and the running "bad" accumulator (a delta past
+// 63 — qualities below 33 wrap — or an 'N').
+__attribute__((target("avx2"))) inline __m256i read_1b32(const uint8_t* q, const uint8_t* b, __m256i& vmax, __m256i& vn)
 {
     const __m256i v = _mm256_sub_epi8(
-        _mm256_and_si256(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(q)), _mm256_set1_epi8(0x7f)), vqb);
-    // v < 64: the 16-bit shift carries only zero bits across bytes
-    return _mm256_or_si256(_mm256_slli_epi16(v, 2),
-                           codes32(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(b))));
+        _mm256_and_si256(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(q)), _mm256_set1_epi8(0x7f)),
+        _mm256_set1_epi8(char(kQBase)));
+    const __m256i bb = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(b));
+    vmax = _mm256_max_epu8(vmax, v);
+    vn = _mm256_or_si256(vn, _mm256_cmpeq_epi8(bb, _mm256_set1_epi8('N')));
+    // v < 64 where it matters (else the read is refused): the 16-bit shift
+    // carries only zero bits across bytes
+    return _mm256_or_si256(_mm256_slli_epi16(v, 2), codes32(bb));
 }
 
-__attribute__((target("avx2"))) void pack_read_1b_avx2(const uint8_t* q, const uint8_t* b, int R, int qbase,
-                                                       uint8_t* d)
+__attribute__((target("avx2"))) bool read_1b_avx2(const uint8_t* q, const uint8_t* b, int R, uint8_t* d)
 {
-    if (R < 32) {
-        pack_read_1b_scalar(q, b, R, qbase, d);
-        return;
-    }
-    const __m256i vqb = _mm256_set1_epi8(char(qbase));
+    if (R < 32) return read_1b_scalar(q, b, R, d);
+    __m256i vmax = _mm256_setzero_si256(), vn = _mm256_setzero_si256();
     int k = 0;
-    for (; k + 32 <= R; k += 32) _mm256_storeu_si256(reinterpret_cast<__m256i*>(d + k), read_1b32(q + k, b + k, vqb));
-    if (k < R) _mm256_storeu_si256(reinterpret_cast<__m256i*>(d + R - 32), read_1b32(q + R - 32, b + R - 32, vqb));
+    for (; k + 32 <= R; k += 32) {
+        const __m256i x = read_1b32(q + k, b + k, vmax, vn);
+        if (d) _mm256_storeu_si256(reinterpret_cast<__m256i*>(d + k), x);
+    }
+    if (k < R) {   // the last 32 overlapping what is written (same values)
+        const __m256i x = read_1b32(q + R - 32, b + R - 32, vmax, vn);
+        if (d) _mm256_storeu_si256(reinterpret_cast<__m256i*>(d + R - 32), x);
+    }
+    // every delta < 64: no byte of vmax has bit 6 or 7 set
+    const __m256i hi = _mm256_and_si256(vmax, _mm256_set1_epi8(char(0xc0)));
+    return _mm256_testz_si256(hi, hi) && _mm256_testz_si256(vn, vn);
 }
 
-void pack_read_1b(const uint8_t* q, const uint8_t* b, int R, int qbase, uint8_t* d)
+// Pack the read (d may be null: check only); false if it does not fit.
+bool read_1b(const uint8_t* q, const uint8_t* b, int R, uint8_t* d)
 {
-    if (has_avx2())
-        pack_read_1b_avx2(q, b, R, qbase, d);
-    else
-        pack_read_1b_scalar(q, b, R, qbase, d);
+    return has_avx2() ? read_1b_avx2(q, b, R, d) : read_1b_scalar(q, b, R, d);
 }
 
 // Hap codes 2 bits each (a hap with no 'N'): false if it has one.
@@ -359,8 +339,7 @@ bool has_n(const uint8_t* s, int n) { return std::memchr(s, 'N', size_t(n)) != n
 }  // namespace
 
 // (test hooks below)
-bool read_1b_hook(const uint8_t* q, const uint8_t* b, int R, int& qbase) { return read_1b(q, b, R, qbase); }
-void pack_read_1b_hook(const uint8_t* q, const uint8_t* b, int R, int qbase, uint8_t* d) { pack_read_1b(q, b, R, qbase, d); }
+bool read_1b_hook(const uint8_t* q, const uint8_t* b, int R, uint8_t* d) { return read_1b(q, b, R, d); }
 bool pack_hap_2b_hook(const uint8_t* s, int n, uint8_t* d) { return pack_hap_2b(s, n, d); }
 
 namespace {
@@ -394,18 +373,17 @@ void fill_chunk(const Src& src, int64_t lo, int64_t n, int64_t m0, int64_t m1, c
                         return;
                     }
                     g = int32_t((ip[0] & 127) | ((dp[0] & 127) << 7) | ((cp[0] & 127) << 14));
-                    fmt = kFmtRead1B | kFmtHap2b;
+                    fmt = assumed_fmt();
                 }
                 const int qa = align4(R);
                 uint8_t* d = reinterpret_cast<uint8_t*>(buf + (ro - r0));
                 size_t at = size_t(qa);
-                int qbase = 0;
+                const int qbase = (fmt & kFmtRead1B) ? kQBase : 0;
                 if (fmt & kFmtRead1B) {
-                    if (!read_1b(src.q + o, src.rs + o, R, qbase)) {
+                    if (!read_1b(src.q + o, src.rs + o, R, d)) {
                         varying.store(true, std::memory_order_relaxed);   // (scan mode never lists such a read)
                         return;
                     }
-                    pack_read_1b(src.q + o, src.rs + o, R, qbase, d);
                 } else {
                     copy_bytes(src.q + o, R, d);
                     pack_nibbles(src.rs + o, R, d + qa);
@@ -454,7 +432,7 @@ void scan_pass(const Src& src, int64_t lo, int64_t n, bool scan_gaps, Mini* mini
                     continue;
                 }
                 int32_t g = 0;
-                int fmt = kFmtRead1B | kFmtHap2b;   // assumed (checked by pass 2) unless scanning
+                int fmt = assumed_fmt();   // assumed (checked by pass 2) unless scanning
                 if (scan_gaps) {
                     const int64_t o = src.read_off[p];
                     const uint8_t *ip = src.ins + o, *dp = src.del + o, *cp = src.gcp + o;
@@ -462,9 +440,9 @@ void scan_pass(const Src& src, int64_t lo, int64_t n, bool scan_gaps, Mini* mini
                             ? int32_t((ip[0] & 127) | ((dp[0] & 127) << 7) | ((cp[0] & 127) << 14))
                             : -1;
                     gapw[k] = g;
-                    int qb;
-                    fmt = (read_1b(src.q + o, src.rs + o, R, qb) ? kFmtRead1B : 0) |
-                          (has_n(src.hap + src.hap_off[p], H) ? 0 : kFmtHap2b);
+                    fmt = assumed_fmt() == 0 ? 0
+                                             : (read_1b(src.q + o, src.rs + o, R, nullptr) ? kFmtRead1B : 0) |
+                                                   (has_n(src.hap + src.hap_off[p], H) ? 0 : kFmtHap2b);
                     fmtw[k] = uint8_t(fmt);
                 }
                 M.rec += record_bytes(R, H, g < 0, fmt);
@@ -847,14 +825,10 @@ int plan_flat_device(Device& dv, const Src& src, const PartSpec& spec, Slot* slo
 // Host-logic test hook (not part of the ABI): the record's nibble packing.
 extern "C" void hcx_pack_nibbles(const uint8_t* s, int n, uint8_t* d) { hcphmm::eng::pack_nibbles(s, n, d); }
 // Host-logic test hooks (not part of the ABI): the compact record fields.
-// Returns 1 (and writes d, *qbase) if the read fits one byte per base, else 0.
-extern "C" int hcx_pack_read_1b(const uint8_t* q, const uint8_t* b, int n, uint8_t* d, int* qbase)
+// Returns 1 if the read fits one byte per base (d holds it), else 0.
+extern "C" int hcx_pack_read_1b(const uint8_t* q, const uint8_t* b, int n, uint8_t* d)
 {
-    int qb = 0;
-    if (!hcphmm::eng::read_1b_hook(q, b, n, qb)) return 0;
-    hcphmm::eng::pack_read_1b_hook(q, b, n, qb, d);
-    *qbase = qb;
-    return 1;
+    return hcphmm::eng::read_1b_hook(q, b, n, d) ? 1 : 0;
 }
 // Returns 1 if the hap has no 'N' (d holds its 2-bit codes), else 0.
 extern "C" int hcx_pack_hap_2b(const uint8_t* s, int n, uint8_t* d) { return hcphmm::eng::pack_hap_2b_hook(s, n, d) ? 1 : 0; }

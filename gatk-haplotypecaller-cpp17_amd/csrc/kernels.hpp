@@ -64,10 +64,9 @@ constexpr int kStealCount = 9;    // [9, 10] stealable rescue list length, by pa
 constexpr int kErrWord = 12;
 constexpr int kErrPlanWait = 1;   // fp64 pass: a workgroup gave up waiting for the rescue plan
 constexpr int kErrFusedWait = 2;  // fused pass: a wave gave up waiting for a listed rescue's entry
-// [16..21] the fused pass's rescue queue (LaneArgs::fz_*), by run parity:
-// waves started, waves done with their fp32 pairs, queue head.
+// [16..17], [20..21] the fused pass's rescue queue (LaneArgs::fz_*), by run
+// parity: waves started, queue head.
 constexpr int kFusedStarted = 16;
-constexpr int kFusedDone = 18;
 constexpr int kFusedHead = 20;
 constexpr int kSegHeads = 24;
 constexpr int kSegQueues = 9;          // 8 XCD queues + the tail queue
@@ -226,17 +225,13 @@ struct LaneArgs {
     // null = off (every deferred rescue to rescue_list).
     int* steal_list;
     int* steal_count;
-    // Fused pass (phmm_seg_kernel<kFusedOcc, true>; run.cpp: small parts of
-    // seg pairs with H <= kSeg64MaxH, every wave resident at once): no fp64
-    // launch. A wave appends its flagged pairs to rescue_list (pid + 1; the
-    // entries are zero before the run and the consumer zeroes them again),
-    // counts itself done, then takes listed rescues from the queue head and
-    // recomputes each in fp64 over its 64 lanes (seg_common.hpp
-    // fused_rescues). It waits for more only while every wave of the launch
-    // has started and some are still in their fp32 pairs, so a waiting wave
-    // never holds a slot an undispatched wave needs. null = off.
+    // Fused pass (phmm_seg_kernel<OCC, true, MAXWI>; run.cpp): no fp64 launch.
+    // A wave appends its flagged pairs to rescue_list (pid + 1; the entries
+    // are zero before the run and the consumer zeroes them again), then, once
+    // every wave of the launch has started (fz_started), takes listed rescues
+    // from the queue head and recomputes each in fp64 over its 64 lanes until
+    // none is listed (seg_common.hpp fused_rescues). null = off.
     int* fz_started;      // launches the fused form of phmm_seg_kernel when set
-    int* fz_done;
     int* fz_head;
     int fz_wide;          // 1: fp64 blocks up to 32 columns (H <= kSeg64MaxH) at kFusedOcc waves per
                           // SIMD; 0: 8 columns (H <= kInWaveRescueMaxH) at the fp32 pass's 3

@@ -475,6 +475,7 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
         // pair id + 1: a zero entry is one whose store has not landed yet
         if (resc) __hip_atomic_store(a.rescue_list + atomicAdd(a.rescue_count, 1), pid + 1, __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // the entries before this wave's claims
     } else {
         const uint64_t todo = __builtin_amdgcn_ballot_w64(resc);
         if (todo) rescue_in_wave(a, todo, pid, slot, cx.H, lane, mt);
@@ -543,7 +544,6 @@ __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
         c[kPlanReady + o] = 0;
         c[kStealCount + o] = 0;
         c[kFusedStarted + o] = 0;
-        c[kFusedDone + o] = 0;
         c[kFusedHead + o] = 0;
     }
     if (wid >= n_waves) return;   // wave-uniform (device-planned parts launch an upper bound)
@@ -778,7 +778,7 @@ __global__ __launch_bounds__(256) void all_f64_list_kernel(int n, float* __restr
 // build at 4 waves per SIMD needs narrower blocks and measured 1-3 % slower,
 // profiles/r02_occ3_vs_occ4_caps.jsonl).
 constexpr int kSegOcc = 3;
-constexpr int kSeg64Occ = 3;   // fp64: 2 VGPRs per value
+constexpr int kSeg64Occ = 2;   // fp64: 2 VGPRs per value
 static const LaneVariant kVariants[] = {
     {1, 64, 3}, {1, 64, 2}, {1, 32, 4},
 };

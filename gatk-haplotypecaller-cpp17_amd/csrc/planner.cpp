@@ -1111,22 +1111,41 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             // [o_rd, o_ord): read / hap descriptors; the order and waves between
             // are built on the device; then the read / hap bytes and the block
             // and segment tables. One fused launch prepares everything.
-            HIP_TRY(hipMemcpyAsync(dev + up0, host + up0, up_mid - up0, hipMemcpyHostToDevice, s));
-            HIP_TRY(hipMemcpyAsync(dev + o_bases, host + o_bases, o_lw - o_bases, hipMemcpyHostToDevice, s));
-            HIP_TRY(hipMemcpyAsync(dev + o_gb, host + o_gb, upload - o_gb, hipMemcpyHostToDevice, s));
+            // Zero copy (a part whose upload is at most HC_PHMM_ZERO_COPY_MAX
+            // bytes, default 4 MiB: one region): the prep launch reads the
+            // pinned staging image itself over PCIe — it is the only reader of
+            // those bytes — instead of three DMA copies ahead of it.
+            char* src = dev;
+            const int64_t up_bytes = int64_t(up_mid - up0) + int64_t(o_lw - o_bases) + int64_t(upload - o_gb);
+            if (slot && up_bytes <= env_i64("HC_PHMM_ZERO_COPY_MAX", int64_t(4) << 20)) {
+                void* hp = nullptr;
+                if (hipHostGetDevicePointer(&hp, host, 0) == hipSuccess && hp) src = static_cast<char*>(hp);
+            }
+            if (src == dev) {
+                HIP_TRY(hipMemcpyAsync(dev + up0, host + up0, up_mid - up0, hipMemcpyHostToDevice, s));
+                HIP_TRY(hipMemcpyAsync(dev + o_bases, host + o_bases, o_lw - o_bases, hipMemcpyHostToDevice, s));
+                HIP_TRY(hipMemcpyAsync(dev + o_gb, host + o_gb, upload - o_gb, hipMemcpyHostToDevice, s));
+            } else {
+                pack.bases = reinterpret_cast<const uint8_t*>(src + o_bases);
+                pack.quals = reinterpret_cast<const uint8_t*>(src + o_quals);
+                pack.gaps = reinterpret_cast<const uint8_t*>(src + o_gaps);
+                pack.rdesc = reinterpret_cast<const int4*>(src + o_rd);
+                pack.hap_bytes = reinterpret_cast<const uint8_t*>(src + o_hb);
+                pack.hdesc = reinterpret_cast<const int4*>(src + o_hd);
+            }
             HIP_TRY(hipEventRecord(b->pack_ev[0], s));
             GridPrepArgs g{};
             g.pack = pack;
-            g.blocks = reinterpret_cast<const GridBlock*>(dev + o_gb);
+            g.blocks = reinterpret_cast<const GridBlock*>(src + o_gb);
             g.nblocks = int(spec.blocks.size());
             g.npairs = (long long)npairs;
             g.pairs = b->d_pairs;
-            g.segs = reinterpret_cast<const GridSeg*>(dev + o_gs);
+            g.segs = reinterpret_cast<const GridSeg*>(src + o_gs);
             g.nsegs = int(gd.segs.size());
             g.nslots = (long long)n_seg_slots;
             g.nwaves = n_seg_waves;
-            g.rord = reinterpret_cast<const int*>(dev + o_gr);
-            g.hord = reinterpret_cast<const int*>(dev + o_gh);
+            g.rord = reinterpret_cast<const int*>(src + o_gr);
+            g.hord = reinterpret_cast<const int*>(src + o_gh);
             g.order = reinterpret_cast<int*>(dev + o_ord);
             g.slot_of = b->d_slot_of;
             g.sdesc = b->d_sdesc;

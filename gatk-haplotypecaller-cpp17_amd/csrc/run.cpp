@@ -180,7 +180,6 @@ int run_part(Part* b, hipStream_t s)
                 g.solo_counters = b->d_count;
                 g.solo_other = par ^ 1;
                 g.fz_started = b->d_count + kFusedStarted + par;
-                g.fz_done = b->d_count + kFusedDone + par;
                 g.fz_head = b->d_count + kFusedHead + par;
                 g.err = b->d_count + kErrWord;
                 g.prio64 = r.prio;

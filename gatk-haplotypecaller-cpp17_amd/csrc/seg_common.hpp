@@ -598,30 +598,33 @@ __device__ __forceinline__ void steal_rescues(const LaneArgs& a, int wid, int la
 }
 
 // The fused pass's rescue queue (LaneArgs::fz_*): this wave has appended its
-// flagged pairs; it counts itself done (after a release, so the entries are
-// visible first), then takes listed rescues from the head, oldest first, each
+// flagged pairs; once every one of the launch's nw waves has been dispatched
+// (before that, a wave that stays for rescues holds a slot an undispatched
+// fp32 wave needs), it takes listed rescues from the head, oldest first, each
 // recomputed in fp64 over its 64 lanes (rescue_one: the rescue of
-// intel_pairhmm.hpp:137-139, as the fp64 launch would). With nothing listed it
-// waits only while every one of the launch's nw waves has started and some are
-// still in their fp32 pairs (they may still list rescues): a waiting wave never
-// holds a slot an undispatched wave needs, and the waves it waits for are
-// running. Claims go by compare-and-swap on the head, never past the count, so
-// no wave holds a claim nobody will fill. Both waits are bounded; giving up
+// intel_pairhmm.hpp:137-139, as the fp64 launch would), until none is listed.
+// No wave ever waits for more: a wave that lists a rescue checks the queue
+// after listing it, so every listed pair is taken by its own wave if by no
+// other (the last waves' rescues run in those waves). Claims go by
+// compare-and-swap on the head, never past the count. (A first form let idle
+// waves poll for rescues until every wave had finished its fp32 pairs: the
+// thousands of polling waves' atomics on the same lines slowed the pass 2-30x.)
+// The one wait, for a claimed entry's store to land, is bounded; giving up
 // sets the part's error word (the host fails the call).
-constexpr int kFusedWaitIters = 1 << 24;
+constexpr int kFusedWaitIters = 1 << 20;
 template <int MAXWI>
 __device__ __forceinline__ void fused_rescues(const LaneArgs& a, int nw, int lane, uint2* __restrict__ mt)
 {
     constexpr auto AG = __HIP_MEMORY_SCOPE_AGENT;
-    if (lane == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_fetch_add(a.fz_done, 1, __ATOMIC_RELAXED, AG);
-        if (a.force_wait_timeout) __hip_atomic_fetch_or(a.err, kErrFusedWait, __ATOMIC_RELAXED, AG);
+    if (a.force_wait_timeout) {   // (test hook: as a wait that timed out)
+        if (lane == 0) __hip_atomic_fetch_or(a.err, kErrFusedWait, __ATOMIC_RELAXED, AG);
+        return;
     }
-    if (a.force_wait_timeout) return;   // (test hook: as a wait that timed out)
-    int idle = 0;
+    int go = 0;
+    if (lane == 0) go = __hip_atomic_load(a.fz_started, __ATOMIC_RELAXED, AG) >= nw;
+    if (!__builtin_amdgcn_readfirstlane(go)) return;
     for (;;) {
-        int v = 0;   // > 0: a claimed pair id + 1; 0: done; -1: wait; -2: lost a race, retry
+        int v = 0;   // > 0: a claimed pair id + 1; 0: nothing listed; -2: lost a race, retry
         if (lane == 0) {
             const int h = __hip_atomic_load(a.fz_head, __ATOMIC_RELAXED, AG);
             const int c = __hip_atomic_load(a.rescue_count, __ATOMIC_RELAXED, AG);
@@ -633,7 +636,7 @@ __device__ __forceinline__ void fused_rescues(const LaneArgs& a, int nw, int lan
                     for (int it = 0; it < kFusedWaitIters; ++it) {
                         e = __hip_atomic_load(a.rescue_list + h, __ATOMIC_RELAXED, AG);
                         if (e != 0) break;
-                        __builtin_amdgcn_s_sleep(1);
+                        __builtin_amdgcn_s_sleep(2);
                     }
                     if (e == 0) __hip_atomic_fetch_or(a.err, kErrFusedWait, __ATOMIC_RELAXED, AG);
                     else __hip_atomic_store(a.rescue_list + h, 0, __ATOMIC_RELAXED, AG);   // clean for the next run
@@ -641,24 +644,11 @@ __device__ __forceinline__ void fused_rescues(const LaneArgs& a, int nw, int lan
                 } else {
                     v = -2;
                 }
-            } else {
-                const int st = __hip_atomic_load(a.fz_started, __ATOMIC_RELAXED, AG);
-                const int dn = __hip_atomic_load(a.fz_done, __ATOMIC_ACQUIRE, AG);
-                v = (st >= nw && dn < nw) ? -1 : 0;
             }
         }
         v = __builtin_amdgcn_readfirstlane(v);
         if (v == 0) return;
         if (v == -2) continue;
-        if (v == -1) {
-            if (++idle >= kFusedWaitIters) {
-                if (lane == 0) __hip_atomic_fetch_or(a.err, kErrFusedWait, __ATOMIC_RELAXED, AG);
-                return;
-            }
-            __builtin_amdgcn_s_sleep(2);
-            continue;
-        }
-        idle = 0;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         rescue_one<MAXWI>(a, a.pairs[v - 1], v - 1, -1, lane, mt);
     }

@@ -139,14 +139,14 @@ def test_flat_record_nibble_packing():
 
 def test_flat_record_compact_fields():
     """Compact flat records (flat_plan.cpp, kernels.hpp kFmtRead1B /
-    kFmtHap2b): a read with no 'N' whose qualities (& 127) span < 64 goes as
-    ((q & 127) - qbase) << 2 | code per base (codes A0 C1 T2 G3, every other
-    byte 0 as ConvertChar), else it is refused; a hap with no 'N' as 2-bit
-    codes, 4 per byte (base k in bits 2(k % 4) of byte k / 4). Every byte value
-    and the lengths around the 32-byte vector step."""
+    kFmtHap2b): a read with no 'N' whose qualities (& 127) lie in [33, 97)
+    goes as ((q & 127) - 33) << 2 | code per base (codes A0 C1 T2 G3, every
+    other byte 0 as ConvertChar), else it is refused; a hap with no 'N' as
+    2-bit codes, 4 per byte (base k in bits 2(k % 4) of byte k / 4). Every
+    byte value and the lengths around the 32-byte vector step."""
     import ctypes as C
     L = hcphmm.lib()
-    L.hcx_pack_read_1b.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.POINTER(C.c_int)]
+    L.hcx_pack_read_1b.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
     L.hcx_pack_hap_2b.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
     code = np.zeros(256, np.uint8)
     for ch, v in ((b"C", 1), (b"T", 2), (b"G", 3), (b"N", 4)):
@@ -157,23 +157,21 @@ def test_flat_record_compact_fields():
         b = rng.choice(nonN, n)
         if n >= 255:
             b[:255] = nonN
-        qb = int(rng.integers(0, 64))
-        q = (rng.integers(qb, qb + 64, n) | (rng.integers(0, 2, n) << 7)).astype(np.uint8)   # bit 7 ignored
+        q = (rng.integers(33, 97, n) | (rng.integers(0, 2, n) << 7)).astype(np.uint8)   # bit 7 ignored
         got = np.full(n + 8, 0xEE, np.uint8)
-        qbase = C.c_int(-1)
-        assert L.hcx_pack_read_1b(q.ctypes.data, b.ctypes.data, n, got.ctypes.data, C.byref(qbase)) == 1, n
+        assert L.hcx_pack_read_1b(q.ctypes.data, b.ctypes.data, n, got.ctypes.data) == 1, n
         qm = (q & 127).astype(np.int32)
-        assert qbase.value == qm.min(), n
-        exp = (((qm - qm.min()) << 2) | (code[b] & 3)).astype(np.uint8)
+        exp = (((qm - 33) << 2) | (code[b] & 3)).astype(np.uint8)
         assert np.array_equal(got[:n], exp), n
         assert (got[n:] == 0xEE).all(), n
-        if n >= 2:   # refused: an 'N', or a quality span of 64
-            bN = b.copy()
-            bN[n // 2] = ord("N")
-            assert L.hcx_pack_read_1b(q.ctypes.data, bN.ctypes.data, n, got.ctypes.data, C.byref(qbase)) == 0
+        assert L.hcx_pack_read_1b(q.ctypes.data, b.ctypes.data, n, None) == 1, n   # check only
+        bN = b.copy()   # refused: an 'N', a quality below 33 or from 97 on
+        bN[n // 2] = ord("N")
+        assert L.hcx_pack_read_1b(q.ctypes.data, bN.ctypes.data, n, got.ctypes.data) == 0
+        for bad in (32, 97, 127, 0):
             q2 = q.copy()
-            q2[0], q2[-1] = 10, 74
-            assert L.hcx_pack_read_1b(q2.ctypes.data, b.ctypes.data, n, got.ctypes.data, C.byref(qbase)) == 0
+            q2[n - 1] = bad
+            assert L.hcx_pack_read_1b(q2.ctypes.data, b.ctypes.data, n, None) == 0, (n, bad)
         h = rng.choice(nonN, n)
         got = np.full((n + 3) // 4 + 8, 0xEE, np.uint8)
         assert L.hcx_pack_hap_2b(h.ctypes.data, n, got.ctypes.data) == 1, n
