@@ -473,9 +473,13 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
     }
     if constexpr (FUSED) {
         // pair id + 1: a zero entry is one whose store has not landed yet
+        // (No fence: the entry is an agent-scope atomic store, polled by its
+        // consumer with atomic loads; everything else the consumer reads was
+        // written by earlier launches. A release fence here — buffer_wbl2, a
+        // write-back of the XCD's whole L2 — in every wave made the 415 x 128
+        // region's pass 5x slower.)
         if (resc) __hip_atomic_store(a.rescue_list + atomicAdd(a.rescue_count, 1), pid + 1, __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // the entries before this wave's claims
     } else {
         const uint64_t todo = __builtin_amdgcn_ballot_w64(resc);
         if (todo) rescue_in_wave(a, todo, pid, slot, cx.H, lane, mt);

@@ -649,8 +649,7 @@ __device__ __forceinline__ void fused_rescues(const LaneArgs& a, int nw, int lan
         v = __builtin_amdgcn_readfirstlane(v);
         if (v == 0) return;
         if (v == -2) continue;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        rescue_one<MAXWI>(a, a.pairs[v - 1], v - 1, -1, lane, mt);
+        rescue_one<MAXWI>(a, a.pairs[v - 1], v - 1, -1, lane, mt);   // inputs from earlier launches: no acquire
     }
 }
 
