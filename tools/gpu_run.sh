@@ -16,7 +16,8 @@
 #   ab:WL:PAIRS:VARIANTS      tools/persist_ab.sh with NO_R3=1; PAIRS comma-separated, VARIANTS
 #                             "tag@ENV=V,ENV=V/tag2@ENV=V" (e.g. ab:S4:2000,20000:on@HC_PHMM_X=1/off@HC_PHMM_X=0)
 #   region:VARIANTS           tools/region_ab.py 128 VARIANTS (e.g. HC_PHMM_X=0,1)
-#   py:SCRIPT[,ARGS]          python3 tools/SCRIPT ARGS
+#   timeline[:NH]             the region call's host phases and device timeline (tools/call_timeline.py)
+#   py:SCRIPT[,ARGS]         python3 tools/SCRIPT ARGS ("py:SCRIPT A=1,2 B=3" when ARGS hold commas)
 # A/B libraries: ab_libs/ is not pushed to the box (.gpurunignore); copy the
 # builds an A/B run needs into ab_stage/ first and name them there.
 set -o pipefail
@@ -59,8 +60,19 @@ for step in "$@"; do
     region)
       timeout -k 10 300 python3 tools/region_ab.py 128 $arg
       rc=$? ;;
+    timeline)
+      # Region call breakdown: host phases (HC_PHMM_TRACE) and the device
+      # timeline of the last calls (kernels + copies) for NH haplotypes.
+      nh=${arg:-128}
+      HC_PHMM_TRACE=1 timeout -k 10 120 python3 tools/region_trace.py $nh > $OUT/region_trace_$nh.log 2>&1 &&
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/tl_$nh -o run \
+          -- python3 tools/region_prof.py $nh > $OUT/tl_$nh.log 2>&1 &&
+      python3 tools/call_timeline.py $OUT/tl_$nh --calls 3 > $OUT/call_timeline_$nh.txt
+      rc=$?; tail -25 $OUT/call_timeline_$nh.txt 2>/dev/null ;;
     py)
-      timeout -k 10 600 python3 tools/${arg//,/ }
+      # Spaces in ARGS: taken as they are (commas kept); otherwise commas for spaces.
+      case "$arg" in *" "*) a=$arg ;; *) a=${arg//,/ } ;; esac
+      timeout -k 10 600 python3 tools/$a
       rc=$? ;;
     *) echo "unknown step $name"; rc=2 ;;
   esac
