@@ -472,14 +472,15 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
         }
     }
     if constexpr (FUSED) {
-        // pair id + 1: a zero entry is one whose store has not landed yet
-        // (No fence: the entry is an agent-scope atomic store, polled by its
-        // consumer with atomic loads; everything else the consumer reads was
-        // written by earlier launches. A release fence here — buffer_wbl2, a
-        // write-back of the XCD's whole L2 — in every wave made the 415 x 128
-        // region's pass 5x slower.)
-        if (resc) __hip_atomic_store(a.rescue_list + atomicAdd(a.rescue_count, 1), pid + 1, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
+        // pair id + 1 (a zero entry: not yet published), published by an
+        // atomic swap: an atomic is performed past the XCD's L2, where a wave
+        // of another XCD sees it. (A plain or relaxed atomic store stays in
+        // this XCD's L2 until the line is evicted: claimants on the other
+        // seven XCDs waited milliseconds for it, 2.6-3.9 ms per rescue in
+        // tools/timeline.py; a release fence instead — buffer_wbl2, a
+        // write-back of the whole L2 — in every wave made the pass 5x slower.)
+        if (resc) (void)__hip_atomic_exchange(a.rescue_list + atomicAdd(a.rescue_count, 1), pid + 1,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
         const uint64_t todo = __builtin_amdgcn_ballot_w64(resc);
         if (todo) rescue_in_wave(a, todo, pid, slot, cx.H, lane, mt);
@@ -494,7 +495,11 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
     }
     if constexpr (FUSED) {
         __builtin_amdgcn_wave_barrier();   // the rescues below rewrite mt
-        fused_rescues<MAXWI>(a, nw, lane, mt);
+        const int nres = fused_rescues<MAXWI>(a, nw, lane, mt);
+        if (a.timeline && lane == 0) {   // fused: (time in rescues << 16) | rescues taken (0xffff: not started)
+            const unsigned long long t_fin = __builtin_amdgcn_s_memrealtime();
+            a.timeline[3 * size_t(wid) + 2] = ((t_fin - a.timeline[3 * size_t(wid) + 1]) << 16) | unsigned(nres & 0xffff);
+        }
     } else if (a.steal_list) {
         steal_rescues(a, wid, lane, mt);
     }

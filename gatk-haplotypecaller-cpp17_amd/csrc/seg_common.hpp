@@ -613,17 +613,17 @@ __device__ __forceinline__ void steal_rescues(const LaneArgs& a, int wid, int la
 // sets the part's error word (the host fails the call).
 constexpr int kFusedWaitIters = 1 << 20;
 template <int MAXWI>
-__device__ __forceinline__ void fused_rescues(const LaneArgs& a, int nw, int lane, uint2* __restrict__ mt)
+__device__ __forceinline__ int fused_rescues(const LaneArgs& a, int nw, int lane, uint2* __restrict__ mt)
 {
     constexpr auto AG = __HIP_MEMORY_SCOPE_AGENT;
     if (a.force_wait_timeout) {   // (test hook: as a wait that timed out)
         if (lane == 0) __hip_atomic_fetch_or(a.err, kErrFusedWait, __ATOMIC_RELAXED, AG);
-        return;
+        return 0;
     }
     int go = 0;
     if (lane == 0) go = __hip_atomic_load(a.fz_started, __ATOMIC_RELAXED, AG) >= nw;
-    if (!__builtin_amdgcn_readfirstlane(go)) return;
-    for (;;) {
+    if (!__builtin_amdgcn_readfirstlane(go)) return -1;
+    for (int n = 0;; ++n) {
         int v = 0;   // > 0: a claimed pair id + 1; 0: nothing listed; -2: lost a race, retry
         if (lane == 0) {
             const int h = __hip_atomic_load(a.fz_head, __ATOMIC_RELAXED, AG);
@@ -631,15 +631,16 @@ __device__ __forceinline__ void fused_rescues(const LaneArgs& a, int nw, int lan
             if (h < c) {
                 int hh = h;
                 if (__hip_atomic_compare_exchange_strong(a.fz_head, &hh, h + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED, AG)) {
-                    // the appender has its index; its store of the entry follows
+                    // the appender has its index; its swap of the entry
+                    // follows. Taken by a swap with 0 (clean for the next
+                    // run), performed where the appender's swap is.
                     int e = 0;
                     for (int it = 0; it < kFusedWaitIters; ++it) {
-                        e = __hip_atomic_load(a.rescue_list + h, __ATOMIC_RELAXED, AG);
+                        e = __hip_atomic_exchange(a.rescue_list + h, 0, __ATOMIC_RELAXED, AG);
                         if (e != 0) break;
                         __builtin_amdgcn_s_sleep(2);
                     }
                     if (e == 0) __hip_atomic_fetch_or(a.err, kErrFusedWait, __ATOMIC_RELAXED, AG);
-                    else __hip_atomic_store(a.rescue_list + h, 0, __ATOMIC_RELAXED, AG);   // clean for the next run
                     v = e;
                 } else {
                     v = -2;
@@ -647,8 +648,8 @@ __device__ __forceinline__ void fused_rescues(const LaneArgs& a, int nw, int lan
             }
         }
         v = __builtin_amdgcn_readfirstlane(v);
-        if (v == 0) return;
-        if (v == -2) continue;
+        if (v == 0) return n;
+        if (v == -2) { --n; continue; }
         rescue_one<MAXWI>(a, a.pairs[v - 1], v - 1, -1, lane, mt);   // inputs from earlier launches: no acquire
     }
 }
