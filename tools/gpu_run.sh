@@ -17,6 +17,7 @@
 #                             "tag@ENV=V,ENV=V/tag2@ENV=V" (e.g. ab:S4:2000,20000:on@HC_PHMM_X=1/off@HC_PHMM_X=0)
 #   region:VARIANTS           tools/region_ab.py 128 VARIANTS (e.g. HC_PHMM_X=0,1)
 #   timeline[:NH]             the region call's host phases and device timeline (tools/call_timeline.py)
+#   e2etl                     the same for the S2 flat call (tools/e2e_timing.py)
 #   py:SCRIPT[,ARGS]         python3 tools/SCRIPT ARGS ("py:SCRIPT A=1,2 B=3" when ARGS hold commas)
 # A/B libraries: ab_libs/ is not pushed to the box (.gpurunignore); copy the
 # builds an A/B run needs into ab_stage/ first and name them there.
@@ -69,6 +70,14 @@ for step in "$@"; do
           -- python3 tools/region_prof.py $nh > $OUT/tl_$nh.log 2>&1 &&
       python3 tools/call_timeline.py $OUT/tl_$nh --calls 3 > $OUT/call_timeline_$nh.txt
       rc=$?; tail -25 $OUT/call_timeline_$nh.txt 2>/dev/null ;;
+    e2etl)
+      # The S2 flat call (host buffers in, log10 out): host phases and the
+      # device timeline of its last call.
+      HC_PHMM_TRACE=1 REPS=4 timeout -k 10 180 python3 tools/e2e_timing.py > $OUT/e2e_trace.log 2>&1 &&
+      REPS=4 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/tl_e2e -o run \
+          -- python3 tools/e2e_timing.py > $OUT/tl_e2e.log 2>&1 &&
+      python3 tools/call_timeline.py $OUT/tl_e2e --calls 1 --gap-us 1000 > $OUT/call_timeline_e2e.txt
+      rc=$?; tail -40 $OUT/call_timeline_e2e.txt 2>/dev/null ;;
     py)
       # Spaces in ARGS: taken as they are (commas kept); otherwise commas for spaces.
       case "$arg" in *" "*) a=$arg ;; *) a=${arg//,/ } ;; esac
