@@ -541,9 +541,9 @@ __device__ __forceinline__ void rescue_or_defer(const LaneArgs& a, bool few, int
     if (here) {
         rescue_one(a, a.sdesc[rs], rp, rs, lane, mt);   // sdesc[rs] = pairs[rp]
     } else if (lane == owner_lane) {
-        if (a.steal_list && fits)
-            __hip_atomic_store(a.steal_list + atomicAdd(a.steal_count, 1), rp + 1, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        if (a.steal_list && fits)   // (a swap: performed past this XCD's L2, seen by the other XCDs' waves)
+            (void)__hip_atomic_exchange(a.steal_list + atomicAdd(a.steal_count, 1), rp + 1, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
         else
             a.rescue_list[atomicAdd(a.rescue_count, 1)] = rp;
     }
