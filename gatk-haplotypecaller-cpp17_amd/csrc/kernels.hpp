@@ -64,15 +64,20 @@ constexpr int kStealCount = 9;    // [9, 10] stealable rescue list length, by pa
 constexpr int kErrWord = 12;
 constexpr int kErrPlanWait = 1;   // fp64 pass: a workgroup gave up waiting for the rescue plan
 constexpr int kErrFusedWait = 2;  // fused pass: a wave gave up waiting for a listed rescue's entry
-// [16..17], [20..21] the fused pass's rescue queue (LaneArgs::fz_*), by run
-// parity: waves started, queue head.
+// [16..17] the fused pass's started waves (LaneArgs::fz_*), by run parity;
+// its queue heads from kFusedHeads (kFusedQueues per parity).
 constexpr int kFusedStarted = 16;
-constexpr int kFusedHead = 20;
 constexpr int kSegHeads = 24;
 constexpr int kSegQueues = 9;          // 8 XCD queues + the tail queue
 constexpr int kSegHeadStride = 16;     // ints: one 64-byte line per head
 constexpr int kSegDone = kSegHeads + kSegQueues * kSegHeadStride;
-constexpr int kNumCounters = kSegDone + 16;
+// The fused pass's rescue list is read through kFusedQueues heads: list
+// index i belongs to queue i % kFusedQueues, whose head counts its taken
+// entries (seg_common.hpp fused_rescues). One head made every finishing wave
+// retry a compare-and-swap on the same word: S4's pass took 22 ms.
+constexpr int kFusedQueues = 32;
+constexpr int kFusedHeads = kSegDone + 16;   // [2][kFusedQueues], by run parity
+constexpr int kNumCounters = kFusedHeads + 2 * kFusedQueues;
 static_assert(kNumCounters <= 256, "the prep kernels zero the counters with one 256-thread block");
 
 struct DiagArgs {
@@ -229,10 +234,10 @@ struct LaneArgs {
     // A wave appends its flagged pairs to rescue_list (pid + 1; the entries
     // are zero before the run and the consumer zeroes them again), then, once
     // every wave of the launch has started (fz_started), takes listed rescues
-    // from the queue head and recomputes each in fp64 over its 64 lanes until
-    // none is listed (seg_common.hpp fused_rescues). null = off.
+    // through the kFusedQueues heads and recomputes each in fp64 over its 64
+    // lanes until none is listed (seg_common.hpp fused_rescues). null = off.
     int* fz_started;      // launches the fused form of phmm_seg_kernel when set
-    int* fz_head;
+    int* fz_head;         // kFusedQueues heads of this run's parity
     int fz_wide;          // 1: fp64 blocks up to 32 columns (H <= kSeg64MaxH) at kFusedOcc waves per
                           // SIMD; 0: 8 columns (H <= kInWaveRescueMaxH) at the fp32 pass's 3
     int* err;             // the part's error word (kErrWord)

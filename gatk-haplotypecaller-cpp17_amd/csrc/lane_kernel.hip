@@ -495,7 +495,7 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
     }
     if constexpr (FUSED) {
         __builtin_amdgcn_wave_barrier();   // the rescues below rewrite mt
-        const int nres = fused_rescues<MAXWI>(a, nw, lane, mt);
+        const int nres = fused_rescues<MAXWI>(a, nw, wid, lane, mt);
         if (a.timeline && lane == 0) {   // fused: (time in rescues << 16) | rescues taken (0xffff: not started)
             const unsigned long long t_fin = __builtin_amdgcn_s_memrealtime();
             a.timeline[3 * size_t(wid) + 2] = ((t_fin - a.timeline[3 * size_t(wid) + 1]) << 16) | unsigned(nres & 0xffff);
@@ -553,8 +553,9 @@ __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
         c[kPlanReady + o] = 0;
         c[kStealCount + o] = 0;
         c[kFusedStarted + o] = 0;
-        c[kFusedHead + o] = 0;
     }
+    if (a.fz_head && blockIdx.x == 0 && threadIdx.x < kFusedQueues)
+        a.solo_counters[kFusedHeads + a.solo_other * kFusedQueues + threadIdx.x] = 0;
     if (wid >= n_waves) return;   // wave-uniform (device-planned parts launch an upper bound)
     float* slut = sluts[wib];
     for (int t = __lane_id(); t < kSlutLen; t += 64) slut[t] = a.lut[t];

@@ -180,7 +180,7 @@ int run_part(Part* b, hipStream_t s)
                 g.solo_counters = b->d_count;
                 g.solo_other = par ^ 1;
                 g.fz_started = b->d_count + kFusedStarted + par;
-                g.fz_head = b->d_count + kFusedHead + par;
+                g.fz_head = b->d_count + kFusedHeads + par * kFusedQueues;
                 g.err = b->d_count + kErrWord;
                 g.prio64 = r.prio;
                 g.force_wait_timeout = r.force_plan_timeout;

@@ -600,22 +600,28 @@ __device__ __forceinline__ void steal_rescues(const LaneArgs& a, int wid, int la
 // The fused pass's rescue queue (LaneArgs::fz_*): this wave has appended its
 // flagged pairs; once every one of the launch's nw waves has been dispatched
 // (before that, a wave that stays for rescues holds a slot an undispatched
-// fp32 wave needs), it takes listed rescues from the head, oldest first, each
-// recomputed in fp64 over its 64 lanes (rescue_one: the rescue of
-// intel_pairhmm.hpp:137-139, as the fp64 launch would), until none is listed.
-// No wave ever waits for more: a wave that lists a rescue checks the queue
-// after listing it, so every listed pair is taken by its own wave if by no
-// other (the last waves' rescues run in those waves). Claims go by
-// compare-and-swap on the head, never past the count. (A first form let idle
-// waves poll for rescues until every wave had finished its fp32 pairs: the
-// thousands of polling waves' atomics on the same lines slowed the pass 2-30x.)
-// The one wait, for a claimed entry's store to land, is bounded; giving up
-// sets the part's error word (the host fails the call).
+// fp32 wave needs), it takes listed rescues, each recomputed in fp64 over its
+// 64 lanes (rescue_one: the rescue of intel_pairhmm.hpp:137-139, as the fp64
+// launch would), until none is listed. No wave ever waits for more: a wave
+// that lists a rescue checks the queue after listing it, so every listed pair
+// is taken by its own wave if by no other (the last waves' rescues run in
+// those waves). List index i is entry i / Q of queue i % Q (Q =
+// kFusedQueues): lanes 0..Q-1 read the Q heads in one load, and the wave
+// takes the first queue with an entry below the list length, starting from
+// its own (wid % Q), by compare-and-swap on that queue's head. (One head for
+// all: the hundreds of waves finishing together retried their CAS on one
+// word, each claim ~12 us, S4's pass 22 ms. A first form let idle waves poll
+// until every wave had finished its fp32 pairs: 2-30x slower.) The one wait,
+// for a claimed entry's swap to land, is bounded; giving up sets the part's
+// error word (the host fails the call). Returns the rescues taken (-1: left
+// before every wave had started), for the timeline.
 constexpr int kFusedWaitIters = 1 << 20;
 template <int MAXWI>
-__device__ __forceinline__ int fused_rescues(const LaneArgs& a, int nw, int lane, uint2* __restrict__ mt)
+__device__ __forceinline__ int fused_rescues(const LaneArgs& a, int nw, int wid, int lane, uint2* __restrict__ mt)
 {
     constexpr auto AG = __HIP_MEMORY_SCOPE_AGENT;
+    constexpr int Q = kFusedQueues;
+    static_assert(Q == 32, "the queue choice below rotates a 32-bit mask");
     if (a.force_wait_timeout) {   // (test hook: as a wait that timed out)
         if (lane == 0) __hip_atomic_fetch_or(a.err, kErrFusedWait, __ATOMIC_RELAXED, AG);
         return 0;
@@ -623,33 +629,39 @@ __device__ __forceinline__ int fused_rescues(const LaneArgs& a, int nw, int lane
     int go = 0;
     if (lane == 0) go = __hip_atomic_load(a.fz_started, __ATOMIC_RELAXED, AG) >= nw;
     if (!__builtin_amdgcn_readfirstlane(go)) return -1;
+    int pref = wid & (Q - 1);
     for (int n = 0;; ++n) {
-        int v = 0;   // > 0: a claimed pair id + 1; 0: nothing listed; -2: lost a race, retry
+        const int c = __hip_atomic_load(a.rescue_count, __ATOMIC_RELAXED, AG);
+        const int h = lane < Q ? __hip_atomic_load(a.fz_head + lane, __ATOMIC_RELAXED, AG) : 0;
+        const uint32_t avail = uint32_t(__builtin_amdgcn_ballot_w64(lane < Q && h * Q + lane < c));
+        if (avail == 0) return n;
+        const uint32_t rot = pref == 0 ? avail : (avail >> pref) | (avail << (Q - pref));
+        const int q = (pref + __builtin_ctz(rot)) & (Q - 1);
+        const int hq = __builtin_amdgcn_readlane(h, q);
+        int v = 0;   // > 0: a claimed pair id + 1; -2: lost the race, retry
         if (lane == 0) {
-            const int h = __hip_atomic_load(a.fz_head, __ATOMIC_RELAXED, AG);
-            const int c = __hip_atomic_load(a.rescue_count, __ATOMIC_RELAXED, AG);
-            if (h < c) {
-                int hh = h;
-                if (__hip_atomic_compare_exchange_strong(a.fz_head, &hh, h + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED, AG)) {
-                    // the appender has its index; its swap of the entry
-                    // follows. Taken by a swap with 0 (clean for the next
-                    // run), performed where the appender's swap is.
-                    int e = 0;
-                    for (int it = 0; it < kFusedWaitIters; ++it) {
-                        e = __hip_atomic_exchange(a.rescue_list + h, 0, __ATOMIC_RELAXED, AG);
-                        if (e != 0) break;
-                        __builtin_amdgcn_s_sleep(2);
-                    }
-                    if (e == 0) __hip_atomic_fetch_or(a.err, kErrFusedWait, __ATOMIC_RELAXED, AG);
-                    v = e;
-                } else {
-                    v = -2;
+            int hh = hq;
+            if (__hip_atomic_compare_exchange_strong(a.fz_head + q, &hh, hq + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED, AG)) {
+                // List index hq * Q + q: the appender has it; its swap of the
+                // entry follows. Taken by a swap with 0 (clean for the next
+                // run), performed where the appender's swap is.
+                const int idx = hq * Q + q;
+                int e = 0;
+                for (int it = 0; it < kFusedWaitIters; ++it) {
+                    e = __hip_atomic_exchange(a.rescue_list + idx, 0, __ATOMIC_RELAXED, AG);
+                    if (e != 0) break;
+                    __builtin_amdgcn_s_sleep(2);
                 }
+                if (e == 0) __hip_atomic_fetch_or(a.err, kErrFusedWait, __ATOMIC_RELAXED, AG);
+                v = e;
+            } else {
+                v = -2;
             }
         }
         v = __builtin_amdgcn_readfirstlane(v);
-        if (v == 0) return n;
-        if (v == -2) { --n; continue; }
+        pref = q;
+        if (v == -2) { --n; pref = (q + 1) & (Q - 1); continue; }
+        if (v == 0) return n;   // (gave up waiting: error word set)
         rescue_one<MAXWI>(a, a.pairs[v - 1], v - 1, -1, lane, mt);   // inputs from earlier launches: no acquire
     }
 }
