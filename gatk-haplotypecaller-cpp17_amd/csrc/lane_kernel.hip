@@ -400,7 +400,8 @@ __device__ void plan_rescue(const Seg64Args& a, int n, PlanLds& L)
 // (LaneArgs::fz_*): flagged pairs go to the queue, then the wave takes queued
 // rescues (seg_common.hpp fused_rescues); nw = the launch's waves.
 template <bool FUSED = false, int MAXWI = 0>
-__device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float* __restrict__ slut, int nw = 0)
+__device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float* __restrict__ slut, int nw = 0,
+                                         double* __restrict__ slut64 = nullptr)
 {
     // Lane id and the wave's LDS tables in forms the compiler can recompute
     // (mbcnt) or keep in SGPRs (wave-uniform): values live across the step
@@ -495,7 +496,7 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
     }
     if constexpr (FUSED) {
         __builtin_amdgcn_wave_barrier();   // the rescues below rewrite mt
-        const int nres = fused_rescues<MAXWI>(a, nw, wid, lane, mt);
+        const int nres = fused_rescues<MAXWI>(a, nw, wid, lane, mt, slut64);
         if (a.timeline && lane == 0) {   // fused: (time in rescues << 16) | rescues taken (0xffff: not started)
             const unsigned long long t_fin = __builtin_amdgcn_s_memrealtime();
             a.timeline[3 * size_t(wid) + 2] = ((t_fin - a.timeline[3 * size_t(wid) + 1]) << 16) | unsigned(nres & 0xffff);
@@ -539,6 +540,7 @@ __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
     // overlaps the wave's descriptor loads (small batches are one round of
     // waves: every wave's start-up latency is on the pass's critical path).
     __shared__ float sluts[kSegWPB][kSlutLen];
+    __shared__ double sluts64[FUSED ? kSegWPB : 1][FUSED ? kSlutLen : 1];   // the fused pass's fp64 priors
     const int n_waves = a.n_waves_dev ? __builtin_amdgcn_readfirstlane(*a.n_waves_dev) : a.n_waves;
     const int wib = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
     const int wid = blockIdx.x * kSegWPB + wib;
@@ -560,7 +562,7 @@ __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
     float* slut = sluts[wib];
     for (int t = __lane_id(); t < kSlutLen; t += 64) slut[t] = a.lut[t];
     __builtin_amdgcn_wave_barrier();
-    seg_wave<FUSED, MAXWI>(a, wid, slut, n_waves);
+    seg_wave<FUSED, MAXWI>(a, wid, slut, n_waves, FUSED ? sluts64[wib] : nullptr);
 }
 
 // The persistent form (a separate instance: its fetch loop around the width

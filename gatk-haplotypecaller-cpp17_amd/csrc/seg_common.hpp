@@ -486,8 +486,9 @@ __device__ __forceinline__ int rescue_width_index(int H)
 
 template <int MAXWI = 0>
 __device__ __forceinline__ void rescue_one(const LaneArgs& a, const PairDesc pd, int rp, int rs, int lane,
-                                           uint2* __restrict__ mt)
+                                           uint2* __restrict__ mt, const double* __restrict__ slut64 = nullptr)
 {
+    const double* __restrict__ slut = slut64 ? slut64 : a.lut64;   // (compile-time at every call site)
     const int R = __builtin_amdgcn_readfirstlane(pd.y), H = __builtin_amdgcn_readfirstlane(pd.w);
     const int rx = __builtin_amdgcn_readfirstlane(pd.x);
     const LaneCtx cx{a.rows - kRowPadBefore, unsigned(rx + kRowPadBefore) * 4u, a.hapw,
@@ -503,7 +504,7 @@ __device__ __forceinline__ void rescue_one(const LaneArgs& a, const PairDesc pd,
     switch (wi) {
 #define HC_RESCUE_CASE(WI) \
     case WI: \
-        if constexpr (WI <= MAXWI) run_seg_bc<double, seg64_width(WI)>(a.lut64, a.lut64, st, lane, lane, cx, T0, sM, sX, mt, eq); \
+        if constexpr (WI <= MAXWI) run_seg_bc<double, seg64_width(WI)>(a.lut64, slut, st, lane, lane, cx, T0, sM, sX, mt, eq); \
         break;
         HC_RESCUE_CASE(0) HC_RESCUE_CASE(1) HC_RESCUE_CASE(2) HC_RESCUE_CASE(3) HC_RESCUE_CASE(4) HC_RESCUE_CASE(5)
         HC_RESCUE_CASE(6)
@@ -617,7 +618,8 @@ __device__ __forceinline__ void steal_rescues(const LaneArgs& a, int wid, int la
 // before every wave had started), for the timeline.
 constexpr int kFusedWaitIters = 1 << 20;
 template <int MAXWI>
-__device__ __forceinline__ int fused_rescues(const LaneArgs& a, int nw, int wid, int lane, uint2* __restrict__ mt)
+__device__ __forceinline__ int fused_rescues(const LaneArgs& a, int nw, int wid, int lane, uint2* __restrict__ mt,
+                                             double* __restrict__ slut64)
 {
     constexpr auto AG = __HIP_MEMORY_SCOPE_AGENT;
     constexpr int Q = kFusedQueues;
@@ -662,7 +664,11 @@ __device__ __forceinline__ int fused_rescues(const LaneArgs& a, int nw, int wid,
         pref = q;
         if (v == -2) { --n; pref = (q + 1) & (Q - 1); continue; }
         if (v == 0) return n;   // (gave up waiting: error word set)
-        rescue_one<MAXWI>(a, a.pairs[v - 1], v - 1, -1, lane, mt);   // inputs from earlier launches: no acquire
+        if (n == 0) {   // this wave's fp64 prior table in LDS, as the fp64 launch has it
+            for (int t = lane; t < kSlutLen; t += 64) slut64[t] = a.lut64[t];
+            __builtin_amdgcn_wave_barrier();
+        }
+        rescue_one<MAXWI>(a, a.pairs[v - 1], v - 1, -1, lane, mt, slut64);   // inputs from earlier launches: no acquire
     }
 }
 
