@@ -166,9 +166,14 @@ int run_part(Part* b, hipStream_t s)
             // dispatched: the 415 x 128 region's ~400 rescues run in its last
             // round instead of a launch after it). Not with per-slot records
             // (their gather is the fp64 launch's) or other fp32 kernels.
-            // HC_PHMM_FUSED: 0 off; 1 (default) where solo does not apply;
-            // 2 wide and narrow also where solo would.
-            const int64_t fz = env_i64("HC_PHMM_FUSED", 1);
+            // HC_PHMM_FUSED: 0 (default) off; 1 where solo does not apply; 2
+            // also where solo would. Opt-in: measured slower than the fp64
+            // launch after the pass (S4 0.94 vs 0.74 ms, the 415 x 128 region
+            // call 1.10 vs 1.02 ms): the fp32 waves of the
+            // fused launch run at its occupancy beside fp64 rescues, and a
+            // rescue started by a late fp32 wave ends after the separate
+            // launch would have.
+            const int64_t fz = env_i64("HC_PHMM_FUSED", 0);
             const bool fz_ok = fz != 0 && !rec && persist == 0 && n_one == 0 && b->n_wide == 0 && b->cls[0].n == 0 &&
                                b->cls[1].n == 0 && (fz == 2 || !solo);
             const bool fz_narrow = fz_ok && b->Hmax <= kInWaveRescueMaxH;

@@ -634,13 +634,13 @@ def test_mode_is_per_call_and_fixed_at_submit(engine, golden, golden_batch):
     assert L.shape[1] == len(haps) and len(kept) == L.shape[0]
 
 
-@pytest.mark.parametrize("mode", ["auto", "forced", "off"])
+@pytest.mark.parametrize("mode", ["on", "forced", "off"])
 @pytest.mark.parametrize("shape", ["S4", "S4-300", "many-per-wave", "short-haps", "big-narrow"])
 def test_fused_pass(engine, oracle_lib, monkeypatch, shape, mode):
     """The fused pass (run.cpp, kernels.hpp LaneArgs::fz_*): a small part's
     waves list their rescues on a queue and drain it themselves, no fp64
-    launch (HC_PHMM_FUSED: auto = haps past 512, forced = whenever it applies,
-    off = the fp64 launch). configs[4] (S4, 2 000 pairs, 93 % rescued) and a
+    launch (HC_PHMM_FUSED, opt-in: on = where the solo path does not apply,
+    forced = whenever it applies, off = the default fp64 launch). configs[4] (S4, 2 000 pairs, 93 % rescued) and a
     subset; 8 000 pairs of 520-700 bases four to a wave, most rescued (a wave
     lists several, other waves take them); short haps (the solo path's domain
     unless forced); a 60k-pair part of 300-500-base haps (the narrow form at
@@ -648,7 +648,7 @@ def test_fused_pass(engine, oracle_lib, monkeypatch, shape, mode):
     last wave is dispatched). Flat call and a prepared batch run three times (the queue
     counters go by run parity, the entries are zeroed by their consumers),
     against the oracle; the rescued count is the oracle's."""
-    monkeypatch.setenv("HC_PHMM_FUSED", {"auto": "1", "forced": "2", "off": "0"}[mode])
+    monkeypatch.setenv("HC_PHMM_FUSED", {"on": "1", "forced": "2", "off": "0"}[mode])
     b = {"S4": lambda: W.config("S4"),
          "S4-300": lambda: W.subset(W.config("S4"), np.arange(300)),
          "many-per-wave": lambda: W.generate(8000, (520, 700), (60, 200), 0.08, seed=41),
