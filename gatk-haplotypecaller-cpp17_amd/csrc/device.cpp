@@ -203,8 +203,8 @@ Slot* take_slot(Device& d)
               hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&s->fork, hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&s->join, hipEventDisableTiming) == hipSuccess;
-    for (int k = 0; ok && k < 6; ++k)
-        ok = hipEventCreateWithFlags(&s->ev[k], k == 5 ? hipEventDisableTiming : 0) == hipSuccess;
+    for (int k = 0; ok && k < 7; ++k)
+        ok = hipEventCreateWithFlags(&s->ev[k], k >= 5 ? hipEventDisableTiming : 0) == hipSuccess;
     for (int k = 0; ok && k < 2; ++k) ok = hipEventCreateWithFlags(&s->up_ev[k], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         for (auto& e : s->ev)

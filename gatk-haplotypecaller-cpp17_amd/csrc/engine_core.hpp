@@ -82,7 +82,7 @@ struct Slot {
     // k + 1 and the kernels of part k, and its kernels fill the chip together).
     hipStream_t stream = nullptr, side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;   // side-stream fork / join (timing disabled)
-    hipEvent_t ev[6] = {};   // pack [2], fp32 / fp64 pass [3], done: reused by every part in the slot
+    hipEvent_t ev[7] = {};   // pack [2], fp32 / fp64 pass [3], done, early results: reused by every part in the slot
     hipEvent_t up_ev[2] = {};   // staging halves: H2D of a half done (timing disabled)
 };
 
@@ -296,6 +296,10 @@ struct Part {
     size_t upload_bytes = 0;
     hipEvent_t pack_ev[2] = {nullptr, nullptr};
     hipEvent_t done = nullptr;    // jobs: D2H complete
+    // Jobs: the fp32 pass's raw sums and flags on the host while the fp64
+    // launch runs (run_part), so collect() finishes the unflagged pairs early.
+    hipEvent_t early = nullptr;   // the slot's; null: never
+    bool early_used = false;      // the last run stored them early
     std::vector<std::array<hipEvent_t, 3>> ev_pool;
     std::vector<uint8_t> ev_solo;   // per pooled run: no fp64 launch, ev[2] not recorded (ev[1] ends the run)
     size_t ev_used = 0;
@@ -350,7 +354,11 @@ int plan_part(Device& d, const Src& src, const PartSpec& spec, Slot* slot, bool 
 int plan_flat_device(Device& d, const Src& src, const PartSpec& spec, Slot* slot, bool with_run, Part** out);
 // run.cpp
 int run_part(Part* b, hipStream_t s);
-void finish_part(const Part& P, const float* f, const double* d, const uint8_t* fl, const Outputs& o);
+// which: every pair; the unflagged ones only (their raw f64 is 0: d unread);
+// the flagged ones only.
+enum class Finish { All, Plain, Rescued };
+void finish_part(const Part& P, const float* f, const double* d, const uint8_t* fl, const Outputs& o,
+                 Finish which = Finish::All);
 // Enqueue the results' return to the pinned host image and the part's done
 // event (with_run parts). A kernel stores them into the mapped host memory
 // rather than a DMA copy: DMA copies run in enqueue order, so a D2H enqueued

@@ -1077,6 +1077,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         b->pack_ev[1] = slot->ev[1];
         b->ev_pool.push_back({slot->ev[2], slot->ev[3], slot->ev[4]});
         b->done = slot->ev[5];
+        b->early = slot->ev[6];
     } else {
         b->stream = dv.stream;
         b->side = dv.side;

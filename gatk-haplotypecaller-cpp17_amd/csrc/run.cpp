@@ -239,6 +239,20 @@ int run_part(Part* b, hipStream_t s)
         HIP_TRY(launch_diag_f32(c.W, a, grid, s));
     }
     HIP_TRY(hipEventRecord(b->ev[1], s));
+    // Early results (a job part whose fp64 launch follows, results in place):
+    // the fp32 pass's raw sums and rescue flags, final now, go to the pinned
+    // image on the side stream while the fp64 launch runs, and collect()
+    // finishes the unflagged pairs' log10 in that time; the fp64 sums and the
+    // counters follow (enqueue_results). The 415 x 128 region's host finish
+    // (~0.06 ms of log10f) overlapped its fp64 launch (~0.1 ms).
+    b->early_used = b->early && b->host_res && !solo && !all_f64 && r.rec == nullptr && b->n > 0 &&
+                    b->d_raw32 == b->own_raw32 && env_i64("HC_PHMM_EARLY_FINISH", 1) != 0;
+    if (b->early_used) {
+        HIP_TRY(hipStreamWaitEvent(b->side, b->ev[1], 0));
+        HIP_TRY(launch_store_to_host(b->host_res, b->own_raw32, b->res_o64, b->side));
+        HIP_TRY(launch_store_to_host(b->host_res + b->res_ofl, b->own_flag, b->res_ocnt - b->res_ofl, b->side));
+        HIP_TRY(hipEventRecord(b->early, b->side));
+    }
     if (b->n > 0 && !solo) {
         // fp64 rescue (intel_pairhmm.hpp:137-139) over the device-built list, no
         // host round trip for its length: device planning + column-segmented
@@ -287,7 +301,13 @@ int check_device_error(const int* counters)
 
 int enqueue_results(Part* b, hipStream_t s)
 {
-    HIP_TRY(launch_store_to_host(b->host_res, b->own_raw32, b->res_bytes, s));
+    if (b->early_used) {   // the rest: raw f64, flags again (same bytes), counters; done covers both
+        HIP_TRY(launch_store_to_host(b->host_res + b->res_o64, reinterpret_cast<const char*>(b->own_raw32) + b->res_o64,
+                                     b->res_bytes - b->res_o64, s));
+        HIP_TRY(hipStreamWaitEvent(s, b->early, 0));
+    } else {
+        HIP_TRY(launch_store_to_host(b->host_res, b->own_raw32, b->res_bytes, s));
+    }
     if (!b->done) HIP_TRY(hipEventCreateWithFlags(&b->done, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(b->done, s));
     return HC_PHMM_OK;
@@ -297,19 +317,21 @@ int enqueue_results(Part* b, hipStream_t s)
 // reference) of a part's results, scattered into the caller's outputs. Chunks
 // of 2 048 pairs: a 415 x 128 region's 53 120 log10 calls spread over the
 // whole pool (in chunks of 8 192 they took 7 threads, ~0.07 ms).
-void finish_part(const Part& P, const float* f, const double* d, const uint8_t* fl, const Outputs& o)
+void finish_part(const Part& P, const float* f, const double* d, const uint8_t* fl, const Outputs& o, Finish which)
 {
     const Luts& L = luts();
     const float l10f = L.log10_init_f;
     const double l10d = L.log10_init_d;
     auto ll = [&](int64_t k) { return fl[k] ? std::log10(d[k]) - l10d : double(std::log10(f[k]) - l10f); };
+    auto want = [&](int64_t k) { return which == Finish::All || (fl[k] != 0) == (which == Finish::Rescued); };
     if (P.spec.flat) {
         const int64_t id0 = P.spec.lo;
         parallel_for(P.n, [&](int64_t lo, int64_t hi) {
             for (int64_t k = lo; k < hi; ++k) {
+                if (!want(k)) continue;
                 if (o.loglik) o.loglik[id0 + k] = ll(k);
                 if (o.raw32) o.raw32[id0 + k] = f[k];
-                if (o.raw64) o.raw64[id0 + k] = d[k];
+                if (o.raw64) o.raw64[id0 + k] = which == Finish::Plain ? 0.0 : d[k];
                 if (o.resc) o.resc[id0 + k] = fl[k];
             }
         }, 2048);
@@ -327,7 +349,7 @@ void finish_part(const Part& P, const float* f, const double* d, const uint8_t* 
             const int64_t end = std::min(hi, base[b + 1]);
             int64_t r = (k - base[b]) / B.nh, h = (k - base[b]) % B.nh;
             for (; k < end; ++k) {
-                B.out[r * B.ostride + h] = ll(k);
+                if (want(k)) B.out[r * B.ostride + h] = ll(k);
                 if (++h == B.nh) {
                     h = 0;
                     ++r;

@@ -146,6 +146,25 @@ def test_cross_regions_vs_oracle(engine, oracle_lib, monkeypatch, split):
         assert np.array_equal(bits(g), bits(e)), f"region {k}"
 
 
+@pytest.mark.parametrize("early", ["1", "0"])
+def test_early_finish(engine, oracle_lib, monkeypatch, early):
+    """A job part's unflagged pairs finished on the host while its fp64 launch
+    runs (run.cpp run_part, api.cpp collect; HC_PHMM_EARLY_FINISH): a region
+    with hundreds of rescues, a flat call of long haps (most pairs rescued) and
+    one with none rescued, against the oracle, every output field."""
+    monkeypatch.setenv("HC_PHMM_EARLY_FINISH", early)
+    monkeypatch.setenv("HC_PHMM_RESCUE_IN_WAVE_MAX", "4")   # most rescues to the fp64 launch
+    reads, haps = W.region(n_reads=415, n_haps=24, seed=211)
+    flat = W.region_flat(reads, haps)
+    ref = oracle_lib.pairs(flat, nthreads=16)
+    assert ref["rescued"].sum() > 50
+    got = engine.cross(reads, haps)
+    assert np.array_equal(bits(got), bits(ref["loglik"].reshape(len(reads), len(haps))))
+    for b in (W.subset(W.config("S4"), np.arange(400)), W.generate(3000, (100, 300), (60, 150), 0.0, seed=7)):
+        ref = oracle_lib.pairs(b, nthreads=16)
+        assert_same(engine.pairs(b), ref, f"early={early}")
+
+
 def test_submit_regions_two_slots(two_slots, oracle_lib):
     regions = [W.region(n_reads=200, n_haps=int(nh), seed=300 + k) for k, nh in enumerate([4, 16, 2, 8])]
     ref = _regions_ref(oracle_lib, regions)
