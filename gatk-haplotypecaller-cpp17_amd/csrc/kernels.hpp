@@ -243,6 +243,8 @@ struct LaneArgs {
     int* err;             // the part's error word (kErrWord)
     int force_wait_timeout;   // test hook (HC_PHMM_TEST_PLAN_TIMEOUT=1): a wave reaching the queue gives up at once
     int prio64;           // the fused pass's fp64 rescues: issue priority by remaining steps (as Seg64Args::prio)
+    int fz_prio;          // 1: fp32 work at issue priority 2, queued rescues at 0 (they fill the issue
+                          // cycles the pass's waves leave idle instead of slowing its last waves)
 };
 // Waves per SIMD of the wide fused pass (fp64 blocks up to 32 columns in the
 // same waves: 256 VGPRs); run.cpp takes it only when every wave of a part is

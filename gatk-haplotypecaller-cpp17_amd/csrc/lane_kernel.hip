@@ -409,6 +409,7 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
     const int lane = __lane_id();
     const unsigned long long t_start = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
     if (FUSED && lane == 0) __hip_atomic_fetch_add(a.fz_started, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (FUSED && a.fz_prio) __builtin_amdgcn_s_setprio(2);
     const LaneWave wv = load_wave(a.waves, wid);
     const int bc = wv.ncols;
     __shared__ uint2 mtab[kSegWPB][5 * 64];

@@ -188,7 +188,8 @@ int run_part(Part* b, hipStream_t s)
                 g.fz_started = b->d_count + kFusedStarted + par;
                 g.fz_head = b->d_count + kFusedHeads + par * kFusedQueues;
                 g.err = b->d_count + kErrWord;
-                g.prio64 = r.prio;
+                g.fz_prio = int(env_i64("HC_PHMM_FUSED_PRIO", 1));
+                g.prio64 = g.fz_prio ? 0 : r.prio;
                 g.force_wait_timeout = r.force_plan_timeout;
                 g.inker_count = nullptr;
                 b->inker_limit = 0;

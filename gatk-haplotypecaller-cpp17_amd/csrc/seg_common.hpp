@@ -665,6 +665,7 @@ __device__ __forceinline__ int fused_rescues(const LaneArgs& a, int nw, int wid,
         if (v == -2) { --n; pref = (q + 1) & (Q - 1); continue; }
         if (v == 0) return n;   // (gave up waiting: error word set)
         if (n == 0) {   // this wave's fp64 prior table in LDS, as the fp64 launch has it
+            if (a.fz_prio) __builtin_amdgcn_s_setprio(0);
             for (int t = lane; t < kSlutLen; t += 64) slut64[t] = a.lut64[t];
             __builtin_amdgcn_wave_barrier();
         }

@@ -15,7 +15,7 @@
 #   profiles                  every bench config's profile (S2 S1 S4 S4_20000 both shards, the region)
 #   ab:WL:PAIRS:VARIANTS      tools/persist_ab.sh with NO_R3=1; PAIRS comma-separated, VARIANTS
 #                             "tag@ENV=V,ENV=V/tag2@ENV=V" (e.g. ab:S4:2000,20000:on@HC_PHMM_X=1/off@HC_PHMM_X=0)
-#   region:VARIANTS           tools/region_ab.py 128 VARIANTS (e.g. HC_PHMM_X=0,1)
+#   region:VARIANTS           tools/region_ab.py 128 VARIANTS (e.g. HC_PHMM_X=0,1; "X=0,1;Y=2,3": cross product)
 #   timeline[:NH]             the region call's host phases and device timeline (tools/call_timeline.py)
 #   e2etl                     the same for the S2 flat call (tools/e2e_timing.py)
 #   py:SCRIPT[,ARGS]         python3 tools/SCRIPT ARGS ("py:SCRIPT A=1,2 B=3" when ARGS hold commas)
@@ -59,7 +59,7 @@ for step in "$@"; do
       WL=$wl NO_R3=1 PAIRS="${pairs//,/ }" VARIANTS="$vv" bash tools/persist_ab.sh
       rc=$? ;;
     region)
-      timeout -k 10 300 python3 tools/region_ab.py 128 $arg
+      timeout -k 10 300 python3 tools/region_ab.py 128 ${arg//;/ }
       rc=$? ;;
     timeline)
       # Region call breakdown: host phases (HC_PHMM_TRACE) and the device
