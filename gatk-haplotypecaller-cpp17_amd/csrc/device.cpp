@@ -52,6 +52,7 @@ void release_device(Device* d)
     for (Slot* s : d->slots) {
         if (s->stream) (void)hipStreamSynchronize(s->stream);
         if (s->side) (void)hipStreamSynchronize(s->side);
+        if (s->prep) (void)hipStreamSynchronize(s->prep);
         if (s->dev) (void)hipFree(s->dev);
         if (s->host) (void)hipHostFree(s->host);
         for (auto& e : s->ev)
@@ -61,6 +62,7 @@ void release_device(Device* d)
         if (s->fork) (void)hipEventDestroy(s->fork);
         if (s->join) (void)hipEventDestroy(s->join);
         if (s->side) (void)hipStreamDestroy(s->side);
+        if (s->prep) (void)hipStreamDestroy(s->prep);
         if (s->stream) (void)hipStreamDestroy(s->stream);
         delete s;
     }
@@ -219,6 +221,10 @@ Slot* take_slot(Device& d)
         fail(HC_PHMM_EHIP, "slot stream / event creation");
         return nullptr;
     }
+    int lo = 0, hi = 0;   // (hi: the greatest priority, numerically lowest)
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&s->prep, hipStreamNonBlocking, hi) != hipSuccess)
+        s->prep = nullptr;
     s->busy = true;
     std::lock_guard<std::mutex> lk(g_mu);
     d.slots.push_back(s);
@@ -267,6 +273,7 @@ void free_part(Part* p)
 {
     if (!p) return;
     if (p->dev) (void)hipSetDevice(p->dev->ordinal);
+    if (p->prep) (void)hipStreamSynchronize(p->prep);   // (its uploads read the slot's memory)
     if (p->timeline) {
         std::lock_guard<std::mutex> lk(g_tl.mu);
         if (p->last_stream) (void)hipStreamSynchronize(p->last_stream);

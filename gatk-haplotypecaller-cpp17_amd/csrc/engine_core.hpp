@@ -81,6 +81,10 @@ struct Slot {
     // run concurrently (a call cut into parts overlaps the planning of part
     // k + 1 and the kernels of part k, and its kernels fill the chip together).
     hipStream_t stream = nullptr, side = nullptr;
+    // The flat path's uploads and preparation kernels, at the device's
+    // greatest stream priority: a part's preparation runs while the previous
+    // part's pass still holds the chip, not after it drains (null: on stream).
+    hipStream_t prep = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;   // side-stream fork / join (timing disabled)
     hipEvent_t ev[7] = {};   // pack [2], fp32 / fp64 pass [3], done, early results: reused by every part in the slot
     hipEvent_t up_ev[2] = {};   // staging halves: H2D of a half done (timing disabled)
@@ -309,6 +313,7 @@ struct Part {
     hipStream_t side = nullptr;               // segmented waves beside one-lane waves
     hipEvent_t fork = nullptr, join = nullptr;
     hipStream_t last_stream = nullptr;
+    hipStream_t prep = nullptr;               // its uploads and preparation, if not on stream (Slot::prep)
     int64_t launch_waves = 0;
     bool ran = false;
     unsigned long long* timeline = nullptr;   // HC_PHMM_TIMELINE=1: this part's wave records
@@ -327,6 +332,7 @@ public:
     ~PartGuard()
     {
         if (!p_) return;
+        if (p_->prep) (void)hipStreamSynchronize(p_->prep);
         if (p_->stream) (void)hipStreamSynchronize(p_->stream);
         discard_part(p_);
     }

@@ -735,6 +735,10 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     b->upload_bytes = size_t(rec) + sizeof(FlatDesc) * n1 + tab_bytes;
     hipStream_t s = b->stream;
 
+    // Uploads and preparation on the slot's priority stream (Slot::prep;
+    // HC_PHMM_PREP_PRIO=0: the part's stream), the pass waits for them.
+    const hipStream_t ps = slot && slot->prep && env_i64("HC_PHMM_PREP_PRIO", 1) != 0 ? slot->prep : s;
+    if (ps != s) b->prep = ps;
     std::atomic<bool> varying{false};
     auto enqueue = [&]() -> int {
         // Pass 2: chunks through the ring, each H2D'd as soon as it is filled.
@@ -752,18 +756,18 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
                 FlatDesc* dd = reinterpret_cast<FlatDesc*>(buf + dbase);
                 fill_chunk(src, lo, n, m0, m1, mini, gapw, fmtw, scan_gaps, buf, r0, dd, p0, varying);
                 if (varying.load()) return kRetryWithPlanes;
-                HIP_TRY(hipMemcpyAsync(dev + o_img + r0, buf, size_t(r1 - r0), hipMemcpyHostToDevice, s));
+                HIP_TRY(hipMemcpyAsync(dev + o_img + r0, buf, size_t(r1 - r0), hipMemcpyHostToDevice, ps));
                 HIP_TRY(hipMemcpyAsync(dev + o_desc + sizeof(FlatDesc) * size_t(p0), dd,
-                                       sizeof(FlatDesc) * size_t(p1 - p0), hipMemcpyHostToDevice, s));
-                HIP_TRY(hipEventRecord(dv.ring.ev[ri], s));
+                                       sizeof(FlatDesc) * size_t(p1 - p0), hipMemcpyHostToDevice, ps));
+                HIP_TRY(hipEventRecord(dv.ring.ev[ri], ps));
                 dv.ring.used[ri] = true;
             }
         }
         tm.mark("flat: fill + H2D");
         if (!b->slot_ev)
             for (auto& e : b->pack_ev) HIP_TRY(hipEventCreate(&e));
-        HIP_TRY(hipMemcpyAsync(dev + o_tab, host, tab_bytes, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipEventRecord(b->pack_ev[0], s));
+        HIP_TRY(hipMemcpyAsync(dev + o_tab, host, tab_bytes, hipMemcpyHostToDevice, ps));
+        HIP_TRY(hipEventRecord(b->pack_ev[0], ps));
         FlatPlanArgs a{};
         a.img = reinterpret_cast<const uint8_t*>(dev + o_img);
         a.desc = reinterpret_cast<const FlatDesc*>(dev + o_desc);
@@ -792,8 +796,9 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
         a.nwaves = reinterpret_cast<int*>(dev + o_nw);
         a.counters = b->d_count;
         a.list = b->d_list;
-        HIP_TRY(launch_flat_plan(a, s));
-        HIP_TRY(hipEventRecord(b->pack_ev[1], s));
+        HIP_TRY(launch_flat_plan(a, ps));
+        HIP_TRY(hipEventRecord(b->pack_ev[1], ps));
+        if (ps != s) HIP_TRY(hipStreamWaitEvent(s, b->pack_ev[1], 0));
         if (with_run) {
             const int r = run_part(b, s);
             if (r) return r;
