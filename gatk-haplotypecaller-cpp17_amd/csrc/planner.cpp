@@ -234,6 +234,67 @@ void grow(std::vector<T>& v, size_t n)
 // partial). Segments run widest block first, so co-resident waves share a
 // width's code. Writes every pair's descriptor, the slot order and the waves;
 // returns the batch's cells.
+// The candidate policy of a structured plan: each hap's cheaper candidate
+// (-1), or candidate 0 / 1 for every hap, whichever the pass model prices
+// lowest over the plan's actual waves. The per-hap choice can push a pass over
+// a waves-per-SIMD boundary the width cap's model (choose_cap: ~60 lanes per
+// wave) did not count on: a 415 x 32 region took 10 lanes of 42 columns per
+// hap, 6 pairs per wave, 2 214 waves — 190 SIMDs with a third wave, which ran
+// alone after the other two: fp32 pass 0.40 ms, where 9 lanes of 48 columns
+// (7 pairs, 1 898 waves, two per SIMD) take 0.21 ms. The model: a SIMD with n
+// waves takes 3 floor(n/3) rounds plus 2 for a partial round (its last one or
+// two waves issue alone or in a pair), up to 12 waves per SIMD (a region's
+// waves are alike, so the SIMDs holding one more wave set the pass); past
+// that, rounds follow the total work.
+int grid_policy(const Local& loc, const int32_t* rlen, const Cand* hcand, const float* waste, int n_simd)
+{
+    const PartSpec& spec = *loc.spec;
+    int best_pol = -1;
+    double best = 0;
+    std::vector<std::pair<uint16_t, int>> cnt;
+    for (int pol = -1; pol <= 1; ++pol) {
+        double waves = 0, work = 0;
+        for (size_t b = 0; b < spec.blocks.size(); ++b) {
+            const Block& B = spec.blocks[b];
+            if (B.nr <= 0 || B.nh <= 0) continue;
+            const int64_t r0 = loc.blk_r[b], h0 = loc.blk_h[b];
+            int64_t rs = 0;
+            for (int r = 0; r < B.nr; ++r) rs += rlen[r0 + r];
+            const int Rm = int((rs + B.nr / 2) / B.nr);
+            cnt.clear();
+            for (int h = 0; h < B.nh; ++h) {
+                const Cand cd = hcand[h0 + h];
+                const int q = pol >= 0 ? pol
+                              : seg_cost(cd.nb[1], cd.bc[1], Rm, waste) < seg_cost(cd.nb[0], cd.bc[0], Rm, waste) ? 1
+                                                                                                                 : 0;
+                const uint16_t k = uint16_t(cd.bc[q] << 8 | cd.nb[q]);
+                auto it = std::find_if(cnt.begin(), cnt.end(), [&](const auto& e) { return e.first == k; });
+                if (it == cnt.end()) cnt.push_back({k, 1});
+                else ++it->second;
+            }
+            for (const auto& e : cnt) {
+                const int bc = e.first >> 8, nb = e.first & 0xff, per = 64 / nb;
+                const double w = double((int64_t(B.nr) * e.second + per - 1) / per);
+                waves += w;
+                work += w * (13.0 * bc + 26.0) * double(Rm + nb - 1);
+            }
+        }
+        if (waves <= 0) return -1;
+        const double per_simd = waves / double(n_simd);
+        double rounds = per_simd;
+        if (per_simd <= 12.0) {
+            const int n = std::max(1, int(std::ceil(per_simd - 1e-9)));
+            rounds = 3.0 * (n / 3) + (n % 3 ? 2.0 : 0.0);
+        }
+        const double est = rounds * work / waves;
+        if (pol == -1 || est < best * 0.98) {
+            best = est;
+            best_pol = pol;
+        }
+    }
+    return best_pol;
+}
+
 int64_t plan_grid(const Local& loc, const int32_t* rlen, const int32_t* hlen, const int64_t* row_off,
                   const int64_t* hap_w, const Cand* hcand, const float* waste, int qforce, PairDesc* pd,
                   bool write_pairs, std::vector<int>& seg_ord, std::vector<LaneWave>& lw, PhaseTimer& tm,
@@ -592,8 +653,11 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         one_ord.clear();
         ord2[0].clear();
         ord2[1].clear();
-        cells_a = plan_grid(loc, rlen, hlen, row_off.data(), hap_w.data(), hcand, waste, qforce, pd, !dev_plan, seg_ord, lw, tm,
-                            dev_plan ? &gd : nullptr);
+        const int qgrid = qforce >= 0 || env_i64("HC_PHMM_GRID_POLICY", 1) == 0
+                              ? qforce
+                              : grid_policy(loc, rlen, hcand, waste, 4 * dv.n_cu);
+        cells_a = plan_grid(loc, rlen, hlen, row_off.data(), hap_w.data(), hcand, waste, qgrid, pd, !dev_plan, seg_ord, lw,
+                            tm, dev_plan ? &gd : nullptr);
         tm.mark("grid: pairs");
     } else {
         // Per pair: descriptor straight into the staging image, class, and for

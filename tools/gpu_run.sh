@@ -18,7 +18,7 @@
 #   region:VARIANTS           tools/region_ab.py 128 VARIANTS (e.g. HC_PHMM_X=0,1; "X=0,1;Y=2,3": cross product)
 #   timeline[:NH]             the region call's host phases and device timeline (tools/call_timeline.py)
 #   e2etl                     the same for the S2 flat call (tools/e2e_timing.py)
-#   py:SCRIPT[,ARGS]         python3 tools/SCRIPT ARGS ("py:SCRIPT A=1,2 B=3" when ARGS hold commas)
+#   py:SCRIPT[,ARGS]          python3 tools/SCRIPT ARGS ("py:SCRIPT A=1,2 B=3" when ARGS hold commas)
 # A/B libraries: ab_libs/ is not pushed to the box (.gpurunignore); copy the
 # builds an A/B run needs into ab_stage/ first and name them there.
 set -o pipefail
