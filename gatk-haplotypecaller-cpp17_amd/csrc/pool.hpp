@@ -91,10 +91,12 @@ private:
         unsigned hw = std::max(1u, std::thread::hardware_concurrency());
         if (const char* e = std::getenv("HC_PHMM_THREADS"))
             if (std::atoi(e) > 0) hw = unsigned(std::atoi(e));
-        // A worker done with a batch spins this long for the next before it
-        // sleeps: a call's host phases are parallel loops microseconds apart,
-        // and a futex wake-up of every worker for each cost more than small
-        // loops' work (415 x 128 region call 0.96 ms at 4 threads, 1.00 at 16).
+        // HC_PHMM_POOL_SPIN_US: a worker done with a batch spins this long for
+        // the next before it sleeps. Default 0: measured no faster on the
+        // region call (0.95 ms at 0, 0.96 at 50 us, 0.98 at 200) and slower
+        // end to end (the spinning takes cores from the staging fill). What
+        // paid was waking only as many workers as a batch has tasks (above:
+        // the 415 x 128 region call 1.00 -> 0.95 ms at 16 threads).
         if (const char* e = std::getenv("HC_PHMM_POOL_SPIN_US"))
             if (std::atoi(e) >= 0) spin_us_ = std::atoi(e);
         const int nw = int(std::min(hw, 16u)) - 1;
@@ -168,7 +170,7 @@ private:
     bool stop_ = false;
     std::atomic<uint64_t> epoch_{0};   // batches queued so far
     std::atomic<int> spinning_{0};     // workers spinning for the next batch
-    int spin_us_ = 50;
+    int spin_us_ = 0;
 };
 
 // f(lo, hi) over [0, n) in chunks of at least `grain`, on the pool.
