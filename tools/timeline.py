@@ -4,6 +4,7 @@ CU / SIMD (HW_ID), after warm-up runs. Prints a summary: pass span, when the
 last wave starts, how busy the wave slots are over time (tenths of the span),
 the idle slot-time at the end, wave duration spread.
     HC_PHMM_TIMELINE=1 python tools/timeline.py S2:125000 [out.npy]
+    HC_PHMM_TIMELINE=1 python tools/timeline.py cross:415:128     (the region call's own plan)
 With the fused pass (HC_PHMM_FUSED, LaneArgs::fz_*) the third word is instead
 (time in queued rescues << 16) | rescues taken (0xffff: the wave left before
 every wave had started); the summary then describes the rescue phase.
@@ -21,22 +22,30 @@ import workloads as W  # noqa: E402
 
 os.environ["HC_PHMM_TIMELINE"] = "1"
 name, _, n = sys.argv[1].partition(":")
-if name == "region":
-    nr, nh = (int(x) for x in n.split(":"))
-    b = W.region_flat(*W.region(n_reads=nr, n_haps=nh))
-else:
-    b = W.config(name, int(n) if n else None)
 hcphmm.init(0)
 L = hcphmm.lib()
 L.hcx_timeline.argtypes = [C.c_void_p, C.c_int]
-bt = hcphmm.Batch(b)
-for _ in range(4):
-    bt.run()
-st = bt.stats()
 cap = 4_000_000
 buf = np.zeros(3 * cap, np.uint64)
-nw = L.hcx_timeline(buf.ctypes.data, cap)
-bt.close()
+if name == "cross":   # the region call itself (structured plan), cross:NR:NH
+    nr, nh = (int(x) for x in n.split(":"))
+    call = hcphmm.CrossCall(*W.region(n_reads=nr, n_haps=nh))
+    for _ in range(8):
+        call()
+    st = type("St", (), {"kernel_ms_f32": float("nan")})()
+    nw = L.hcx_timeline(buf.ctypes.data, cap)
+else:
+    if name == "region":   # the same pairs as a flat batch
+        nr, nh = (int(x) for x in n.split(":"))
+        b = W.region_flat(*W.region(n_reads=nr, n_haps=nh))
+    else:
+        b = W.config(name, int(n) if n else None)
+    bt = hcphmm.Batch(b)
+    for _ in range(4):
+        bt.run()
+    st = bt.stats()
+    nw = L.hcx_timeline(buf.ctypes.data, cap)
+    bt.close()
 rec = buf[:3 * nw].reshape(nw, 3).astype(np.int64)
 t0 = rec[:, 0].min()
 start = (rec[:, 0] - t0) / 100.0   # us
