@@ -59,9 +59,12 @@ constexpr int ITERS = 2048;
     F(41, "v_lshlrev_b32(vgpr-shift)", "v_lshlrev_b32 %0, %1, %0")                \
     F(42, "v_subrev_u32", "v_subrev_u32 %0, %0, %1")                              \
     F(43, "v_mad_u32_u24", "v_mad_u32_u24 %0, %0, %1, %1")                        \
-    F(44, "v_mul_u32_u24", "v_mul_u32_u24 %0, %0, %1")
+    F(44, "v_mul_u32_u24", "v_mul_u32_u24 %0, %0, %1")                            \
+    F(45, "v_and_b32_sdwa sext(BYTE_1)", "v_and_b32_sdwa %0, %1, sext(%0) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1") \
+    F(46, "prior select v_bfe_i32+v_bitop3_b32(2)", "v_bfe_i32 %0, %1, %0, 1\n v_bitop3_b32 %0, %0, %1, %1 bitop3:0xe4") \
+    F(47, "prior select v_and_b32_sdwa+v_xor_b32(2)", "v_and_b32_sdwa %0, %1, sext(%0) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1\n v_xor_b32 %0, %0, %1")
 
-constexpr int NOPS = 45;
+constexpr int NOPS = 48;
 
 template <int MODE>
 __global__ __launch_bounds__(256) void k(int* out, int c)
@@ -136,7 +139,7 @@ void all(int* out, int blocks)
             OPS(NAME)
 #undef NAME
         };
-        g_per = (M == 34) ? 2 : (M == 40) ? 3 : 1;
+        g_per = (M == 34 || M == 46 || M == 47) ? 2 : (M == 40) ? 3 : 1;
         report(names[M], run(k<M>, out, blocks));
         g_per = 1;
         all<M + 1>(out, blocks);
