@@ -103,3 +103,25 @@ def test_region_plan_uses_full_waves(L):
     lanes = [(-(-pairs[order[s0:s0 + np_], 3] // bc)).sum() for s0, _, _, bc, np_, _ in waves]
     groups = len({(bc, -(-int(pairs[order[s0], 3]) // bc)) for s0, _, _, bc, _, _ in waves})
     assert sum(1 for x in lanes if x + 7 < 64) <= groups
+
+
+@pytest.mark.parametrize("policy", ["1", "0"])
+def test_region_plan_policy_keeps_two_waves_per_simd(L, monkeypatch, policy):
+    """planner.cpp grid_policy: a 415 x 32 region's per-hap choice (10 lanes of
+    42 columns, 6 pairs per wave) gives 2 214 waves — a third wave on 190 of
+    the 1 024 SIMDs; the pass model takes 9 lanes of 48 columns everywhere
+    instead (7 pairs per wave, 1 898 waves). HC_PHMM_GRID_POLICY=0 keeps the
+    per-hap choice. Either plan must stay exact."""
+    monkeypatch.setenv("HC_PHMM_GRID_POLICY", policy)
+    reads, haps = W.region(415, 32)
+    arr, outs, keep = hcphmm._region_array([(reads, haps)])
+    L.hcx_plan_regions(arr, 1, 256, 1)
+    pairs, order, n_seg, waves, used_grid = dump(L)
+    assert used_grid == 1
+    R = np.repeat([len(r[0]) for r in reads], len(haps))
+    H = np.tile([len(h) for h in haps], len(reads))
+    check_plan(pairs, order, n_seg, waves, R, H)
+    if policy == "1":
+        assert len(waves) <= 2 * 1024 and set(waves[:, 3]) <= {46, 48}
+    else:
+        assert len(waves) > 2 * 1024
