@@ -392,6 +392,22 @@ struct FlatDesc {
 // uploads ~250 instead of ~416 bytes per pair.
 constexpr int kFmtRead1B = 1;
 constexpr int kFmtHap2b = 2;
+// Dispatch position of the wave of rank r (descending modelled duration) in a
+// plan of W waves that are all resident at once (S < W <= 3 S, S = SIMDs):
+// one-wave workgroups are dealt to the SIMDs in order, position p and p + S
+// sharing one (per-wave HW_ID, tools/timeline.py), so a SIMD's waves are ranks
+// of rounds q = 0, 1, 2 and the pass lasts as long as its heaviest SIMD's sum.
+// Snake order: round 0 heaviest first, round 1 lightest first, round 2 heaviest
+// first again (the heaviest wave shares its SIMD with the lightest); a partial
+// last odd round puts its lightest waves on the lowest SIMDs (positions must
+// stay below W).
+__host__ __device__ inline int one_round_pos(int r, int W, int S)
+{
+    const int q = r / S, i = r - q * S;
+    if ((q & 1) == 0) return r;
+    return (q + 1) * S <= W ? q * S + (S - 1 - i) : q * S + (W - 1 - r);
+}
+
 struct FlatPlanArgs {
     const uint8_t* img;
     const FlatDesc* desc;
@@ -416,6 +432,8 @@ struct FlatPlanArgs {
     int max_waves;         // waves the launch covers (upper bound of the plan's)
     int* nwaves;           // the plan's wave count
     int tail;              // waves dispatched last, longest first (0: packing order)
+    int n_simd;            // one-round plans (waves within the resident slots): snake order over
+                           // the SIMDs (one_round_pos), 0 = off
     int* counters;         // kNumCounters run counters, zeroed
     int* list;             // the rescue list (n entries), zeroed (the fused pass's queue)
 };

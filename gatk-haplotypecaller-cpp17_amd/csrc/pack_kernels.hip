@@ -462,6 +462,8 @@ __global__ __launch_bounds__(256) void flat_waves_kernel(FlatPlanArgs a)
 // bulk in packing order (co-resident waves share one width's code), the
 // `tail` shortest waves (modelled duration BC x steps, in 1024 buckets) last,
 // longest first, so the chip drains evenly; order inside a bucket arbitrary.
+__device__ __forceinline__ int wave_cost(const LaneWave& v) { return (13 * v.ncols + 26) * v.nsteps; }   // plan_model.hpp
+
 __global__ __launch_bounds__(1024) void flat_tail_kernel(FlatPlanArgs a)
 {
     constexpr int NB = 1024;
@@ -476,17 +478,20 @@ __global__ __launch_bounds__(1024) void flat_tail_kernel(FlatPlanArgs a)
     const int C = (nw + 1023) / 1024;
     const int w0 = min(nw, t * C), w1 = min(nw, w0 + C);
     int m = 1;
-    for (int w = w0; w < w1; ++w) m = max(m, in[w].ncols * in[w].nsteps);
+    for (int w = w0; w < w1; ++w) m = max(m, wave_cost(in[w]));
     atomicMax(&cmax_s, m);
     __syncthreads();
     const long long cm = cmax_s;
-    auto bucket = [&](const LaneWave& v) { return int((long long)(v.ncols * v.nsteps) * (NB - 1) / cm); };
+    auto bucket = [&](const LaneWave& v) { return int((long long)wave_cost(v) * (NB - 1) / cm); };
     for (int w = w0; w < w1; ++w) atomicAdd(&hist[bucket(in[w])], 1);
     __syncthreads();
+    // One round (every wave resident at once, waves of unequal length): all
+    // waves in snake order over the SIMDs (kernels.hpp one_round_pos).
+    const bool snake = a.n_simd > 0 && nw > a.n_simd && nw <= 3 * a.n_simd;
     if (t == 0) {   // the smallest bucket threshold holding at least `tail` waves below it
         int acc = 0, thr = 0;
         while (thr < NB && acc < a.tail) acc += hist[thr++];
-        thr_s = acc >= nw ? 0 : thr;   // nothing to gain when every wave is in the tail
+        thr_s = snake ? NB : acc >= nw ? 0 : thr;   // nothing to gain when every wave is in the tail
         int off = 0;   // tail buckets longest first
         for (int b = thr_s - 1; b >= 0; --b) {
             cur[b] = off;
@@ -513,6 +518,8 @@ __global__ __launch_bounds__(1024) void flat_tail_kernel(FlatPlanArgs a)
         const int bk = bucket(v);
         if (bk >= thr)
             a.waves[pos++] = v;
+        else if (snake)
+            a.waves[one_round_pos(atomicAdd(&cur[bk], 1), nw, a.n_simd)] = v;
         else
             a.waves[nbulk + atomicAdd(&cur[bk], 1)] = v;
     }

@@ -894,6 +894,25 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             lw.swap(ordered);
             seg_tail = int(K);   // the persistent pass's shared tail queue
         }
+        // One round (every wave resident at once) of unequal waves: snake order
+        // over the SIMDs by modelled duration (kernels.hpp one_round_pos).
+        const size_t nsimd = 4 * size_t(dv.n_cu);
+        if (!grid && nw > nsimd && nw <= kSegWavesPerSimd * nsimd && cmax * 20 > cmin * 21 &&
+            env_i64("HC_PHMM_ONE_ROUND_SNAKE", 1) != 0) {
+            std::vector<uint64_t>& key = S.wkey;
+            key.resize(nw);
+            for (size_t k = 0; k < nw; ++k) {
+                const uint64_t c = uint64_t(13 * lw[k].ncols + 26) * uint64_t(lw[k].nsteps);
+                key[k] = (~c & 0xffffffffull) << 32 | k;   // descending cost, ties in packing order
+            }
+            std::sort(key.begin(), key.end());
+            std::vector<LaneWave>& ordered = S.ordered;
+            ordered.resize(nw);
+            for (size_t r = 0; r < nw; ++r)
+                ordered[size_t(one_round_pos(int(r), int(nw), int(nsimd)))] = lw[key[r] & 0xffffffffu];
+            lw.swap(ordered);
+            seg_tail = 0;
+        }
     }
     tm.mark("seg pack");
     const int n_seg_waves = dev_plan ? int(gd.waves) : int(lw.size());
