@@ -125,3 +125,22 @@ def test_region_plan_policy_keeps_two_waves_per_simd(L, monkeypatch, policy):
         assert len(waves) <= 2 * 1024 and set(waves[:, 3]) <= {46, 48}
     else:
         assert len(waves) > 2 * 1024
+
+
+@pytest.mark.parametrize("snake", ["1", "0"])
+def test_one_round_plan_balances_simds(L, monkeypatch, snake):
+    """configs[4] (S4: 2 000 waves of unequal length, all resident at once on
+    1 024 SIMDs): the snake order (kernels.hpp one_round_pos) pairs the
+    heaviest wave with the lightest on each SIMD — position p and p + 1 024
+    share one — so the busiest SIMD's modelled work drops from 1.3x the mean
+    to about 1.1x. The plan stays exact either way (HC_PHMM_ONE_ROUND_SNAKE)."""
+    monkeypatch.setenv("HC_PHMM_ONE_ROUND_SNAKE", snake)
+    b = W.config("S4")
+    args, keep = hcphmm._flat_args(b)
+    L.hcx_plan_pairs(*args, C.c_int(256), C.c_int(1), C.c_int(1))
+    pairs, order, n_seg, waves, used_grid = dump(L)
+    check_plan(pairs, order, n_seg, waves, b["R"].astype(np.int64), b["H"].astype(np.int64))
+    cost = (13 * waves[:, 3].astype(np.int64) + 26) * waves[:, 5]
+    sums = np.bincount(np.arange(len(waves)) % 1024, weights=cost, minlength=1024)
+    ratio = sums.max() / sums.mean()
+    assert (ratio < 1.15) if snake == "1" else (ratio > 1.2)
