@@ -792,7 +792,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
         a.waves = b->d_lane_waves;
         a.waves_tmp = reinterpret_cast<LaneWave*>(dev + o_wtmp);
         a.tail = tail;
-        a.n_simd = env_i64("HC_PHMM_ONE_ROUND_SNAKE", 1) != 0 ? 4 * dv.n_cu : 0;
+        a.n_simd = env_i64("HC_PHMM_ONE_ROUND_SNAKE", 0) != 0 ? 4 * dv.n_cu : 0;
         a.max_waves = int(max_waves);
         a.nwaves = reinterpret_cast<int*>(dev + o_nw);
         a.counters = b->d_count;

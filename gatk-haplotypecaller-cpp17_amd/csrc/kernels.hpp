@@ -433,7 +433,7 @@ struct FlatPlanArgs {
     int* nwaves;           // the plan's wave count
     int tail;              // waves dispatched last, longest first (0: packing order)
     int n_simd;            // one-round plans (waves within the resident slots): snake order over
-                           // the SIMDs (one_round_pos), 0 = off
+                           // the SIMDs (one_round_pos), 0 = off (default: measured no faster)
     int* counters;         // kNumCounters run counters, zeroed
     int* list;             // the rescue list (n entries), zeroed (the fused pass's queue)
 };

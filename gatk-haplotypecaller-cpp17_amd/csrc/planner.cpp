@@ -896,9 +896,13 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         }
         // One round (every wave resident at once) of unequal waves: snake order
         // over the SIMDs by modelled duration (kernels.hpp one_round_pos).
+        // Opt-in (HC_PHMM_ONE_ROUND_SNAKE=1): it cut S4's busiest-SIMD modelled
+        // sum from 1.30x the mean to 1.10x but not the pass (0.278 vs 0.274 ms):
+        // two waves of this pass on one SIMD are latency-bound, so the SIMD
+        // lasts as long as its longest wave, not the sum of its waves.
         const size_t nsimd = 4 * size_t(dv.n_cu);
         if (!grid && nw > nsimd && nw <= kSegWavesPerSimd * nsimd && cmax * 20 > cmin * 21 &&
-            env_i64("HC_PHMM_ONE_ROUND_SNAKE", 1) != 0) {
+            env_i64("HC_PHMM_ONE_ROUND_SNAKE", 0) != 0) {
             std::vector<uint64_t>& key = S.wkey;
             key.resize(nw);
             for (size_t k = 0; k < nw; ++k) {
