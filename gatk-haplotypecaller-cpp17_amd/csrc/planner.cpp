@@ -246,7 +246,9 @@ void grow(std::vector<T>& v, size_t n)
 // two waves issue alone or in a pair), up to 12 waves per SIMD (a region's
 // waves are alike, so the SIMDs holding one more wave set the pass); past
 // that, rounds follow the total work.
-int grid_policy(const Local& loc, const int32_t* rlen, const Cand* hcand, const float* waste, int n_simd)
+template <typename CandOf>
+int grid_policy(const Local& loc, const int32_t* rlen, CandOf&& hcand, const float* waste, int n_simd,
+                double* est_out = nullptr)
 {
     const PartSpec& spec = *loc.spec;
     int best_pol = -1;
@@ -263,7 +265,7 @@ int grid_policy(const Local& loc, const int32_t* rlen, const Cand* hcand, const 
             const int Rm = int((rs + B.nr / 2) / B.nr);
             cnt.clear();
             for (int h = 0; h < B.nh; ++h) {
-                const Cand cd = hcand[h0 + h];
+                const Cand cd = hcand(h0 + h);
                 const int q = pol >= 0 ? pol
                               : seg_cost(cd.nb[1], cd.bc[1], Rm, waste) < seg_cost(cd.nb[0], cd.bc[0], Rm, waste) ? 1
                                                                                                                  : 0;
@@ -279,7 +281,10 @@ int grid_policy(const Local& loc, const int32_t* rlen, const Cand* hcand, const 
                 work += w * (13.0 * bc + 26.0) * double(Rm + nb - 1);
             }
         }
-        if (waves <= 0) return -1;
+        if (waves <= 0) {
+            if (est_out) *est_out = 0;
+            return -1;
+        }
         const double per_simd = waves / double(n_simd);
         double rounds = per_simd;
         if (per_simd <= 12.0) {
@@ -292,6 +297,7 @@ int grid_policy(const Local& loc, const int32_t* rlen, const Cand* hcand, const 
             best_pol = pol;
         }
     }
+    if (est_out) *est_out = best;
     return best_pol;
 }
 
@@ -653,9 +659,37 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         one_ord.clear();
         ord2[0].clear();
         ord2[1].clear();
-        const int qgrid = qforce >= 0 || env_i64("HC_PHMM_GRID_POLICY", 1) == 0
-                              ? qforce
-                              : grid_policy(loc, rlen, hcand, waste, 4 * dv.n_cu);
+        // The width cap and candidate policy of a structured plan, priced over
+        // its actual waves (grid_policy) at every cap: the cap model's ~60
+        // filled lanes per wave misjudges haps that need more than 32 lanes
+        // (one pair per wave): a 415 x 8 region took 12-column blocks, 35
+        // lanes, one pair per wave, 3 320 waves (a fourth wave on a quarter
+        // of the SIMDs), where 16-column blocks give two pairs per wave and
+        // 1 660 waves.
+        int qgrid = qforce;
+        if (qforce < 0 && env_i64("HC_PHMM_GRID_POLICY", 1) != 0) {
+            const int n_simd = 4 * dv.n_cu;
+            double best = 0;
+            qgrid = grid_policy(loc, rlen, [&](int64_t h) { return hcand[h]; }, waste, n_simd, &best);
+            int best_cap = cap;
+            if (env_i64("HC_PHMM_SEG_CAP", 0) <= 0 && env_i64("HC_PHMM_GRID_CAPS", 1) != 0)
+                for (int c : kCaps) {
+                    if (c == cap) continue;
+                    double e = 0;
+                    const int q = grid_policy(loc, rlen, [&](int64_t h) { return cand_of(hlen[size_t(h)], c); }, waste,
+                                              n_simd, &e);
+                    if (e > 0 && e < best * 0.98) {
+                        best = e;
+                        best_cap = c;
+                        qgrid = q;
+                    }
+                }
+            if (best_cap != cap)
+                parallel_for(nh, [&](int64_t lo, int64_t hi) {
+                    for (int64_t h = lo; h < hi; ++h)
+                        if (hcls[size_t(h)] == 0) hcand[size_t(h)] = cand_of(hlen[size_t(h)], best_cap);
+                }, 1 << 14);
+        }
         cells_a = plan_grid(loc, rlen, hlen, row_off.data(), hap_w.data(), hcand, waste, qgrid, pd, !dev_plan, seg_ord, lw,
                             tm, dev_plan ? &gd : nullptr);
         tm.mark("grid: pairs");
