@@ -222,18 +222,6 @@ void grow(std::vector<T>& v, size_t n)
 }
 
 
-// Cross-product fast path of the planner (regions: hc_phmm_cross,
-// cross_regions, submit_regions) when every hap takes segmented waves. The
-// pairs of a block are reads x haps, so their sorted order need not be found
-// by sorting pairs: each hap takes one (BC, nb) candidate (chosen at its
-// block's mean read length), the block's haps are grouped by (BC, nb) and its
-// reads sorted by R, and a group's pairs in (read by R descending) x (hap)
-// order fill waves of floor(64 / nb) pairs — the order the general planner's
-// sort + greedy packing reaches on such a batch, built in one parallel pass
-// over segments (one per block and group; a segment's last wave may be
-// partial). Segments run widest block first, so co-resident waves share a
-// width's code. Writes every pair's descriptor, the slot order and the waves;
-// returns the batch's cells.
 // The candidate policy of a structured plan: each hap's cheaper candidate
 // (-1), or candidate 0 / 1 for every hap, whichever the pass model prices
 // lowest over the plan's actual waves. The per-hap choice can push a pass over
@@ -243,9 +231,11 @@ void grow(std::vector<T>& v, size_t n)
 // alone after the other two: fp32 pass 0.40 ms, where 9 lanes of 48 columns
 // (7 pairs, 1 898 waves, two per SIMD) take 0.21 ms. The model: a SIMD with n
 // waves takes 3 floor(n/3) rounds plus 2 for a partial round (its last one or
-// two waves issue alone or in a pair), up to 12 waves per SIMD (a region's
+// two waves issue alone or in a pair), up to 9 waves per SIMD (a region's
 // waves are alike, so the SIMDs holding one more wave set the pass); past
-// that, rounds follow the total work.
+// that, rounds follow the total work (priced up to 12, it moved a 415 x 200
+// region to 11 858 narrower waves: 1.32 -> 1.43 ms; up to 6, it left a
+// 415 x 128 region at 6 491 waves where 5 903 take 4 % less).
 template <typename CandOf>
 int grid_policy(const Local& loc, const int32_t* rlen, CandOf&& hcand, const float* waste, int n_simd,
                 double* est_out = nullptr)
@@ -287,7 +277,7 @@ int grid_policy(const Local& loc, const int32_t* rlen, CandOf&& hcand, const flo
         }
         const double per_simd = waves / double(n_simd);
         double rounds = per_simd;
-        if (per_simd <= 12.0) {
+        if (per_simd <= 9.0) {
             const int n = std::max(1, int(std::ceil(per_simd - 1e-9)));
             rounds = 3.0 * (n / 3) + (n % 3 ? 2.0 : 0.0);
         }
@@ -301,6 +291,18 @@ int grid_policy(const Local& loc, const int32_t* rlen, CandOf&& hcand, const flo
     return best_pol;
 }
 
+// Cross-product fast path of the planner (regions: hc_phmm_cross,
+// cross_regions, submit_regions) when every hap takes segmented waves. The
+// pairs of a block are reads x haps, so their sorted order need not be found
+// by sorting pairs: each hap takes one (BC, nb) candidate (chosen at its
+// block's mean read length), the block's haps are grouped by (BC, nb) and its
+// reads sorted by R, and a group's pairs in (read by R descending) x (hap)
+// order fill waves of floor(64 / nb) pairs — the order the general planner's
+// sort + greedy packing reaches on such a batch, built in one parallel pass
+// over segments (one per block and group; a segment's last wave may be
+// partial). Segments run widest block first, so co-resident waves share a
+// width's code. Writes every pair's descriptor, the slot order and the waves;
+// returns the batch's cells.
 int64_t plan_grid(const Local& loc, const int32_t* rlen, const int32_t* hlen, const int64_t* row_off,
                   const int64_t* hap_w, const Cand* hcand, const float* waste, int qforce, PairDesc* pd,
                   bool write_pairs, std::vector<int>& seg_ord, std::vector<LaneWave>& lw, PhaseTimer& tm,
