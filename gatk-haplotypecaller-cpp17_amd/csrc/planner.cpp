@@ -673,6 +673,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             const int n_simd = 4 * dv.n_cu;
             double best = 0;
             qgrid = grid_policy(loc, rlen, [&](int64_t h) { return hcand[h]; }, waste, n_simd, &best);
+            const double best_default = best;
             int best_cap = cap;
             if (env_i64("HC_PHMM_SEG_CAP", 0) <= 0 && env_i64("HC_PHMM_GRID_CAPS", 1) != 0)
                 for (int c : kCaps) {
@@ -680,7 +681,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
                     double e = 0;
                     const int q = grid_policy(loc, rlen, [&](int64_t h) { return cand_of(hlen[size_t(h)], c); }, waste,
                                               n_simd, &e);
-                    if (e > 0 && e < best * 0.98) {
+                    if (e > 0 && e < best * 0.98 && e < best_default * 0.95) {   // (another cap only for a clear gain)
                         best = e;
                         best_cap = c;
                         qgrid = q;
