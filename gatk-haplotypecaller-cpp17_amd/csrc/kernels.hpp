@@ -213,6 +213,7 @@ struct LaneArgs {
     // fp64 pass gathers the records into the per-pair outputs (Seg64Args).
     uint4* rec;
     int prio;   // 1: issue priority by remaining steps (seg_common.hpp set_prio_by_remaining)
+    int prio_from;   // prio 2: only waves wid >= prio_from (the last round of slots) take it
     const PairDesc* sdesc;   // seg slots' pair descriptors in slot order (pairs[order[slot]])
     // No fp64 launch after this pass (run.cpp: small parts of seg waves only,
     // every hap within kInWaveRescueMaxH): each flagged pair is rescued in its

@@ -447,7 +447,8 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
     const uint32_t w1 = row_word(cx, 0);
     const float T0 = row0_t<float>(a.lut, w1, cx.H);
     const bool wave_eq = __builtin_amdgcn_ballot_w64(!read_eq(w1)) == 0;
-    const SegSteps st{wv.rmax, wv.rmin, wv.nsteps, a.prio};
+    const int prio = a.prio == 2 ? (wid >= a.prio_from ? 1 : 0) : a.prio;   // (wave-uniform)
+    const SegSteps st{wv.rmax, wv.rmin, wv.nsteps, prio};
     float sumM = 0.f, sumX = 0.f;
     switch (bc) {
 #define HC_SEG_CASE(W) \

@@ -125,6 +125,9 @@ int run_part(Part* b, hipStream_t s)
             g.n_waves = b->n_seg_waves;
             g.n_waves_dev = b->d_nwaves;
             g.sdesc = b->d_sdesc;
+            // HC_PHMM_PRIO=2: priority by remaining steps for the waves of the
+            // last round of slots only (the pass's drain).
+            g.prio_from = std::max(0, b->n_seg_waves - 3 * 4 * dv.n_cu);   // (3: phmm_seg_kernel occupancy)
             // Persistent waves fetching from per-XCD queues
             // (HC_PHMM_SEG_PERSIST=1) or one queue (=2); default 0: one wave
             // per launched slot, the hardware dispatching them in order (the
