@@ -57,10 +57,16 @@ int run_part(Part* b, hipStream_t s)
     r.n_simd = 4 * dv.n_cu;
     r.n_pairs = int(b->n);
     // Issue priority by remaining steps (seg_common.hpp set_prio_by_remaining):
-    // on for the fp64 pass (S4: fp64 0.476 -> 0.462 ms), off for the fp32 pass
-    // (S2 8.66 -> 8.81 ms, 125k pairs 1.22 -> 1.25 ms); HC_PHMM_PRIO /
-    // HC_PHMM_PRIO64 override (A/B).
-    const int prio = int(env_i64("HC_PHMM_PRIO", 0));
+    // on for the fp64 pass (S4: fp64 0.476 -> 0.462 ms); for the fp32 pass on
+    // region parts (cross products) of at most 8 waves per SIMD — their waves
+    // are alike and the pass ends when each SIMD's last ones do, which the
+    // priority makes finish together (415 x 64 0.63 -> 0.59 ms, x 128 0.98 ->
+    // 0.94, x 144 1.09 -> 1.07; x 200, ten waves per SIMD: 1.37 -> 1.44,
+    // profiles/r05_prio_ab.txt) — and off for flat batches (S2 8.66 -> 8.81 ms,
+    // 125k pairs 1.22 -> 1.25 ms). HC_PHMM_PRIO / HC_PHMM_PRIO64 override (A/B).
+    const int prio = int(env_i64("HC_PHMM_PRIO", !b->spec.flat && b->n_seg_waves > 0 &&
+                                                      int64_t(b->n_seg_waves) <= int64_t(8) * 4 * dv.n_cu
+                                                  ? 1 : 0));
     r.prio = int(env_i64("HC_PHMM_PRIO64", 1));
     r.raw32 = b->d_raw32;
     r.flag = b->d_flag;
