@@ -150,13 +150,16 @@ void pack_nibbles_scalar(const uint8_t* __restrict s, int n, uint8_t* __restrict
 
 __attribute__((target("avx2"))) inline __m256i codes32(__m256i v)
 {
-    const __m256i kC = _mm256_set1_epi8('C'), kT = _mm256_set1_epi8('T'), kG = _mm256_set1_epi8('G'),
-                  kN = _mm256_set1_epi8('N');
-    return _mm256_or_si256(
-        _mm256_or_si256(_mm256_and_si256(_mm256_cmpeq_epi8(v, kC), _mm256_set1_epi8(1)),
-                        _mm256_and_si256(_mm256_cmpeq_epi8(v, kT), _mm256_set1_epi8(2))),
-        _mm256_or_si256(_mm256_and_si256(_mm256_cmpeq_epi8(v, kG), _mm256_set1_epi8(3)),
-                        _mm256_and_si256(_mm256_cmpeq_epi8(v, kN), _mm256_set1_epi8(4))));
+    // Two nibble lookups instead of four compares: the low nibble gives the
+    // code (A 1 -> 0, C 3 -> 1, T 4 -> 2, G 7 -> 3, N E -> 4) and the high
+    // nibble that byte must have (4, or 5 for T); any other byte -> 0.
+    const __m256i lo = _mm256_and_si256(v, _mm256_set1_epi8(0x0f));
+    const __m256i hi = _mm256_and_si256(_mm256_srli_epi16(v, 4), _mm256_set1_epi8(0x0f));
+    const __m256i code_lut = _mm256_setr_epi8(0, 0, 0, 1, 2, 0, 0, 3, 0, 0, 0, 0, 0, 0, 4, 0,   //
+                                              0, 0, 0, 1, 2, 0, 0, 3, 0, 0, 0, 0, 0, 0, 4, 0);
+    const __m256i hi_lut = _mm256_setr_epi8(16, 16, 16, 4, 5, 16, 16, 4, 16, 16, 16, 16, 16, 16, 4, 16,   //
+                                            16, 16, 16, 4, 5, 16, 16, 4, 16, 16, 16, 16, 16, 16, 4, 16);
+    return _mm256_and_si256(_mm256_cmpeq_epi8(_mm256_shuffle_epi8(hi_lut, lo), hi), _mm256_shuffle_epi8(code_lut, lo));
 }
 
 // 32 bytes -> 16 nibble bytes.
