@@ -259,7 +259,6 @@ struct Part {
     } cls[2];
     int n_lane = 0;
     int n_seg_waves = 0;
-    int seg_bc_max = 64;             // widest seg block of the plan (the narrow kernel instance fits up to kSegNarrowBC)
     int seg_tail = 0;                // last seg waves in LPT order: the persistent pass's tail queue
     int lane_waves = 0;
     int lane_variant = 0;

@@ -691,11 +691,6 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     b->Hmax = hmax;
     b->n_lane = int(n);
     b->n_seg_waves = int(max_waves);
-    {
-        int m = 0;   // the widest candidate any pair may take (the device picks per pair)
-        for (int g = 0; g < ngroups; ++g) m = std::max(m, int(keys[size_t(g)] >> 8));
-        b->seg_bc_max = m > 0 ? m : 64;
-    }
     b->seg_tail = tail;
     b->lane_waves = int(max_waves);
     b->d_nwaves = reinterpret_cast<int*>(dev + o_nw);

@@ -76,9 +76,6 @@ constexpr int kSegDone = kSegHeads + kSegQueues * kSegHeadStride;
 // entries (seg_common.hpp fused_rescues). One head made every finishing wave
 // retry a compare-and-swap on the same word: S4's pass took 22 ms.
 constexpr int kFusedQueues = 32;
-// The narrow instance of the fp32 seg kernel (LaneArgs::narrow_occ4): blocks
-// of at most this many columns fit 128 VGPRs, 4 waves per SIMD.
-constexpr int kSegNarrowBC = 16;
 constexpr int kFusedHeads = kSegDone + 16;   // [2][kFusedQueues], by run parity
 constexpr int kNumCounters = kFusedHeads + 2 * kFusedQueues;
 static_assert(kNumCounters <= 256, "the prep kernels zero the counters with one 256-thread block");
@@ -247,7 +244,6 @@ struct LaneArgs {
     int* err;             // the part's error word (kErrWord)
     int force_wait_timeout;   // test hook (HC_PHMM_TEST_PLAN_TIMEOUT=1): a wave reaching the queue gives up at once
     int prio64;           // the fused pass's fp64 rescues: issue priority by remaining steps (as Seg64Args::prio)
-    int narrow_occ4;      // every seg wave at most kSegNarrowBC columns: the 4-waves-per-SIMD instance
     int fz_prio;          // 1: fp32 work at issue priority 2, queued rescues at 0 (they fill the issue
                           // cycles the pass's waves leave idle instead of slowing its last waves)
 };

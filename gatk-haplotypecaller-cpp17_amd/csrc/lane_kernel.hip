@@ -399,7 +399,7 @@ __device__ void plan_rescue(const Seg64Args& a, int n, PlanLds& L)
 // One column-segmented wave (wid) of the fp32 pass. FUSED: the fused pass
 // (LaneArgs::fz_*): flagged pairs go to the queue, then the wave takes queued
 // rescues (seg_common.hpp fused_rescues); nw = the launch's waves.
-template <bool FUSED = false, int MAXWI = 0, int MAXBC = 64>
+template <bool FUSED = false, int MAXWI = 0>
 __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float* __restrict__ slut, int nw = 0,
                                          double* __restrict__ slut64 = nullptr)
 {
@@ -452,9 +452,7 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
     float sumM = 0.f, sumX = 0.f;
     switch (bc) {
 #define HC_SEG_CASE(W) \
-    case W: \
-        if constexpr (W <= MAXBC) run_seg_bc<float, W>(a.lut, slut, st, lane, s, cx, T0, sumM, sumX, mt, wave_eq); \
-        break;
+    case W: run_seg_bc<float, W>(a.lut, slut, st, lane, s, cx, T0, sumM, sumX, mt, wave_eq); break;
         HC_SEG_WIDTHS(HC_SEG_CASE)
 #undef HC_SEG_CASE
     default: break;
@@ -536,7 +534,7 @@ __device__ __forceinline__ int seg_fetch(int* head)
 // FUSED: the fused pass (LaneArgs::fz_*); its rescues take fp64 blocks up to
 // seg64_width(MAXWI) columns: 32 at 2 waves per SIMD (haps up to 2 048), 8 at
 // the fp32 pass's 3 (haps up to 512, the in-wave rescue's registers).
-template <int OCC, bool FUSED = false, int MAXWI = 0, int MAXBC = 64>
+template <int OCC, bool FUSED = false, int MAXWI = 0>
 __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
 {
     // Each wave fills its own copy of the prior tables: no workgroup barrier
@@ -566,7 +564,7 @@ __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
     float* slut = sluts[wib];
     for (int t = __lane_id(); t < kSlutLen; t += 64) slut[t] = a.lut[t];
     __builtin_amdgcn_wave_barrier();
-    seg_wave<FUSED, MAXWI, MAXBC>(a, wid, slut, n_waves, FUSED ? sluts64[wib] : nullptr);
+    seg_wave<FUSED, MAXWI>(a, wid, slut, n_waves, FUSED ? sluts64[wib] : nullptr);
 }
 
 // The persistent form (a separate instance: its fetch loop around the width
@@ -856,8 +854,6 @@ hipError_t launch_lane_seg_f32(const LaneArgs& a, int max_waves, int queues, hip
             hipLaunchKernelGGL((phmm_seg_persist_kernel<kSegOcc, 8>), dim3(max_blocks), dim3(64 * kSegWPB), 0, s, a);
         else
             hipLaunchKernelGGL((phmm_seg_persist_kernel<kSegOcc, 1>), dim3(max_blocks), dim3(64 * kSegWPB), 0, s, a);
-    } else if (a.narrow_occ4) {   // every wave at most kSegNarrowBC columns: 4 waves per SIMD
-        hipLaunchKernelGGL((phmm_seg_kernel<4, false, 0, kSegNarrowBC>), dim3(grid), dim3(64 * kSegWPB), 0, s, a);
     } else {
         hipLaunchKernelGGL((phmm_seg_kernel<kSegOcc>), dim3(grid), dim3(64 * kSegWPB), 0, s, a);
     }

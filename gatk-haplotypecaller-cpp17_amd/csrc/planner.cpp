@@ -1150,14 +1150,6 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     b->Hmax = Hmax;
     b->n_lane = int(size_t(n_seg_slots) + one_ord.size());
     b->n_seg_waves = n_seg_waves;
-    {
-        int m = 0;
-        if (dev_plan)
-            for (const auto& g : gd.segs) m = std::max(m, g.bc);
-        else
-            for (const auto& w : lw) m = std::max(m, int(w.ncols));
-        b->seg_bc_max = m > 0 ? m : 64;
-    }
     b->seg_tail = seg_tail;
     b->lane_variant = lane_var;
     b->lane_waves = dev_plan ? n_seg_waves : int(lw.size());

@@ -218,10 +218,6 @@ int run_part(Part* b, hipStream_t s)
                 g.steal_count = b->d_count + kStealCount + par;
                 r.steal_count = g.steal_count;
             }
-            // Plans of narrow blocks only (<= kSegNarrowBC columns) on the
-            // 4-waves-per-SIMD instance (HC_PHMM_SEG_OCC4).
-            g.narrow_occ4 = persist == 0 && !g.fz_started && b->seg_bc_max <= kSegNarrowBC &&
-                            env_i64("HC_PHMM_SEG_OCC4", 0) != 0;
             HIP_TRY(launch_lane_seg_f32(g, max_waves, persist == 2 ? 1 : 8, fork ? b->side : s));
             if (fork) HIP_TRY(hipEventRecord(b->join, b->side));
         }
