@@ -1030,6 +1030,10 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         std::memcpy(host + o_gh, gd.hord.data(), sizeof(int) * gd.hord.size());
         upload = o_gh + sizeof(int) * gd.hord.size();
     }
+    // Reads (haps) per staging task: a region's few hundred reads go on this
+    // thread alone below HC_PHMM_FILL_GRAIN (a pool wake-up cost about what
+    // the packing of 415 reads does).
+    const int64_t fill_grain = std::max<int64_t>(1, env_i64("HC_PHMM_FILL_GRAIN", 256));
     int4* rdesc = reinterpret_cast<int4*>(host + o_rd);
     uint8_t* hb = reinterpret_cast<uint8_t*>(host + o_bases);
     uint8_t* hq = reinterpret_cast<uint8_t*>(host + o_quals);
@@ -1050,7 +1054,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             }
             rdesc[r] = make_int4(int(o), v.len, g, go);
         }
-    }, 256);
+    }, fill_grain);
     int4* hdesc = reinterpret_cast<int4*>(host + o_hd);
     uint8_t* hbytes = reinterpret_cast<uint8_t*>(host + o_hb);
     parallel_for(nh, [&](int64_t b, int64_t e) {
@@ -1059,7 +1063,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
             pack_nibbles(v.bases, v.len, hbytes + hap_b[size_t(h)]);
             hdesc[h] = make_int4(int(hap_b[size_t(h)]), v.len, int(hap_w[size_t(h)]), 0);
         }
-    }, 256);
+    }, fill_grain);
     tm.mark("staging fill");
     if (dry) {
         // Dry runs keep the last part's plan for the host-logic tests
