@@ -115,6 +115,10 @@ struct Device {
     std::vector<Slot*> slots;
     double outstanding = 0;   // cells submitted and not yet collected
     Ring ring;
+    // Host staging time of flat parts (scan + fill), ns per cell, a running
+    // mean over the calls so far (0: none yet): sizes a call's parts
+    // (api.cpp submit_flat, HC_PHMM_PART_GROWTH_PCT).
+    std::atomic<double> stage_ns_per_cell{0.0};
 };
 
 // Engine state, guarded by g_mu: the device list, the slot pools, the
@@ -219,6 +223,12 @@ struct PartSpec {
     // is per IntelPairHMM instance (intel_pairhmm.hpp:58,81), so a later init
     // from another thread must not switch the mode of work already submitted.
     uint32_t flags = 0;
+    // Parts below this many pairs write results in place instead of per-slot
+    // records (run.cpp); -1: HC_PHMM_REC_MIN_PAIRS (200 000). A part of a
+    // pipelined call takes 40 000: its gather's latency is hidden behind the
+    // next part's staging.
+    int64_t rec_min = -1;
+    double cells = 0;   // R x H summed over the part's pairs (flat parts)
 };
 
 // Planning modes: a real part (device calls), or a dry run that plans on the

@@ -20,6 +20,7 @@
 #include <immintrin.h>
 
 #include <algorithm>
+#include <chrono>
 #include <array>
 #include <atomic>
 #include <cstring>
@@ -486,6 +487,9 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
 {
     *out = nullptr;
     PhaseTimer tm;
+    using clk = std::chrono::steady_clock;
+    const clk::time_point t_begin = clk::now();
+    clk::duration t_stage{};   // scan + fill: the host staging rate (Device::stage_ns_per_cell)
     const int64_t lo = spec.lo, n = spec.hi - spec.lo;
     if (n <= 0 || n > (int64_t(1) << 31) - 1) return HC_PHMM_OK;
     FlatScratch& S = t_fs;
@@ -502,6 +506,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     int32_t* hsamp = S.hsamp.data();
 
     scan_pass(src, lo, n, scan_gaps, mini, gapw, fmtw, hsamp, stride);
+    t_stage += clk::now() - t_begin;
     tm.mark("flat: scan");
 
     int rmax = 0, rmin = INT32_MAX, hmax = 0, hmin = INT32_MAX;
@@ -745,6 +750,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     std::atomic<bool> varying{false};
     auto enqueue = [&]() -> int {
         // Pass 2: chunks through the ring, each H2D'd as soon as it is filled.
+        const clk::time_point t_fill = clk::now();
         {
             std::lock_guard<std::mutex> lk(dv.ring.mu);
             for (size_t c = 0; c + 1 < chunk_m.size(); ++c) {
@@ -767,6 +773,12 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
             }
         }
         tm.mark("flat: fill + H2D");
+        t_stage += clk::now() - t_fill;
+        if (spec.cells > 0) {   // running mean over calls (weight 1/2 to the newest part)
+            const double ns = std::chrono::duration<double, std::nano>(t_stage).count() / spec.cells;
+            const double old_ns = dv.stage_ns_per_cell.load(std::memory_order_relaxed);
+            dv.stage_ns_per_cell.store(old_ns > 0 ? 0.5 * (old_ns + ns) : ns, std::memory_order_relaxed);
+        }
         if (!b->slot_ev)
             for (auto& e : b->pack_ev) HIP_TRY(hipEventCreate(&e));
         HIP_TRY(hipMemcpyAsync(dev + o_tab, host, tab_bytes, hipMemcpyHostToDevice, ps));
@@ -800,6 +812,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
         a.nwaves = reinterpret_cast<int*>(dev + o_nw);
         a.counters = b->d_count;
         a.list = b->d_list;
+        a.prep_blocks = int(env_i64("HC_PHMM_PREP_BLOCKS", 0));
         HIP_TRY(launch_flat_plan(a, ps));
         HIP_TRY(hipEventRecord(b->pack_ev[1], ps));
         if (ps != s) HIP_TRY(hipStreamWaitEvent(s, b->pack_ev[1], 0));

@@ -437,6 +437,7 @@ struct FlatPlanArgs {
                            // the SIMDs (one_round_pos), 0 = off (default: measured no faster)
     int* counters;         // kNumCounters run counters, zeroed
     int* list;             // the rescue list (n entries), zeroed (the fused pass's queue)
+    int prep_blocks;       // flat_prep_kernel's grid bound (0: a wave per pair, up to 65 536 blocks)
 };
 hipError_t launch_flat_plan(const FlatPlanArgs& a, hipStream_t s);
 // bytes (a multiple of 16, both 16-byte aligned) from device memory to mapped

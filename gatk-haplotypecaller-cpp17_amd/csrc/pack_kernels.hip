@@ -36,16 +36,22 @@ __device__ __forceinline__ uint32_t zero_nibbles(uint32_t t) { return ~(t | (t >
 // columns 32 * (w) + 1 .. 32 * (w + 1), w = base / 32 + q; all 64 lanes take part.
 __device__ __forceinline__ void hap_words(uint32_t x, int nv, int base, int nw, uint32_t* __restrict__ o, int lane)
 {
-    const uint32_t vmask = nv >= 8 ? 0x11111111u : (nv > 0 ? 0x11111111u & ((1u << (4 * nv)) - 1u) : 0u);
-    const uint32_t isN = zero_nibbles(x ^ 0x44444444u);
+    // Nibble order reversed first (column 8 * lane + 7 - k in nibble k), so
+    // the match bits come out MSB first by a three-step compress of the
+    // nibbles' bit 0 (6 ops per read code instead of an 8-step gather of 24;
+    // equal for every input, checked exhaustively over random words and nv).
+    const uint32_t y = __builtin_bswap32(x);
+    const uint32_t xr = ((y >> 4) & 0x0f0f0f0fu) | ((y & 0x0f0f0f0fu) << 4);
+    const uint32_t vmask = nv >= 8 ? 0x11111111u : (nv > 0 ? 0x11111111u & ~((1u << (4 * (8 - nv))) - 1u) : 0u);
+    const uint32_t isN = zero_nibbles(xr ^ 0x44444444u);
     uint32_t word[5];
 #pragma unroll
     for (int rc = 0; rc < 5; ++rc) {
         // read code rc matches: equal code, hap 'N' (matches every rc), or read 'N'
-        const uint32_t eq = (rc == 4 ? 0x11111111u : (zero_nibbles(x ^ (uint32_t(rc) * 0x11111111u)) | isN)) & vmask;
-        uint32_t m = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) m |= ((eq >> (4 * j)) & 1u) << (7 - j);
+        uint32_t m = (rc == 4 ? 0x11111111u : (zero_nibbles(xr ^ (uint32_t(rc) * 0x11111111u)) | isN)) & vmask;
+        m = (m | (m >> 3)) & 0x03030303u;
+        m = (m | (m >> 6)) & 0x000f000fu;
+        m = (m | (m >> 12)) & 0xffu;
         const uint32_t m1 = __builtin_amdgcn_mov_dpp(int(m), 0x55, 0xf, 0xf, false);   // quad_perm [1,1,1,1]
         const uint32_t m2 = __builtin_amdgcn_mov_dpp(int(m), 0xaa, 0xf, 0xf, false);   // quad_perm [2,2,2,2]
         const uint32_t m3 = __builtin_amdgcn_mov_dpp(int(m), 0xff, 0xf, 0xf, false);   // quad_perm [3,3,3,3]
@@ -464,64 +470,110 @@ __global__ __launch_bounds__(256) void flat_waves_kernel(FlatPlanArgs a)
 // longest first, so the chip drains evenly; order inside a bucket arbitrary.
 __device__ __forceinline__ int wave_cost(const LaneWave& v) { return (13 * v.ncols + 26) * v.nsteps; }   // plan_model.hpp
 
+// One workgroup. Every pass reads the waves coalesced (thread t takes waves
+// t, t + 1024, ...; four loads in flight per thread) and the bucket prefix is
+// a block scan: the first form walked a contiguous run of ~50 waves per
+// thread (one dependent load per step) and found the tail threshold and the
+// bucket cursors with two serial loops over the 1 024 buckets on one thread,
+// 161 us of every 250k-pair part's preparation (profiles/r05_e2e_call_timeline.txt).
+// The bulk keeps packing order through a stable compaction per tile of 1 024
+// waves (wave ballots, then the block's wave counts).
+__device__ __forceinline__ int block_incl_scan(int v, int* part)
+{
+    const int t = threadIdx.x;
+    part[t] = v;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int u = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += u;
+        __syncthreads();
+    }
+    return part[t];
+}
+
 __global__ __launch_bounds__(1024) void flat_tail_kernel(FlatPlanArgs a)
 {
-    constexpr int NB = 1024;
+    constexpr int NB = 1024, K = 4;
     __shared__ int hist[NB], cur[NB], part[1024];
-    __shared__ int cmax_s, thr_s;
-    const int t = threadIdx.x;
+    __shared__ int cmax_s, thr_s, acc_s, wcnt[16];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int nw = *a.nwaves;
     const LaneWave* __restrict__ in = a.waves_tmp;
     hist[t] = 0;
     if (t == 0) cmax_s = 1;
     __syncthreads();
-    const int C = (nw + 1023) / 1024;
-    const int w0 = min(nw, t * C), w1 = min(nw, w0 + C);
     int m = 1;
-    for (int w = w0; w < w1; ++w) m = max(m, wave_cost(in[w]));
+    for (int w0 = t; w0 < nw; w0 += K * 1024) {
+        int c[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) c[k] = w0 + k * 1024 < nw ? wave_cost(in[w0 + k * 1024]) : 1;
+#pragma unroll
+        for (int k = 0; k < K; ++k) m = max(m, c[k]);
+    }
     atomicMax(&cmax_s, m);
     __syncthreads();
     const long long cm = cmax_s;
     auto bucket = [&](const LaneWave& v) { return int((long long)wave_cost(v) * (NB - 1) / cm); };
-    for (int w = w0; w < w1; ++w) atomicAdd(&hist[bucket(in[w])], 1);
+    for (int w0 = t; w0 < nw; w0 += K * 1024) {
+        int b[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) b[k] = w0 + k * 1024 < nw ? bucket(in[w0 + k * 1024]) : -1;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (b[k] >= 0) atomicAdd(&hist[b[k]], 1);
+    }
+    __syncthreads();
+    // incl[b] = waves in buckets 0..b. The tail threshold: the fewest lowest
+    // buckets holding at least `tail` waves.
+    const int hb = hist[t];
+    const int incl = block_incl_scan(hb, part);
+    if (t == 0) {
+        thr_s = a.tail > 0 ? NB : 0;   // (NB: fewer than `tail` waves in all)
+        acc_s = a.tail > 0 ? part[NB - 1] : 0;
+    }
+    __syncthreads();
+    if (a.tail > 0 && incl >= a.tail && incl - hb < a.tail) {   // the one bucket where the prefix reaches tail
+        thr_s = t + 1;
+        acc_s = incl;
+    }
     __syncthreads();
     // One round (every wave resident at once, waves of unequal length): all
     // waves in snake order over the SIMDs (kernels.hpp one_round_pos).
     const bool snake = a.n_simd > 0 && nw > a.n_simd && nw <= 3 * a.n_simd;
-    if (t == 0) {   // the smallest bucket threshold holding at least `tail` waves below it
-        int acc = 0, thr = 0;
-        while (thr < NB && acc < a.tail) acc += hist[thr++];
-        thr_s = snake ? NB : acc >= nw ? 0 : thr;   // nothing to gain when every wave is in the tail
-        int off = 0;   // tail buckets longest first
-        for (int b = thr_s - 1; b >= 0; --b) {
-            cur[b] = off;
-            off += hist[b];
+    const int thr = snake ? NB : (acc_s >= nw ? 0 : thr_s);   // nothing to gain when every wave is in the tail
+    // tail buckets longest first: bucket b's first position is the count in buckets (b, thr)
+    if (t < thr) cur[t] = part[thr - 1] - incl;
+    const int nbulk = nw - (thr > 0 ? part[thr - 1] : 0);
+    __syncthreads();
+    int base = 0;
+    for (int w0 = 0; w0 < nw; w0 += K * 1024) {
+        LaneWave v[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (w0 + k * 1024 + t < nw) v[k] = in[w0 + k * 1024 + t];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int w = w0 + k * 1024 + t;
+            const int bk = w < nw ? bucket(v[k]) : -1;
+            const bool bulk = bk >= thr;
+            const uint64_t bal = __builtin_amdgcn_ballot_w64(bulk);
+            if (lane == 0) wcnt[wv] = __popcll(bal);
+            __syncthreads();
+            int off = 0, tot = 0;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int c = wcnt[q];
+                off += q < wv ? c : 0;
+                tot += c;
+            }
+            __syncthreads();   // wcnt is rewritten by the next tile
+            if (bulk)
+                a.waves[base + off + __popcll(bal & ((1ull << lane) - 1))] = v[k];
+            else if (bk >= 0)
+                a.waves[snake ? one_round_pos(atomicAdd(&cur[bk], 1), nw, a.n_simd) : nbulk + atomicAdd(&cur[bk], 1)] = v[k];
+            base += tot;
         }
-    }
-    __syncthreads();
-    const int thr = thr_s;
-    // the bulk (bucket >= thr) in packing order: chunk counts, block scan
-    int mine = 0;
-    for (int w = w0; w < w1; ++w) mine += bucket(in[w]) >= thr;
-    part[t] = mine;
-    __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {
-        const int v = t >= d ? part[t - d] : 0;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    const int nbulk = part[1023];
-    int pos = part[t] - mine;
-    for (int w = w0; w < w1; ++w) {
-        const LaneWave v = in[w];
-        const int bk = bucket(v);
-        if (bk >= thr)
-            a.waves[pos++] = v;
-        else if (snake)
-            a.waves[one_round_pos(atomicAdd(&cur[bk], 1), nw, a.n_simd)] = v;
-        else
-            a.waves[nbulk + atomicAdd(&cur[bk], 1)] = v;
     }
 }
 
@@ -571,7 +623,8 @@ hipError_t launch_flat_plan(const FlatPlanArgs& a, hipStream_t s)
     if (a.n <= 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(a.hist, 0, sizeof(int) * size_t(a.nbins), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(flat_prep_kernel, dim3(grid_for(a.n)), dim3(256), 0, s, a);
+    const int pg = a.prep_blocks > 0 ? std::min(grid_for(a.n), a.prep_blocks) : grid_for(a.n);
+    hipLaunchKernelGGL(flat_prep_kernel, dim3(pg), dim3(256), 0, s, a);
     hipLaunchKernelGGL(flat_scan_kernel, dim3(1), dim3(1024), 0, s, a);
     const int gs = std::min(8192, (a.n + 255) / 256);
     hipLaunchKernelGGL(flat_scatter_kernel, dim3(gs), dim3(256), 0, s, a);

@@ -154,7 +154,8 @@ int run_part(Part* b, hipStream_t s)
             // loads sit on the pass's critical path, and the scattered stores
             // they replace are a few MB: parts below HC_PHMM_REC_MIN_PAIRS
             // write their results in place.
-            const bool rec = b->d_rec && b->n >= env_i64("HC_PHMM_REC_MIN_PAIRS", 200000);
+            const int64_t rec_min = b->spec.rec_min >= 0 ? b->spec.rec_min : env_i64("HC_PHMM_REC_MIN_PAIRS", 200000);
+            const bool rec = b->d_rec && b->n >= rec_min;
             g.rec = rec ? b->d_rec : nullptr;
             r.rec = g.rec;   // the fp64 launch gathers the seg slots' records
             r.slot_of = b->d_slot_of;

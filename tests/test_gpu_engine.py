@@ -165,6 +165,25 @@ def test_early_finish(engine, oracle_lib, monkeypatch, early):
         assert_same(engine.pairs(b), ref, f"early={early}")
 
 
+@pytest.mark.parametrize("order", ["tail", "snake", "tail_blocks"])
+def test_flat_dispatch_order_vs_oracle(engine, oracle_lib, monkeypatch, order):
+    """The device-planned flat part's dispatch order (pack_kernels.hip
+    flat_tail_kernel: coalesced passes, block-scanned bucket cursors, stable
+    bulk compaction): a tail of shortest waves after the bulk (one round of
+    tail at ~6 000 waves), the one-round snake order (1 024 < waves <= 3 072),
+    and the tail with flat_prep_kernel on a bounded grid (several pairs per
+    wave); every pair against the oracle."""
+    if order == "snake":
+        monkeypatch.setenv("HC_PHMM_ONE_ROUND_SNAKE", "1")
+        b = W.generate(9000, (100, 500), (40, 250), 0.01, seed=61)
+    else:
+        monkeypatch.setenv("HC_PHMM_TAIL_ROUNDS", "1")
+        if order == "tail_blocks":
+            monkeypatch.setenv("HC_PHMM_PREP_BLOCKS", "64")
+        b = W.generate(30000, (100, 600), (40, 250), 0.01, seed=62)
+    assert_same(engine.pairs(b), oracle_lib.pairs(b, nthreads=16), order)
+
+
 def test_submit_regions_two_slots(two_slots, oracle_lib):
     regions = [W.region(n_reads=200, n_haps=int(nh), seed=300 + k) for k, nh in enumerate([4, 16, 2, 8])]
     ref = _regions_ref(oracle_lib, regions)

@@ -15,8 +15,15 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import hcphmm  # noqa: E402
 import workloads as W  # noqa: E402
 
-axes = [(a.split("=", 1)[0], a.split("=", 1)[1].split(",")) for a in sys.argv[1:]]
+# "@name:K=V;K=V" arguments name whole settings (compared as they are, no
+# cross product); the others are VAR=v1,v2 axes.
+presets = [a for a in sys.argv[1:] if a.startswith("@")]
+axes = [(a.split("=", 1)[0], a.split("=", 1)[1].split(",")) for a in sys.argv[1:] if not a.startswith("@")]
 combos = list(itertools.product(*[[(k, v) for v in vals] for k, vals in axes]))
+if presets:
+    combos = [(("preset", a[1:].split(":", 1)[0]),) + tuple(tuple(kv.split("=", 1)) for kv in a.split(":", 1)[1].split(";") if kv)
+              for a in presets]
+all_keys = {k for c in combos for k, _ in c if k != "preset"}
 hcphmm.init(0)
 b = W.config("S2")
 outs = [hcphmm.result_arrays(len(b["R"])) for _ in range(2)]
@@ -24,8 +31,11 @@ ref = None
 times = {c: [] for c in combos}
 for rnd in range(3):
     for c in combos:
+        for k in all_keys:   # a setting that leaves a variable out runs with it unset
+            os.environ.pop(k, None)
         for k, v in c:
-            os.environ[k] = v
+            if k != "preset":
+                os.environ[k] = v
         hcphmm.pairs(b, outs[0])
         if ref is None:
             ref = outs[0]["loglik"].copy()
