@@ -115,10 +115,10 @@ struct Device {
     std::vector<Slot*> slots;
     double outstanding = 0;   // cells submitted and not yet collected
     Ring ring;
-    // Host staging time of flat parts (scan + fill), ns per cell, a running
+    // Host staging time of flat parts (scan + fill), ps per cell, a running
     // mean over the calls so far (0: none yet): sizes a call's parts
     // (api.cpp submit_flat, HC_PHMM_PART_GROWTH_PCT).
-    std::atomic<double> stage_ns_per_cell{0.0};
+    std::atomic<double> stage_ps_per_cell{0.0};
 };
 
 // Engine state, guarded by g_mu: the device list, the slot pools, the

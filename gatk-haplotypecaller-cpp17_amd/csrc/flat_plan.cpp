@@ -489,7 +489,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     PhaseTimer tm;
     using clk = std::chrono::steady_clock;
     const clk::time_point t_begin = clk::now();
-    clk::duration t_stage{};   // scan + fill: the host staging rate (Device::stage_ns_per_cell)
+    clk::duration t_stage{};   // scan + fill: the host staging rate (Device::stage_ps_per_cell)
     const int64_t lo = spec.lo, n = spec.hi - spec.lo;
     if (n <= 0 || n > (int64_t(1) << 31) - 1) return HC_PHMM_OK;
     FlatScratch& S = t_fs;
@@ -775,9 +775,9 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
         tm.mark("flat: fill + H2D");
         t_stage += clk::now() - t_fill;
         if (spec.cells > 0) {   // running mean over calls (weight 1/2 to the newest part)
-            const double ns = std::chrono::duration<double, std::nano>(t_stage).count() / spec.cells;
-            const double old_ns = dv.stage_ns_per_cell.load(std::memory_order_relaxed);
-            dv.stage_ns_per_cell.store(old_ns > 0 ? 0.5 * (old_ns + ns) : ns, std::memory_order_relaxed);
+            const double ps = std::chrono::duration<double, std::pico>(t_stage).count() / spec.cells;
+            const double old_ps = dv.stage_ps_per_cell.load(std::memory_order_relaxed);
+            dv.stage_ps_per_cell.store(old_ps > 0 ? 0.5 * (old_ps + ps) : ps, std::memory_order_relaxed);
         }
         if (!b->slot_ev)
             for (auto& e : b->pack_ev) HIP_TRY(hipEventCreate(&e));
