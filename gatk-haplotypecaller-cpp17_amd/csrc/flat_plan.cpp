@@ -631,7 +631,8 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     // (planner.cpp: 125k-pair shard 1.39 -> 1.25 ms with it on the host plan).
     const int tail = int(std::max<int64_t>(0, env_i64("HC_PHMM_TAIL_ROUNDS", 2))) * 4 * dv.n_cu * 3;
     const size_t o_wtmp = L.take(tail > 0 ? sizeof(LaneWave) * size_t(max_waves) : 0);
-    const size_t o_nw = L.take(sizeof(int));
+    const size_t o_wcost = L.take(tail > 0 ? sizeof(int) * size_t(max_waves) : 0);
+    const size_t o_nw = L.take(2 * sizeof(int));   // wave count, then the largest modelled wave cost
     const size_t o_res = L.take(res_bytes);
     const size_t o_list = L.take(sizeof(int) * n1);
     const size_t o_rec = L.take(sizeof(uint4) * n1);   // seg slot records (every pair is a seg pair)
@@ -806,6 +807,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
         a.sdesc = b->d_sdesc;
         a.waves = b->d_lane_waves;
         a.waves_tmp = reinterpret_cast<LaneWave*>(dev + o_wtmp);
+        a.wcost = reinterpret_cast<int*>(dev + o_wcost);
         a.tail = tail;
         a.n_simd = env_i64("HC_PHMM_ONE_ROUND_SNAKE", 0) != 0 ? 4 * dv.n_cu : 0;
         a.max_waves = int(max_waves);

@@ -430,8 +430,9 @@ struct FlatPlanArgs {
     int4* sdesc;           // slot -> pair descriptor
     LaneWave* waves;       // the plan's waves (packing order), then the dispatch order
     LaneWave* waves_tmp;   // max_waves entries: the packing order while the tail is reordered
+    int* wcost;            // max_waves entries: each wave's modelled cost (with the tail)
     int max_waves;         // waves the launch covers (upper bound of the plan's)
-    int* nwaves;           // the plan's wave count
+    int* nwaves;           // the plan's wave count; [1]: its largest modelled wave cost (with the tail)
     int tail;              // waves dispatched last, longest first (0: packing order)
     int n_simd;            // one-round plans (waves within the resident slots): snake order over
                            // the SIMDs (one_round_pos), 0 = off (default: measured no faster)

@@ -375,7 +375,8 @@ __global__ __launch_bounds__(1024) void flat_scan_kernel(FlatPlanArgs a)
     const int C = (nbins + 1023) / 1024;
     const int b0 = min(nbins, t * C), b1 = min(nbins, b0 + C);
     int s = 0;
-    for (int i = b0; i < b1; ++i) s += a.hist[i];
+#pragma unroll 8
+    for (int i = b0; i < b1; ++i) s += a.hist[i];   // (independent loads: eight in flight)
     part[t] = s;
     __syncthreads();
     for (int d = 1; d < 1024; d <<= 1) {
@@ -386,6 +387,7 @@ __global__ __launch_bounds__(1024) void flat_scan_kernel(FlatPlanArgs a)
     }
     const int total = part[1023];
     int run = part[t] - s;
+#pragma unroll 8
     for (int i = b0; i < b1; ++i) {
         const int c = a.hist[i];
         a.hist[i] = run;
@@ -415,7 +417,10 @@ __global__ __launch_bounds__(1024) void flat_scan_kernel(FlatPlanArgs a)
         a.gtab[3 * t + 1] = cnt;
         a.gtab[3 * t + 2] = part[t] - wc;
     }
-    if (t == 0) *a.nwaves = part[1023];
+    if (t == 0) {
+        a.nwaves[0] = part[1023];
+        a.nwaves[1] = 1;   // the largest wave cost, raised by flat_waves_kernel
+    }
 }
 
 // Thread per pair: its slot (order inside a bin is arbitrary: a pair's result
@@ -430,11 +435,15 @@ __global__ __launch_bounds__(256) void flat_scatter_kernel(FlatPlanArgs a)
     }
 }
 
+// Modelled wave duration (plan_model.hpp).
+__device__ __forceinline__ int wave_cost(const LaneWave& v) { return (13 * v.ncols + 26) * v.nsteps; }   // plan_model.hpp
+
 // Thread per wave: its group by binary search over the groups' first waves,
 // its slots, and its row bounds from its pairs.
 __global__ __launch_bounds__(256) void flat_waves_kernel(FlatPlanArgs a)
 {
     const int nw = *a.nwaves;
+    int cmax = 1;
     for (int w = blockIdx.x * 256 + threadIdx.x; w < nw; w += gridDim.x * 256) {
         int lo = 0, hi = a.ngroups;   // the last group whose first wave is <= w
         while (hi - lo > 1) {
@@ -461,6 +470,16 @@ __global__ __launch_bounds__(256) void flat_waves_kernel(FlatPlanArgs a)
         v.nsteps = rmax + g.y - 1;
         v.carry_row = 0;
         (a.tail > 0 ? a.waves_tmp : a.waves)[w] = v;
+        if (a.tail > 0) {
+            const int c = wave_cost(v);
+            a.wcost[w] = c;
+            cmax = max(cmax, c);
+        }
+    }
+    if (a.tail > 0) {   // the largest cost for flat_tail_kernel's buckets: wave max, one atomic per wave
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) cmax = max(cmax, __shfl_xor(cmax, d, 64));
+        if ((threadIdx.x & 63) == 0 && cmax > 1) atomicMax(a.nwaves + 1, cmax);
     }
 }
 
@@ -468,11 +487,11 @@ __global__ __launch_bounds__(256) void flat_waves_kernel(FlatPlanArgs a)
 // bulk in packing order (co-resident waves share one width's code), the
 // `tail` shortest waves (modelled duration BC x steps, in 1024 buckets) last,
 // longest first, so the chip drains evenly; order inside a bucket arbitrary.
-__device__ __forceinline__ int wave_cost(const LaneWave& v) { return (13 * v.ncols + 26) * v.nsteps; }   // plan_model.hpp
 
-// One workgroup. Every pass reads the waves coalesced (thread t takes waves
-// t, t + 1024, ...; four loads in flight per thread) and the bucket prefix is
-// a block scan: the first form walked a contiguous run of ~50 waves per
+// One workgroup. The waves' costs and their maximum come from
+// flat_waves_kernel (a 4-byte cost per wave, not the 32-byte wave); every
+// pass reads coalesced (thread t takes waves t, t + 1024, ...; four loads in
+// flight per thread) and the bucket prefix is a block scan: the first form walked a contiguous run of ~50 waves per
 // thread (one dependent load per step) and found the tail threshold and the
 // bucket cursors with two serial loops over the 1 024 buckets on one thread,
 // 161 us of every 250k-pair part's preparation (profiles/r05_e2e_call_timeline.txt).
@@ -496,29 +515,18 @@ __global__ __launch_bounds__(1024) void flat_tail_kernel(FlatPlanArgs a)
 {
     constexpr int NB = 1024, K = 4;
     __shared__ int hist[NB], cur[NB], part[1024];
-    __shared__ int cmax_s, thr_s, acc_s, wcnt[16];
+    __shared__ int thr_s, acc_s, wcnt[16];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int nw = *a.nwaves;
     const LaneWave* __restrict__ in = a.waves_tmp;
     hist[t] = 0;
-    if (t == 0) cmax_s = 1;
     __syncthreads();
-    int m = 1;
-    for (int w0 = t; w0 < nw; w0 += K * 1024) {
-        int c[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) c[k] = w0 + k * 1024 < nw ? wave_cost(in[w0 + k * 1024]) : 1;
-#pragma unroll
-        for (int k = 0; k < K; ++k) m = max(m, c[k]);
-    }
-    atomicMax(&cmax_s, m);
-    __syncthreads();
-    const long long cm = cmax_s;
-    auto bucket = [&](const LaneWave& v) { return int((long long)wave_cost(v) * (NB - 1) / cm); };
+    const long long cm = max(1, a.nwaves[1]);   // flat_waves_kernel's largest cost
+    auto bucket_c = [&](int c) { return int((long long)c * (NB - 1) / cm); };
     for (int w0 = t; w0 < nw; w0 += K * 1024) {
         int b[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) b[k] = w0 + k * 1024 < nw ? bucket(in[w0 + k * 1024]) : -1;
+        for (int k = 0; k < K; ++k) b[k] = w0 + k * 1024 < nw ? bucket_c(a.wcost[w0 + k * 1024]) : -1;
 #pragma unroll
         for (int k = 0; k < K; ++k)
             if (b[k] >= 0) atomicAdd(&hist[b[k]], 1);
@@ -549,13 +557,17 @@ __global__ __launch_bounds__(1024) void flat_tail_kernel(FlatPlanArgs a)
     int base = 0;
     for (int w0 = 0; w0 < nw; w0 += K * 1024) {
         LaneWave v[K];
+        int c[K];
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            if (w0 + k * 1024 + t < nw) v[k] = in[w0 + k * 1024 + t];
+            if (w0 + k * 1024 + t < nw) {
+                v[k] = in[w0 + k * 1024 + t];
+                c[k] = a.wcost[w0 + k * 1024 + t];
+            }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int w = w0 + k * 1024 + t;
-            const int bk = w < nw ? bucket(v[k]) : -1;
+            const int bk = w < nw ? bucket_c(c[k]) : -1;
             const bool bulk = bk >= thr;
             const uint64_t bal = __builtin_amdgcn_ballot_w64(bulk);
             if (lane == 0) wcnt[wv] = __popcll(bal);
