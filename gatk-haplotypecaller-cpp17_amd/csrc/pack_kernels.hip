@@ -279,10 +279,108 @@ __device__ __forceinline__ uint32_t hap_2b_nibbles(uint32_t h16)
     return x;
 }
 
-// One wave per pair (grid-stride): its rows, its hap table, its pair
-// descriptor, and its plan key — the cheaper of its two (block width, lanes)
-// candidates by the host planner's cost model, and the counting-sort bin of
-// (candidate group, R descending).
+// A flat pair's descriptor fields (wave-uniform) and the first chunk of its
+// record as this lane loaded it (raw words: converted only when packed, so a
+// prefetch never waits on its own loads).
+struct PrepIn {
+    const uint8_t* quals;
+    int R, H, ro, ho, gw, fmt;
+    uint32_t q4, c4, i4, d4, g4, hraw;
+    int2 c;
+};
+
+__device__ __forceinline__ void prep_load(const FlatPlanArgs& a, const FlatDesc& dn, int lane, PrepIn& x)
+{
+    const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(dn.rec & 0xffffffffll));
+    const unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(dn.rec >> 32));
+    x.quals = a.img + (long long)(((unsigned long long)hi << 32) | lo);
+    x.R = __builtin_amdgcn_readfirstlane(dn.R);
+    x.H = __builtin_amdgcn_readfirstlane(dn.H);
+    x.ro = __builtin_amdgcn_readfirstlane(dn.row_off);
+    x.ho = __builtin_amdgcn_readfirstlane(dn.hapw_off);
+    x.gw = __builtin_amdgcn_readfirstlane(dn.gapw);
+    x.fmt = __builtin_amdgcn_readfirstlane(dn.fmt);
+    const bool r1b = (x.fmt & kFmtRead1B) != 0, h2b = (x.fmt & kFmtHap2b) != 0;
+    const int qa = align4(x.R), qa4 = qa >> 2;
+    const uint32_t* __restrict__ q32 = reinterpret_cast<const uint32_t*>(x.quals);
+    const uint16_t* __restrict__ c16 = reinterpret_cast<const uint16_t*>(x.quals + qa);
+    const uint32_t* __restrict__ g32 = reinterpret_cast<const uint32_t*>(x.quals + qa + (r1b ? 0 : align4((x.R + 1) / 2)));
+    const uint32_t* __restrict__ h32 = g32 + (x.gw < 0 ? 3 * qa4 : 0);
+    const uint16_t* __restrict__ h16 = reinterpret_cast<const uint16_t*>(h32);
+    x.q4 = x.c4 = x.i4 = x.d4 = x.g4 = x.hraw = 0;
+    if (4 * lane < x.R) {
+        x.q4 = q32[lane];
+        if (!r1b) x.c4 = c16[lane];
+        if (x.gw < 0) {
+            x.i4 = g32[lane];
+            x.d4 = g32[qa4 + lane];
+            x.g4 = g32[2 * qa4 + lane];
+        }
+    }
+    if (8 * lane < x.H) x.hraw = h2b ? uint32_t(h16[lane]) : h32[lane];
+    x.c = a.ctab[x.H];
+}
+
+// Pair p's rows, hap table, descriptor and plan key from its prefetched first
+// chunk (longer reads and haps load their further chunks here).
+__device__ __forceinline__ void prep_pack(const FlatPlanArgs& a, const PrepIn& x, int p, int lane)
+{
+    const int R = x.R, H = x.H, gw = x.gw, fmt = x.fmt;
+    const bool r1b = (fmt & kFmtRead1B) != 0, h2b = (fmt & kFmtHap2b) != 0;
+    const uint32_t qbase4 = uint32_t((fmt >> 8) & 127) * 0x01010101u;
+    const int qa = align4(R), qa4 = qa >> 2;
+    const uint32_t* __restrict__ q32 = reinterpret_cast<const uint32_t*>(x.quals);
+    const uint16_t* __restrict__ c16 = reinterpret_cast<const uint16_t*>(x.quals + qa);
+    const uint32_t* __restrict__ g32 = reinterpret_cast<const uint32_t*>(x.quals + qa + (r1b ? 0 : align4((R + 1) / 2)));
+    const uint32_t* __restrict__ h32 = g32 + (gw < 0 ? 3 * qa4 : 0);
+    const uint16_t* __restrict__ h16 = reinterpret_cast<const uint16_t*>(h32);
+    uint32_t q4 = x.q4, c4 = x.c4, i4 = x.i4, d4 = x.d4, g4 = x.g4;
+    uint4* __restrict__ rows = reinterpret_cast<uint4*>(a.rows + x.ro);
+    for (int t0 = 0; 4 * t0 < R; t0 += 64) {
+        const int t = t0 + lane;
+        if (t0 > 0 && 4 * t < R) {
+            q4 = q32[t];
+            if (!r1b) c4 = c16[t];
+            if (gw < 0) {
+                i4 = g32[t];
+                d4 = g32[qa4 + t];
+                g4 = g32[2 * qa4 + t];
+            }
+        }
+        if (4 * t < R) {
+            uint32_t qq = q4, cc = c4;
+            if (r1b) read_1b_unpack(q4, qbase4, qq, cc);
+            rows[t] = rows_rec4(qq, cc, i4, d4, g4, gw, t == 0);
+        }
+    }
+    uint32_t* __restrict__ o = a.hapw + x.ho;
+    const int nw = (H + 31) / 32;
+    hap_zero_rows(nw, o, lane);
+    uint32_t hx = h2b ? hap_2b_nibbles(x.hraw) : x.hraw;
+    for (int base = 0; base < H; base += 512) {
+        const int nv = H - base - 8 * lane;   // valid columns of this lane (<= 0: none)
+        if (base > 0) hx = nv > 0 ? (h2b ? hap_2b_nibbles(h16[base / 8 + lane]) : h32[base / 8 + lane]) : 0u;
+        hap_words(hx, nv, base, nw, o, lane);
+    }
+    if (lane == 0) {
+        const int2 c = x.c;
+        a.pairs[p] = make_int4(x.ro, R, x.ho, H);
+        // modelled wave instructions of each candidate (plan_model.hpp seg_cost)
+        const int bc0 = c.x & 0xff, nb0 = (c.x >> 8) & 0xff, bc1 = c.y & 0xff, nb1 = (c.y >> 8) & 0xff;
+        const float k0 = float((long long)nb0 * (13 * bc0 + 26) * (R + nb0 - 1)) * a.waste[nb0];
+        const float k1 = float((long long)nb1 * (13 * bc1 + 26) * (R + nb1 - 1)) * a.waste[nb1];
+        const int g = k1 < k0 ? (c.y >> 16) : (c.x >> 16);
+        const int bin = g * a.rspan + ((a.rmax - R) >> a.rshift);
+        a.bin_of[p] = bin;
+        atomicAdd(&a.hist[bin], 1);
+    }
+}
+
+// Pairs in grid-stride order, software-pipelined two deep: while pair p is
+// packed, pair p + stride's record chunk and table entry and pair p + 2 *
+// stride's descriptor are in flight (one wave per pair left each wave's two
+// dependent load rounds exposed: 185 us per 250k-pair part; the launcher now
+// bounds the grid so each wave pipelines several pairs).
 __global__ __launch_bounds__(256) void flat_prep_kernel(FlatPlanArgs a)
 {
     if (blockIdx.x == 0 && threadIdx.x < kNumCounters) a.counters[threadIdx.x] = 0;
@@ -290,77 +388,17 @@ __global__ __launch_bounds__(256) void flat_prep_kernel(FlatPlanArgs a)
     const int lane = threadIdx.x & 63;
     const int stride = gridDim.x * 4;
     int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (p >= a.n) return;   // wave-uniform
+    PrepIn cur, nxt;
+    prep_load(a, a.desc[p], lane, cur);
     FlatDesc dn{};
-    if (p < a.n) dn = a.desc[p];
-    // As pack_items: the record's first chunk (rows and hap columns) is loaded
-    // before either is used and the next pair's descriptor while this one packs.
+    if (p + stride < a.n) dn = a.desc[p + stride];
     for (; p < a.n; p += stride) {
-        const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(dn.rec & 0xffffffffll));
-        const unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(dn.rec >> 32));
-        const uint8_t* quals = a.img + (long long)(((unsigned long long)hi << 32) | lo);
-        const int R = __builtin_amdgcn_readfirstlane(dn.R), H = __builtin_amdgcn_readfirstlane(dn.H);
-        const int ro = __builtin_amdgcn_readfirstlane(dn.row_off), ho = __builtin_amdgcn_readfirstlane(dn.hapw_off);
-        const int gw = __builtin_amdgcn_readfirstlane(dn.gapw);
-        const int fmt = __builtin_amdgcn_readfirstlane(dn.fmt);
-        if (p + stride < a.n) dn = a.desc[p + stride];
-        const bool r1b = (fmt & kFmtRead1B) != 0, h2b = (fmt & kFmtHap2b) != 0;
-        const uint32_t qbase4 = uint32_t((fmt >> 8) & 127) * 0x01010101u;
-        const int qa = align4(R);
-        const uint32_t* __restrict__ q32 = reinterpret_cast<const uint32_t*>(quals);
-        const uint16_t* __restrict__ c16 = reinterpret_cast<const uint16_t*>(quals + qa);
-        const uint32_t* __restrict__ g32 = reinterpret_cast<const uint32_t*>(quals + qa + (r1b ? 0 : align4((R + 1) / 2)));
-        const uint32_t* __restrict__ h32 = g32 + (gw < 0 ? 3 * (qa >> 2) : 0);
-        const uint16_t* __restrict__ h16 = reinterpret_cast<const uint16_t*>(h32);
-        const int qa4 = qa >> 2;
-        uint32_t q4 = 0, c4 = 0, i4 = 0, d4 = 0, g4 = 0, hx = 0;
-        if (4 * lane < R) {
-            q4 = q32[lane];
-            if (!r1b) c4 = c16[lane];
-            if (gw < 0) {
-                i4 = g32[lane];
-                d4 = g32[qa4 + lane];
-                g4 = g32[2 * qa4 + lane];
-            }
-        }
-        if (8 * lane < H) hx = h2b ? hap_2b_nibbles(h16[lane]) : h32[lane];
-        const int2 c = a.ctab[H];
-        uint4* __restrict__ rows = reinterpret_cast<uint4*>(a.rows + ro);
-        for (int t0 = 0; 4 * t0 < R; t0 += 64) {
-            const int t = t0 + lane;
-            if (t0 > 0 && 4 * t < R) {
-                q4 = q32[t];
-                if (!r1b) c4 = c16[t];
-                if (gw < 0) {
-                    i4 = g32[t];
-                    d4 = g32[qa4 + t];
-                    g4 = g32[2 * qa4 + t];
-                }
-            }
-            if (4 * t < R) {
-                uint32_t qq = q4, cc = c4;
-                if (r1b) read_1b_unpack(q4, qbase4, qq, cc);
-                rows[t] = rows_rec4(qq, cc, i4, d4, g4, gw, t == 0);
-            }
-        }
-        uint32_t* __restrict__ o = a.hapw + ho;
-        const int nw = (H + 31) / 32;
-        hap_zero_rows(nw, o, lane);
-        for (int base = 0; base < H; base += 512) {
-            const int nv = H - base - 8 * lane;   // valid columns of this lane (<= 0: none)
-            if (base > 0) hx = nv > 0 ? (h2b ? hap_2b_nibbles(h16[base / 8 + lane]) : h32[base / 8 + lane]) : 0u;
-            hap_words(hx, nv, base, nw, o, lane);
-        }
-        if (lane == 0) {
-            a.pairs[p] = make_int4(ro, R, ho, H);
-            // modelled wave instructions of each candidate (plan_model.hpp seg_cost)
-            const int bc0 = c.x & 0xff, nb0 = (c.x >> 8) & 0xff, bc1 = c.y & 0xff, nb1 = (c.y >> 8) & 0xff;
-            const float k0 = float((long long)nb0 * (13 * bc0 + 26) * (R + nb0 - 1)) * a.waste[nb0];
-            const float k1 = float((long long)nb1 * (13 * bc1 + 26) * (R + nb1 - 1)) * a.waste[nb1];
-            const int g = k1 < k0 ? (c.y >> 16) : (c.x >> 16);
-            const int bin = g * a.rspan + ((a.rmax - R) >> a.rshift);
-            a.bin_of[p] = bin;
-            atomicAdd(&a.hist[bin], 1);
-        }
+        const bool more = p + stride < a.n;
+        if (more) prep_load(a, dn, lane, nxt);
+        if (p + 2 * stride < a.n) dn = a.desc[p + 2 * stride];
+        prep_pack(a, cur, p, lane);
+        if (more) cur = nxt;
     }
 }
 
@@ -490,8 +528,8 @@ __global__ __launch_bounds__(256) void flat_waves_kernel(FlatPlanArgs a)
 
 // One workgroup. The waves' costs and their maximum come from
 // flat_waves_kernel (a 4-byte cost per wave, not the 32-byte wave); every
-// pass reads coalesced (thread t takes waves t, t + 1024, ...; four loads in
-// flight per thread) and the bucket prefix is a block scan: the first form walked a contiguous run of ~50 waves per
+// pass reads coalesced (thread t takes waves t, t + 1024, ...; two loads in
+// flight per thread: four spilled at this workgroup size) and the bucket prefix is a block scan: the first form walked a contiguous run of ~50 waves per
 // thread (one dependent load per step) and found the tail threshold and the
 // bucket cursors with two serial loops over the 1 024 buckets on one thread,
 // 161 us of every 250k-pair part's preparation (profiles/r05_e2e_call_timeline.txt).
@@ -513,7 +551,7 @@ __device__ __forceinline__ int block_incl_scan(int v, int* part)
 
 __global__ __launch_bounds__(1024) void flat_tail_kernel(FlatPlanArgs a)
 {
-    constexpr int NB = 1024, K = 4;
+    constexpr int NB = 1024, K = 2;
     __shared__ int hist[NB], cur[NB], part[1024];
     __shared__ int thr_s, acc_s, wcnt[16];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -635,7 +673,9 @@ hipError_t launch_flat_plan(const FlatPlanArgs& a, hipStream_t s)
     if (a.n <= 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(a.hist, 0, sizeof(int) * size_t(a.nbins), s);
     if (e != hipSuccess) return e;
-    const int pg = a.prep_blocks > 0 ? std::min(grid_for(a.n), a.prep_blocks) : grid_for(a.n);
+    // Bounded grid (HC_PHMM_PREP_BLOCKS; default 1 280 blocks: 5 waves per
+    // SIMD, the kernel's occupancy at 92 VGPRs): each wave pipelines several pairs.
+    const int pg = std::min(grid_for(a.n), a.prep_blocks > 0 ? a.prep_blocks : 1280);
     hipLaunchKernelGGL(flat_prep_kernel, dim3(pg), dim3(256), 0, s, a);
     hipLaunchKernelGGL(flat_scan_kernel, dim3(1), dim3(1024), 0, s, a);
     const int gs = std::min(8192, (a.n + 255) / 256);

@@ -16,10 +16,10 @@ for v in "$@"; do
   st=$(find $out -name '*kernel_stats.csv' | head -1)
   echo "== $tag ($envs)"
   python3 - "$st" <<'EOF'
-import csv, sys
+import csv, re, sys
 for r in csv.DictReader(open(sys.argv[1])):
-    n = r["Name"]
-    if any(k in n for k in ("flat_", "phmm_seg_kernel", "copyBuffer", "fillBuffer")):
-        print(f'  {n.split("(")[0][-48:]:48s} calls {r["Calls"]:>4s} avg {float(r["AverageNs"]) / 1e3:8.1f} us')
+    m = re.search(r"(flat_\w+|phmm_seg_kernel|phmm_seg64_kernel|copyBuffer|fillBufferAligned|store_to_host_kernel)", r["Name"])
+    if m:
+        print(f'  {m.group(1):24s} calls {r["Calls"]:>4s} avg {float(r["AverageNs"]) / 1e3:8.1f} us')
 EOF
 done
