@@ -673,9 +673,11 @@ hipError_t launch_flat_plan(const FlatPlanArgs& a, hipStream_t s)
     if (a.n <= 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(a.hist, 0, sizeof(int) * size_t(a.nbins), s);
     if (e != hipSuccess) return e;
-    // Bounded grid (HC_PHMM_PREP_BLOCKS; default 1 280 blocks: 5 waves per
-    // SIMD, the kernel's occupancy at 92 VGPRs): each wave pipelines several pairs.
-    const int pg = std::min(grid_for(a.n), a.prep_blocks > 0 ? a.prep_blocks : 1280);
+    // Bounded grid (HC_PHMM_PREP_BLOCKS; default 2 560 blocks, two rounds of
+    // the kernel's 5 waves per SIMD at 92 VGPRs): each wave pipelines several
+    // pairs. Per part beside the passes (tools/prep_prof.sh): 144 us vs 186
+    // one wave per pair, 204 at 1 280 blocks, 250 at 640.
+    const int pg = std::min(grid_for(a.n), a.prep_blocks > 0 ? a.prep_blocks : 2560);
     hipLaunchKernelGGL(flat_prep_kernel, dim3(pg), dim3(256), 0, s, a);
     hipLaunchKernelGGL(flat_scan_kernel, dim3(1), dim3(1024), 0, s, a);
     const int gs = std::min(8192, (a.n + 255) / 256);
