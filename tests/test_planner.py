@@ -144,3 +144,37 @@ def test_one_round_plan_balances_simds(L, monkeypatch, snake):
     sums = np.bincount(np.arange(len(waves)) % 1024, weights=cost, minlength=1024)
     ratio = sums.max() / sums.mean()
     assert (ratio < 1.15) if snake == "1" else (ratio > 1.2)
+
+
+@pytest.mark.parametrize("stage_ps,growth", [(0.0, 1.0), (0.12, 1.3), (0.24, 1.0), (0.2, 1.2), (1.0, 0.8)])
+def test_flat_part_growth(L, monkeypatch, stage_ps, growth):
+    """A flat call's pipelined parts on one device (api.cpp flat_part_weights):
+    growth = device / host staging time per cell, clamped to [0.8, 1.3], none
+    before the first measurement; the parts tile the call in order and their
+    cells follow the growth within one pair's cells."""
+    for k in ("HC_PHMM_PART_GROWTH_PCT", "HC_PHMM_PART_LAST_PCT", "HC_PHMM_PART_TAPER_PCT"):
+        monkeypatch.delenv(k, raising=False)
+    L.hcx_flat_cuts.restype = C.c_int
+    L.hcx_flat_cuts.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_double, C.c_void_p]
+    rng = np.random.default_rng(5)
+    cells = (rng.integers(50, 251, 200_000) * rng.integers(100, 501, 200_000)).astype(np.int64)
+    np_ = 6
+    cuts = np.zeros(np_ + 1, np.int64)
+    g = L.hcx_flat_cuts(cells.ctypes.data, len(cells), np_, stage_ps, cuts.ctypes.data) / 1000.0
+    assert g == pytest.approx(growth, abs=1e-3)
+    assert cuts[0] == 0 and cuts[-1] == len(cells) and np.all(np.diff(cuts) > 0)
+    pc = np.add.reduceat(cells, cuts[:-1]).astype(float)
+    expect = growth ** np.arange(np_)
+    expect *= cells.sum() / expect.sum()
+    assert np.all(np.abs(pc - expect) <= cells.max()), (pc, expect)
+
+
+def test_flat_part_growth_forced(L, monkeypatch):
+    monkeypatch.setenv("HC_PHMM_PART_GROWTH_PCT", "125")
+    L.hcx_flat_cuts.restype = C.c_int
+    L.hcx_flat_cuts.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_double, C.c_void_p]
+    cells = np.full(10_000, 1000, np.int64)
+    cuts = np.zeros(5, np.int64)
+    assert L.hcx_flat_cuts(cells.ctypes.data, len(cells), 4, 0.0, cuts.ctypes.data) == 1250
+    sizes = np.diff(cuts)
+    assert np.allclose(sizes[1:] / sizes[:-1], 1.25, atol=0.01)
