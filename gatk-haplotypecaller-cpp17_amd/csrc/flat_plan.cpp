@@ -744,9 +744,13 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     b->upload_bytes = size_t(rec) + sizeof(FlatDesc) * n1 + tab_bytes;
     hipStream_t s = b->stream;
 
-    // Uploads and preparation on the slot's priority stream (Slot::prep;
-    // HC_PHMM_PREP_PRIO=0: the part's stream), the pass waits for them.
-    const hipStream_t ps = slot && slot->prep && env_i64("HC_PHMM_PREP_PRIO", 1) != 0 ? slot->prep : s;
+    // Uploads and preparation on the part's own stream by default; with
+    // HC_PHMM_PREP_PRIO=1 on the slot's greatest-priority stream (Slot::prep),
+    // the pass waiting for them. The priority stream gained ~0.2 ms with four
+    // equal parts; with eight growing parts the part's own stream is faster
+    // (12.60 / 12.70 vs 12.99 / 13.23 ms, and 14.20 vs 14.69 / 14.88 on another
+    // box: profiles/r05_e2e_parts_ab.txt).
+    const hipStream_t ps = slot && slot->prep && env_i64("HC_PHMM_PREP_PRIO", 0) != 0 ? slot->prep : s;
     if (ps != s) b->prep = ps;
     std::atomic<bool> varying{false};
     auto enqueue = [&]() -> int {
