@@ -320,13 +320,10 @@ def resident_pass(hcphmm, W, name, npairs, prof, batch=None):
         ent["rescued_cells"] = rc
         # The whole pass against both peaks: the time the fp32 cells (12 ops
         # each at 78.6 T) and the rescued fp64 cells (12 at 39.3 T) take at
-        # peak, over the device pass — the one measure that also covers the
-        # fused pass, whose rescues run inside the fp32 launch (no fp64 time).
+        # peak, over the device pass.
         t_peak = FLOPS_PER_CELL * cells / 78.6e12 + FLOPS_PER_CELL * rc / (FP64_PEAK_TOPS * 1e12)
         ent["roofline_pass"] = dict(bound="valu f32 + f64", time_at_peak_ms=round(t_peak * 1e3, 4),
-                                    frac=round(t_peak * 1e3 / s2.run_ms, 4),
-                                    mode="fused (rescues inside the fp32 launch)" if s2.kernel_ms_f64 == 0
-                                    else "fp64 launch after the fp32 pass")
+                                    frac=round(t_peak * 1e3 / s2.run_ms, 4))
     if s2.n_rescued and s2.kernel_ms_f64 > 0:
         ach = FLOPS_PER_CELL * rc / (s2.kernel_ms_f64 * 1e-3) / 1e12
         ent["fp64_tcups"] = round(rc / (s2.kernel_ms_f64 * 1e-3) / 1e12, 3)
@@ -439,6 +436,67 @@ def region_calls(hcphmm, W, no_cpu):
                                                stream_8x8_submits_ms=round(dj * 1e3, 2),
                                                stream_gcups=round(rc / dj / 1e9, 2))
     return sec
+
+
+def compact_line(out, detail_path):
+    """The bench line: the contract's keys, the roofline and CPU baseline, and
+    the secondaries' headline figures (device pass / call times, fractions of
+    peak); everything else is in the detail file (`detail`)."""
+    rf = out["roofline"]
+    line = {k: out[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                "higher_is_better", "scaling", "vs_baseline", "dtype")}
+    line["data"] = "synthetic (seeded generator, SURVEY 8d)"
+    line["config"] = {k: out["config"][k] for k in ("pairs", "cells", "parallelism", "rescued_fp64")
+                      if k in out["config"]}
+    line["config"]["workload"] = out["config"]["workload"].replace("independent pairs", "pairs").replace(
+        "1000000 ", "1M ")
+    line["roofline"] = {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel",
+                                               "kernel_ms", "traffic_source")}
+    if "cpu_baseline" in out:
+        cb = out["cpu_baseline"]
+        line["cpu_baseline"] = dict(value=round(cb["value"], 2), unit=cb["unit"], cores=cb["cores"], kind=cb["kind"],
+                                    sample=f"full batch, {cb['cores']} threads, {cb.get('cpu_model', '?')[:24]}")
+    for k in ("parity_vs_cpu_reference", "device_pass_ms", "kernel_ms_f64", "new_batch_device_ms",
+              "end_to_end_gcups", "end_to_end_first_call_ms", "end_to_end_async_2calls_gcups",
+              "multi_rank_check", "gather"):
+        if k in out:
+            line[k] = out[k]
+    if "cpu_baseline_1core" in out:
+        line["cpu_1core_gcups"] = round(out["cpu_baseline_1core"]["value"], 3)
+    sec = out.get("secondary") or {}
+    short = {}
+    for k in ("S1", "S1w", "S1w1M", "S4", "S4_20k"):
+        if k in sec:
+            e = sec[k]
+            v = dict(gcups=e.get("gcups"), pass_ms=e.get("device_pass_ms"), f32_frac=e.get("frac_f32_kernel"))
+            if k in ("S1", "S1w", "S4"):   # one-round passes: a lone call's (cold) time beside
+                v["cold_ms"] = e.get("device_pass_ms_cold")
+            if e.get("roofline_f64"):
+                v.update(f64_ms=e.get("kernel_ms_f64"), f64_frac=e["roofline_f64"]["frac"],
+                         rescued=e.get("rescued"))
+            short[k] = v
+    for k in ("S2_shard_125k", "S2_shard_250k"):
+        if k in sec:
+            short[k] = dict(pass_ms=sec[k]["device_pass_ms"], eff=sec[k].get("implied_efficiency_vs_1gpu"))
+    for k in ("region_415x32", "region_415x128"):
+        if k in sec:
+            short[k] = dict(call_ms=sec[k]["call_ms"], cold_ms=sec[k]["call_ms_cold"])
+    if "regions_64x_415x32_one_call" in sec:
+        e = sec["regions_64x_415x32_one_call"]
+        short["regions_64"] = dict(call_ms=e["call_ms"], gcups=e["gcups"])
+    if "smith_waterman" in sec:
+        e = sec["smith_waterman"]
+        short["sw"] = dict(pass_ms=e["device_pass_ms"], frac=e["roofline"]["frac"],
+                           parity=e.get("parity_vs_cpu_reference"))
+    if "genotyper" in sec:
+        e = sec["genotyper"]
+        short["gt"] = dict(call_ms=e["call_ms"], parity=e.get("parity_vs_cpu_oracle"))
+    if short:
+        line["secondary"] = short
+    bid = out.get("build_id") or {}
+    line["build"] = f"{bid.get('kernel')} {bid.get('git')}"
+    line["detail"] = os.path.relpath(detail_path, ROOT) if detail_path else None
+    return line
 
 
 def main():
@@ -702,7 +760,17 @@ def main():
             np.savez(args.check_out, raw_f32=full32, raw_f64=full64)
     bt.close()
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        # The whole record (every secondary's PMC summary, notes, baselines) goes
+        # to a file; stdout carries one compact line (< 2 kB) that a driver's
+        # output tail holds whole (verdict round 5, item 5).
+        detail = os.environ.get("HC_BENCH_DETAIL", os.path.join(ROOT, "gpurun_out", "bench_detail.json"))
+        try:
+            os.makedirs(os.path.dirname(detail), exist_ok=True)
+            with open(detail, "w") as f:
+                json.dump(out, f, indent=1)
+        except OSError:
+            detail = None
+        print(json.dumps(compact_line(out, detail), separators=(",", ":")), flush=True)
     if distributed:
         dist.destroy_process_group()
 

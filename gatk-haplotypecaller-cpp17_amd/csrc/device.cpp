@@ -41,6 +41,7 @@ TimelineRef g_tl;
 namespace {
 // Host copy of the last traced part's records once that part is freed.
 std::vector<unsigned long long> g_tl_saved;
+int g_tl_saved_n32 = 0;
 }
 
 void release_device(Device* d)
@@ -52,7 +53,6 @@ void release_device(Device* d)
     for (Slot* s : d->slots) {
         if (s->stream) (void)hipStreamSynchronize(s->stream);
         if (s->side) (void)hipStreamSynchronize(s->side);
-        if (s->prep) (void)hipStreamSynchronize(s->prep);
         if (s->dev) (void)hipFree(s->dev);
         if (s->host) (void)hipHostFree(s->host);
         for (auto& e : s->ev)
@@ -62,7 +62,6 @@ void release_device(Device* d)
         if (s->fork) (void)hipEventDestroy(s->fork);
         if (s->join) (void)hipEventDestroy(s->join);
         if (s->side) (void)hipStreamDestroy(s->side);
-        if (s->prep) (void)hipStreamDestroy(s->prep);
         if (s->stream) (void)hipStreamDestroy(s->stream);
         delete s;
     }
@@ -221,10 +220,6 @@ Slot* take_slot(Device& d)
         fail(HC_PHMM_EHIP, "slot stream / event creation");
         return nullptr;
     }
-    int lo = 0, hi = 0;   // (hi: the greatest priority, numerically lowest)
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&s->prep, hipStreamNonBlocking, hi) != hipSuccess)
-        s->prep = nullptr;
     s->busy = true;
     std::lock_guard<std::mutex> lk(g_mu);
     d.slots.push_back(s);
@@ -273,7 +268,6 @@ void free_part(Part* p)
 {
     if (!p) return;
     if (p->dev) (void)hipSetDevice(p->dev->ordinal);
-    if (p->prep) (void)hipStreamSynchronize(p->prep);   // (its uploads read the slot's memory)
     if (p->timeline) {
         std::lock_guard<std::mutex> lk(g_tl.mu);
         if (p->last_stream) (void)hipStreamSynchronize(p->last_stream);
@@ -281,6 +275,7 @@ void free_part(Part* p)
             g_tl_saved.assign(size_t(p->timeline_n) * 3, 0ull);
             (void)hipMemcpy(g_tl_saved.data(), p->timeline, g_tl_saved.size() * sizeof(unsigned long long),
                             hipMemcpyDeviceToHost);
+            g_tl_saved_n32 = p->timeline_n32;
             g_tl.part = nullptr;
         }
         (void)hipFree(p->timeline);
@@ -313,20 +308,25 @@ void discard_part(Part* p)
 
 // Records of the last traced part (alive: read from the device; freed: the copy
 // saved at free_part).
-int timeline_records(unsigned long long* out, int max_waves)
+// fp64: the fp64 waves' records (after the fp32 seg waves').
+int timeline_records(unsigned long long* out, int max_waves, bool fp64)
 {
     std::lock_guard<std::mutex> lk(g_tl.mu);
     if (g_tl.part) {
-        const int n = std::min(max_waves, g_tl.part->timeline_n);
-        (void)hipSetDevice(g_tl.part->dev->ordinal);
-        if (hipStreamSynchronize(g_tl.part->last_stream) != hipSuccess) return -1;
-        if (hipMemcpy(out, g_tl.part->timeline, size_t(n) * 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost) !=
-            hipSuccess)
+        const Part* p = g_tl.part;
+        const int off = fp64 ? p->timeline_n32 : 0;
+        const int n = std::min(max_waves, fp64 ? p->timeline_n - p->timeline_n32 : p->timeline_n32);
+        (void)hipSetDevice(p->dev->ordinal);
+        if (hipStreamSynchronize(p->last_stream) != hipSuccess) return -1;
+        if (hipMemcpy(out, p->timeline + 3 * size_t(off), size_t(n) * 3 * sizeof(unsigned long long),
+                      hipMemcpyDeviceToHost) != hipSuccess)
             return -1;
         return n;
     }
-    const int n = std::min<int>(max_waves, int(g_tl_saved.size() / 3));
-    std::copy(g_tl_saved.begin(), g_tl_saved.begin() + 3 * size_t(n), out);
+    const int tot = int(g_tl_saved.size() / 3);
+    const int off = fp64 ? g_tl_saved_n32 : 0;
+    const int n = std::min<int>(max_waves, fp64 ? tot - g_tl_saved_n32 : g_tl_saved_n32);
+    std::copy(g_tl_saved.begin() + 3 * size_t(off), g_tl_saved.begin() + 3 * size_t(off + n), out);
     return n;
 }
 

@@ -49,6 +49,10 @@ int fail(int code, const std::string& msg);
     } while (0)
 
 int64_t env_i64(const char* name, int64_t dflt);
+// Test hook (hcx_test_plan_timeout, api.cpp): the fp64 launch's non-planner
+// workgroups give up waiting for the plan at once. Off unless a test sets it;
+// no environment variable reaches it.
+bool test_plan_timeout();
 
 // HC_PHMM_TRACE=1: per-phase host timings on stderr.
 struct PhaseTimer {
@@ -81,10 +85,6 @@ struct Slot {
     // run concurrently (a call cut into parts overlaps the planning of part
     // k + 1 and the kernels of part k, and its kernels fill the chip together).
     hipStream_t stream = nullptr, side = nullptr;
-    // The flat path's uploads and preparation kernels, at the device's
-    // greatest stream priority: a part's preparation runs while the previous
-    // part's pass still holds the chip, not after it drains (null: on stream).
-    hipStream_t prep = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;   // side-stream fork / join (timing disabled)
     hipEvent_t ev[7] = {};   // pack [2], fp32 / fp64 pass [3], done, early results: reused by every part in the slot
     hipEvent_t up_ev[2] = {};   // staging halves: H2D of a half done (timing disabled)
@@ -269,7 +269,6 @@ struct Part {
     } cls[2];
     int n_lane = 0;
     int n_seg_waves = 0;
-    int seg_tail = 0;                // last seg waves in LPT order: the persistent pass's tail queue
     int lane_waves = 0;
     int lane_variant = 0;
     const int* d_nwaves = nullptr;   // device-planned parts: the wave count lives on the device
@@ -292,7 +291,6 @@ struct Part {
     uint4* d_rec = nullptr;       // seg slot result records (LaneArgs::rec), gathered by the fp64 launch
     int* d_slot_of = nullptr;     // pair -> seg slot (-1: one-lane / anti-diagonal pair)
     PairDesc* d_sdesc = nullptr;  // seg slot -> pair descriptor (pairs[order[slot]])
-    int* d_steal = nullptr;       // stealable rescue list (LaneArgs::steal_list; host-planned parts)
     int* d_list = nullptr;
     int* d_sorted = nullptr;
     int* d_worder = nullptr;      // fp64 pass: dispatch position -> wave
@@ -323,11 +321,11 @@ struct Part {
     hipStream_t side = nullptr;               // segmented waves beside one-lane waves
     hipEvent_t fork = nullptr, join = nullptr;
     hipStream_t last_stream = nullptr;
-    hipStream_t prep = nullptr;               // its uploads and preparation, if not on stream (Slot::prep)
     int64_t launch_waves = 0;
     bool ran = false;
     unsigned long long* timeline = nullptr;   // HC_PHMM_TIMELINE=1: this part's wave records
-    int timeline_n = 0;
+    int timeline_n = 0;                       //   (allocated), of which the fp32 seg waves' first,
+    int timeline_n32 = 0;                     //   then the fp64 waves' (Seg64Args::timeline)
 };
 
 Part* new_part(Device* d);   // counted in g_live_parts
@@ -342,7 +340,6 @@ public:
     ~PartGuard()
     {
         if (!p_) return;
-        if (p_->prep) (void)hipStreamSynchronize(p_->prep);
         if (p_->stream) (void)hipStreamSynchronize(p_->stream);
         discard_part(p_);
     }

@@ -12,7 +12,9 @@
 //           (the reference's constant 'I'/'+' strings, sam.hpp:30-32, travel
 //           as three bytes per read) is checked while filling; a part that
 //           turns out to hold a read with varying gap qualities is planned
-//           again with the check in pass 1, so its records carry the planes.
+//           again with the check in pass 1, so its records carry the planes;
+//           one whose reads or haps do not fit the compact fields (an 'N') is
+//           planned again with the nibble fields (pass 1 still lengths only).
 // The device then packs rows and hap tables, chooses each pair's
 // column-segmented shape by the planner's cost model (plan_model.hpp), sorts
 // the pairs by (block width, lanes, R) and cuts the sorted runs into waves
@@ -226,9 +228,8 @@ namespace {
 
 // ---- compact record fields (kernels.hpp kFmtRead1B / kFmtHap2b)
 
-// The format pass 1 assumes for every pair (pass 2 checks it): compact read and
-// hap fields, or (HC_PHMM_FLAT_COMPACT=0, A/B) the nibble records.
-int assumed_fmt()
+// The compact fields, unless HC_PHMM_FLAT_COMPACT=0 (A/B: the nibble records).
+int compact_fmt()
 {
     static const int f = std::getenv("HC_PHMM_FLAT_COMPACT") && std::getenv("HC_PHMM_FLAT_COMPACT")[0] == '0'
                              ? 0
@@ -348,14 +349,20 @@ bool pack_hap_2b_hook(const uint8_t* s, int n, uint8_t* d) { return pack_hap_2b(
 
 namespace {
 
+// Why pass 2 refused a part planned without scanning (fill_chunk `retry` bits).
+constexpr int kGapsVary = 1;     // a read's gap qualities vary: plan again scanning them (planes)
+constexpr int kNotCompact = 2;   // a read or hap does not fit the compact fields: plan again with nibbles
+
 // Pass 2 over mini-tasks [m0, m1): each pair's record at buf + (its offset
 // - r0) and its descriptor at dd[k - p0]. With scan_gaps false (pass 1 assumed
-// constant gap qualities and compact fields everywhere), a read whose gap
-// qualities vary or that does not fit one byte per base, or a hap with an 'N',
-// sets `varying` (the part is planned again with pass 1 scanning: fmtw[k]).
+// constant gap qualities and format fmt0 everywhere), a read whose gap
+// qualities vary sets kGapsVary in `retry` (the part is planned again with
+// pass 1 scanning: gapw[k], fmtw[k]); a read that does not fit one byte per
+// base, or a hap with an 'N', where fmt0 assumed so, sets kNotCompact (planned
+// again with fmt0 = 0, still without scanning).
 void fill_chunk(const Src& src, int64_t lo, int64_t n, int64_t m0, int64_t m1, const Mini* mini,
-                const int32_t* gapw, const uint8_t* fmtw, bool scan_gaps, char* buf, int64_t r0, FlatDesc* dd,
-                int64_t p0, std::atomic<bool>& varying)
+                const int32_t* gapw, const uint8_t* fmtw, bool scan_gaps, int fmt0, char* buf, int64_t r0,
+                FlatDesc* dd, int64_t p0, std::atomic<int>& retry)
 {
     parallel_for(m1 - m0, [&](int64_t a, int64_t e) {
         for (int64_t m = m0 + a; m < m0 + e; ++m) {
@@ -373,11 +380,11 @@ void fill_chunk(const Src& src, int64_t lo, int64_t n, int64_t m0, int64_t m1, c
                 } else {
                     const uint8_t *ip = src.ins + o, *dp = src.del + o, *cp = src.gcp + o;
                     if (!constant_gaps(ip, dp, cp, R)) {
-                        varying.store(true, std::memory_order_relaxed);
+                        retry.fetch_or(kGapsVary, std::memory_order_relaxed);
                         return;
                     }
                     g = int32_t((ip[0] & 127) | ((dp[0] & 127) << 7) | ((cp[0] & 127) << 14));
-                    fmt = assumed_fmt();
+                    fmt = fmt0;
                 }
                 const int qa = align4(R);
                 uint8_t* d = reinterpret_cast<uint8_t*>(buf + (ro - r0));
@@ -385,7 +392,7 @@ void fill_chunk(const Src& src, int64_t lo, int64_t n, int64_t m0, int64_t m1, c
                 const int qbase = (fmt & kFmtRead1B) ? kQBase : 0;
                 if (fmt & kFmtRead1B) {
                     if (!read_1b(src.q + o, src.rs + o, R, d)) {
-                        varying.store(true, std::memory_order_relaxed);   // (scan mode never lists such a read)
+                        retry.fetch_or(kNotCompact, std::memory_order_relaxed);   // (scan mode never lists such a read)
                         return;
                     }
                 } else {
@@ -401,7 +408,7 @@ void fill_chunk(const Src& src, int64_t lo, int64_t n, int64_t m0, int64_t m1, c
                 }
                 if (fmt & kFmtHap2b) {
                     if (!pack_hap_2b(src.hap + src.hap_off[p], H, d + at)) {
-                        varying.store(true, std::memory_order_relaxed);
+                        retry.fetch_or(kNotCompact, std::memory_order_relaxed);
                         return;
                     }
                 } else {
@@ -417,10 +424,11 @@ void fill_chunk(const Src& src, int64_t lo, int64_t n, int64_t m0, int64_t m1, c
 }
 
 // Pass 1 over pairs [lo, lo + n): per mini-task sums and bounds; with
-// scan_gaps, each read's constant gap triple (or -1) in gapw; every stride-th
-// hap length in hsamp.
-void scan_pass(const Src& src, int64_t lo, int64_t n, bool scan_gaps, Mini* mini, int32_t* gapw, uint8_t* fmtw,
-               int32_t* hsamp, int64_t stride)
+// scan_gaps, each read's constant gap triple (or -1) in gapw and its format
+// (compact fields where they fit, if compact_fmt() allows) in fmtw; without,
+// every pair is assumed to take format fmt0; every stride-th hap length in hsamp.
+void scan_pass(const Src& src, int64_t lo, int64_t n, bool scan_gaps, int fmt0, Mini* mini, int32_t* gapw,
+               uint8_t* fmtw, int32_t* hsamp, int64_t stride)
 {
     const int64_t nmini = (n + kMini - 1) / kMini;
     parallel_for(nmini, [&](int64_t m0, int64_t m1) {
@@ -436,7 +444,7 @@ void scan_pass(const Src& src, int64_t lo, int64_t n, bool scan_gaps, Mini* mini
                     continue;
                 }
                 int32_t g = 0;
-                int fmt = assumed_fmt();   // assumed (checked by pass 2) unless scanning
+                int fmt = fmt0;   // assumed (checked by pass 2) unless scanning
                 if (scan_gaps) {
                     const int64_t o = src.read_off[p];
                     const uint8_t *ip = src.ins + o, *dp = src.del + o, *cp = src.gcp + o;
@@ -444,7 +452,7 @@ void scan_pass(const Src& src, int64_t lo, int64_t n, bool scan_gaps, Mini* mini
                             ? int32_t((ip[0] & 127) | ((dp[0] & 127) << 7) | ((cp[0] & 127) << 14))
                             : -1;
                     gapw[k] = g;
-                    fmt = assumed_fmt() == 0 ? 0
+                    fmt = compact_fmt() == 0 ? 0
                                              : (read_1b(src.q + o, src.rs + o, R, nullptr) ? kFmtRead1B : 0) |
                                                    (has_n(src.hap + src.hap_off[p], H) ? 0 : kFmtHap2b);
                     fmtw[k] = uint8_t(fmt);
@@ -463,7 +471,25 @@ void scan_pass(const Src& src, int64_t lo, int64_t n, bool scan_gaps, Mini* mini
     }, 8);
 }
 
-constexpr int kRetryWithPlanes = 1;   // plan_flat_try: a read's gap qualities vary, or a field is not compact
+constexpr int kRetryWithPlanes = 1;   // plan_flat_try: a read's gap qualities vary
+constexpr int kRetryNibbles = 2;      // plan_flat_try: a read or hap does not fit the compact fields
+
+// Does a sample of the part's pairs (every stride-th, at most ~1 024) all fit
+// the compact fields? Real reads often hold an 'N': such a part then starts
+// with the nibble fields instead of finding out in pass 2, where the refusal
+// costs the chunks filled so far and a second planning (advisor round 5).
+bool sample_fits_compact(const Src& src, int64_t lo, int64_t n)
+{
+    if (compact_fmt() == 0) return false;
+    const int64_t stride = std::max<int64_t>(1, n / 1024);
+    for (int64_t k = 0; k < n; k += stride) {
+        const int64_t p = lo + k, o = src.read_off[p];
+        const int R = src.R[p], H = src.H[p];
+        if (R <= 0 || H <= 0) continue;   // (pass 1 refuses the part)
+        if (!read_1b(src.q + o, src.rs + o, R, nullptr) || has_n(src.hap + src.hap_off[p], H)) return false;
+    }
+    return true;
+}
 
 bool default_policies()
 {
@@ -479,11 +505,13 @@ bool default_policies()
 
 namespace {
 
-// One attempt: scan_gaps = false assumes constant gap qualities and compact
-// read / hap fields (checked in pass 2; kRetryWithPlanes if one is not), true
-// finds each pair's in pass 1.
+// One attempt: scan_gaps = false assumes constant gap qualities and format
+// fmt0 everywhere (checked in pass 2; kRetryWithPlanes / kRetryNibbles if
+// not), true finds each pair's in pass 1. record_rate: this attempt's host
+// staging time updates the device's measured rate (not after a refused
+// attempt, whose wasted work would read as slow staging).
 int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool with_run, bool scan_gaps,
-                  Part** out)
+                  int fmt0, bool record_rate, Part** out)
 {
     *out = nullptr;
     PhaseTimer tm;
@@ -505,7 +533,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     Mini* mini = S.mini.data();
     int32_t* hsamp = S.hsamp.data();
 
-    scan_pass(src, lo, n, scan_gaps, mini, gapw, fmtw, hsamp, stride);
+    scan_pass(src, lo, n, scan_gaps, fmt0, mini, gapw, fmtw, hsamp, stride);
     t_stage += clk::now() - t_begin;
     tm.mark("flat: scan");
 
@@ -652,6 +680,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     char* host = nullptr;
     int rc = HC_PHMM_OK;
     if (slot) {
+        tm.mark("flat: layout (sizes)");
         rc = slot_reserve(*slot, total, host_res_off + res_bytes);
         if (rc) return rc;
         dev = slot->dev;
@@ -697,7 +726,6 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     b->Hmax = hmax;
     b->n_lane = int(n);
     b->n_seg_waves = int(max_waves);
-    b->seg_tail = tail;
     b->lane_waves = int(max_waves);
     b->d_nwaves = reinterpret_cast<int*>(dev + o_nw);
     b->d_pairs = reinterpret_cast<PairDesc*>(dev + o_pairs);
@@ -744,18 +772,16 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     b->upload_bytes = size_t(rec) + sizeof(FlatDesc) * n1 + tab_bytes;
     hipStream_t s = b->stream;
 
-    // Uploads and preparation on the part's own stream by default; with
-    // HC_PHMM_PREP_PRIO=1 on the slot's greatest-priority stream (Slot::prep),
-    // the pass waiting for them. The priority stream gained ~0.2 ms with four
-    // equal parts; with eight growing parts the part's own stream is faster
-    // (12.60 / 12.70 vs 12.99 / 13.23 ms, and 14.20 vs 14.69 / 14.88 on another
-    // box: profiles/r05_e2e_parts_ab.txt).
-    const hipStream_t ps = slot && slot->prep && env_i64("HC_PHMM_PREP_PRIO", 0) != 0 ? slot->prep : s;
-    if (ps != s) b->prep = ps;
-    std::atomic<bool> varying{false};
+    // Uploads and preparation on the part's own stream (a greatest-priority
+    // stream for them gained ~0.2 ms with four equal parts and lost with the
+    // growing parts, profiles/r05_e2e_parts_ab.txt; removed).
+    const hipStream_t ps = s;
+    std::atomic<int> retry{0};
     auto enqueue = [&]() -> int {
         // Pass 2: chunks through the ring, each H2D'd as soon as it is filled.
-        const clk::time_point t_fill = clk::now();
+        // The staging rate counts the fills only: not the wait for the ring's
+        // lock (another part's fill) nor for a chunk's previous H2D (device
+        // backpressure), which are not host staging (advisor round 5).
         {
             std::lock_guard<std::mutex> lk(dv.ring.mu);
             for (size_t c = 0; c + 1 < chunk_m.size(); ++c) {
@@ -768,8 +794,10 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
                 char* buf = dv.ring.buf[ri];
                 const size_t dbase = (size_t(r1 - r0) + 255) & ~size_t(255);
                 FlatDesc* dd = reinterpret_cast<FlatDesc*>(buf + dbase);
-                fill_chunk(src, lo, n, m0, m1, mini, gapw, fmtw, scan_gaps, buf, r0, dd, p0, varying);
-                if (varying.load()) return kRetryWithPlanes;
+                const clk::time_point t_fill = clk::now();
+                fill_chunk(src, lo, n, m0, m1, mini, gapw, fmtw, scan_gaps, fmt0, buf, r0, dd, p0, retry);
+                t_stage += clk::now() - t_fill;
+                if (const int why = retry.load()) return (why & kGapsVary) ? kRetryWithPlanes : kRetryNibbles;
                 HIP_TRY(hipMemcpyAsync(dev + o_img + r0, buf, size_t(r1 - r0), hipMemcpyHostToDevice, ps));
                 HIP_TRY(hipMemcpyAsync(dev + o_desc + sizeof(FlatDesc) * size_t(p0), dd,
                                        sizeof(FlatDesc) * size_t(p1 - p0), hipMemcpyHostToDevice, ps));
@@ -778,11 +806,12 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
             }
         }
         tm.mark("flat: fill + H2D");
-        t_stage += clk::now() - t_fill;
-        if (spec.cells > 0) {   // running mean over calls (weight 1/2 to the newest part)
+        if (record_rate && spec.cells > 0) {   // running mean over calls (weight 1/2 to the newest part)
             const double ps = std::chrono::duration<double, std::pico>(t_stage).count() / spec.cells;
-            const double old_ps = dv.stage_ps_per_cell.load(std::memory_order_relaxed);
-            dv.stage_ps_per_cell.store(old_ps > 0 ? 0.5 * (old_ps + ps) : ps, std::memory_order_relaxed);
+            double old_ps = dv.stage_ps_per_cell.load(std::memory_order_relaxed);
+            while (!dv.stage_ps_per_cell.compare_exchange_weak(old_ps, old_ps > 0 ? 0.5 * (old_ps + ps) : ps,
+                                                               std::memory_order_relaxed)) {
+            }
         }
         if (!b->slot_ev)
             for (auto& e : b->pack_ev) HIP_TRY(hipEventCreate(&e));
@@ -813,15 +842,12 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
         a.waves_tmp = reinterpret_cast<LaneWave*>(dev + o_wtmp);
         a.wcost = reinterpret_cast<int*>(dev + o_wcost);
         a.tail = tail;
-        a.n_simd = env_i64("HC_PHMM_ONE_ROUND_SNAKE", 0) != 0 ? 4 * dv.n_cu : 0;
         a.max_waves = int(max_waves);
         a.nwaves = reinterpret_cast<int*>(dev + o_nw);
         a.counters = b->d_count;
-        a.list = b->d_list;
         a.prep_blocks = int(env_i64("HC_PHMM_PREP_BLOCKS", 0));
         HIP_TRY(launch_flat_plan(a, ps));
         HIP_TRY(hipEventRecord(b->pack_ev[1], ps));
-        if (ps != s) HIP_TRY(hipStreamWaitEvent(s, b->pack_ev[1], 0));
         if (with_run) {
             const int r = run_part(b, s);
             if (r) return r;
@@ -843,8 +869,14 @@ int plan_flat_device(Device& dv, const Src& src, const PartSpec& spec, Slot* slo
 {
     *out = nullptr;
     if (!spec.flat || !src.R || !default_policies() || (!slot && with_run)) return HC_PHMM_OK;
-    int rc = plan_flat_try(dv, src, spec, slot, with_run, false, out);
-    if (rc == kRetryWithPlanes) rc = plan_flat_try(dv, src, spec, slot, with_run, true, out);
+    // Compact fields unless a sample of the part shows a pair that does not
+    // fit them; refused in pass 2: the nibble fields (pass 1 still lengths
+    // only), and varying gap qualities: pass 1 scanning every read.
+    const int64_t n = spec.hi - spec.lo;
+    int fmt0 = n > 0 && sample_fits_compact(src, spec.lo, n) ? compact_fmt() : 0;
+    int rc = plan_flat_try(dv, src, spec, slot, with_run, false, fmt0, true, out);
+    if (rc == kRetryNibbles) rc = plan_flat_try(dv, src, spec, slot, with_run, false, 0, false, out);
+    if (rc == kRetryWithPlanes) rc = plan_flat_try(dv, src, spec, slot, with_run, true, 0, false, out);
     return rc;
 }
 
@@ -892,7 +924,9 @@ extern "C" void hcx_flat_host_passes(int64_t n, const int64_t* read_off, const i
     for (int r = 0; r <= reps; ++r) {   // rep 0 sizes the buffers (untimed)
         auto t0 = std::chrono::steady_clock::now();
         mini.assign(size_t(nmini), Mini{});
-        scan_pass(src, 0, n, false, mini.data(), gapw.data(), fmtw.data(), hsamp.data(), std::max<int64_t>(1, n / 8192));
+        const int fmt0 = sample_fits_compact(src, 0, n) ? compact_fmt() : 0;
+        scan_pass(src, 0, n, false, fmt0, mini.data(), gapw.data(), fmtw.data(), hsamp.data(),
+                  std::max<int64_t>(1, n / 8192));
         int64_t rec = 0;
         for (auto& M : mini) {
             const int64_t x = M.rec;
@@ -901,9 +935,9 @@ extern "C" void hcx_flat_host_passes(int64_t n, const int64_t* read_off, const i
         }
         if (buf.size() < size_t(rec)) buf.resize(size_t(rec));
         auto t1 = std::chrono::steady_clock::now();
-        std::atomic<bool> varying{false};
-        fill_chunk(src, 0, n, 0, nmini, mini.data(), gapw.data(), fmtw.data(), false, buf.data(), 0, dd.data(), 0,
-                   varying);
+        std::atomic<int> retry{0};
+        fill_chunk(src, 0, n, 0, nmini, mini.data(), gapw.data(), fmtw.data(), false, fmt0, buf.data(), 0, dd.data(),
+                   0, retry);
         auto t2 = std::chrono::steady_clock::now();
         if (r == 0) continue;
         ms[0] += std::chrono::duration<double, std::milli>(t1 - t0).count() / reps;

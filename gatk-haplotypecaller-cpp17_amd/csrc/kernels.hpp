@@ -46,16 +46,11 @@ constexpr long long kMaxHapWords = (1ll << 30) - 1024;
 // Run counters of a part (zeroed when the part is prepared): [0, 1] rescue
 // list lengths and [2, 3] in-wave rescue counts, by run parity (a run zeroes
 // the other parity's for the next run: no memset per run); [4] the fp64
-// pass's wave counter (zeroed by its plan each run); [5..10] the fp64
-// planner's ticket and flag and the stealable list's length, by parity
-// likewise; from kSegHeads the
-// persistent fp32 pass's queue heads (8 XCD queues + the tail queue, one
-// 64-byte line each) and its finished-wave count, which the last wave to
-// finish zeroes again for the next run (lane_kernel.hip phmm_seg_kernel).
+// pass's wave counter (zeroed by its plan each run); [5..8] the fp64
+// planner's ticket and flag, by parity likewise.
 constexpr int kNextWave = 4;
 constexpr int kPlanTicket = 5;   // [5, 6] fp64 planner ticket, [7, 8] plan-published flag, by run parity
 constexpr int kPlanReady = 7;
-constexpr int kStealCount = 9;    // [9, 10] stealable rescue list length, by parity
 // [12] device error word (sticky, not by parity): a kernel that cannot finish
 // its share sets a bit here instead of leaving results silently undone; the
 // host reads it with the results (the counters are the last field of a part's
@@ -63,21 +58,7 @@ constexpr int kStealCount = 9;    // [9, 10] stealable rescue list length, by pa
 // with HC_PHMM_EHIP. Batches clear it when they report it.
 constexpr int kErrWord = 12;
 constexpr int kErrPlanWait = 1;   // fp64 pass: a workgroup gave up waiting for the rescue plan
-constexpr int kErrFusedWait = 2;  // fused pass: a wave gave up waiting for a listed rescue's entry
-// [16..17] the fused pass's started waves (LaneArgs::fz_*), by run parity;
-// its queue heads from kFusedHeads (kFusedQueues per parity).
-constexpr int kFusedStarted = 16;
-constexpr int kSegHeads = 24;
-constexpr int kSegQueues = 9;          // 8 XCD queues + the tail queue
-constexpr int kSegHeadStride = 16;     // ints: one 64-byte line per head
-constexpr int kSegDone = kSegHeads + kSegQueues * kSegHeadStride;
-// The fused pass's rescue list is read through kFusedQueues heads: list
-// index i belongs to queue i % kFusedQueues, whose head counts its taken
-// entries (seg_common.hpp fused_rescues). One head made every finishing wave
-// retry a compare-and-swap on the same word: S4's pass took 22 ms.
-constexpr int kFusedQueues = 32;
-constexpr int kFusedHeads = kSegDone + 16;   // [2][kFusedQueues], by run parity
-constexpr int kNumCounters = kFusedHeads + 2 * kFusedQueues;
+constexpr int kNumCounters = 16;
 static_assert(kNumCounters <= 256, "the prep kernels zero the counters with one 256-thread block");
 
 struct DiagArgs {
@@ -124,8 +105,7 @@ struct Seg64Args {
     const uint32_t* rows;
     const uint32_t* hapw;
     const double* lut;
-    int* list;                // rescue list (fp32 pass, arbitrary order); the planner appends the
-                              // stealable list's untaken entries to it
+    int* list;                // rescue list (fp32 pass, arbitrary order)
     const int* count;         // its length
     int* count_reset;         // the other run parity's counter, zeroed for the next run
     int* inker_reset;         // the other run parity's in-wave rescue counter, likewise
@@ -140,6 +120,7 @@ struct Seg64Args {
     double* raw_out;          // raw f64 sums by pair id
     long long min_lanes;      // narrower blocks below this many lanes at bc = 32
     int* wave_order;          // dispatch position -> wave (n entries), see rescue_plan_kernel
+    int order_mode;           // one-round plans: 1 heaviest with lightest per SIMD; 2 the heaviest alone first
     int* next_wave;           // dynamic wave counter (zeroed by the plan)
     int n_simd;               // SIMDs of the device (4 per CU)
     // Gather of the seg slots' result records (LaneArgs::rec) into the
@@ -151,15 +132,13 @@ struct Seg64Args {
     float* raw32;
     uint8_t* flag;
     int prio;   // as LaneArgs::prio
-    // The fp32 pass's stealable rescues (LaneArgs::steal_list): entries of
-    // [0, steal_count) still holding a pair id + 1 were not taken by a seg
-    // wave and are planned here with the list's; every entry is zeroed again
-    // for the next run.
-    int* steal_list;          // null: no stealable list this run
-    const int* steal_count;
-    int* steal_count_reset;   // the other run parity's, zeroed for the next run
     int* err;                 // the part's error word (kErrWord): kErrPlanWait on a plan-wait timeout
-    int force_plan_timeout;   // test hook (HC_PHMM_TEST_PLAN_TIMEOUT=1): non-planner workgroups time out at once
+    // Diagnostics (HC_PHMM_TIMELINE=1): per fp64 wave w (class order), record
+    // timeline[3 * w] = {start, end, HW_ID | XCC_ID << 32 | first pair id << 40};
+    // record n_pairs: {the planner workgroup's start, plan published, list
+    // length}; null = off.
+    unsigned long long* timeline;
+    int force_plan_timeout;   // test hook (hcx_test_plan_timeout): non-planner workgroups time out at once
 };
 // Lane-per-pair kernel (large batches): one lane owns one pair and sweeps it
 // row by row over register-resident blocks of kLaneBlock columns. A wave holds
@@ -202,18 +181,12 @@ struct LaneArgs {
     // Diagnostics (HC_PHMM_TIMELINE=1, seg waves only): per wave
     // {start, end} of s_memrealtime (100 MHz) and the HW_ID register; null = off.
     unsigned long long* timeline;
-    // Persistent seg pass (phmm_seg_kernel): the run counters (kSegHeads..),
-    // null = one wave per launched slot (the classic grid); the last n_tail
-    // waves of the order form the shared tail queue (shortest, longest first).
-    int* seg_counters;
-    int n_tail;
     // Column-segmented waves: per-slot result records instead of the per-pair
     // outputs (null: write raw_out / rescue_flag / raw64_zero by pair id). A
     // wave's pairs own consecutive slots, so its stores are contiguous; the
     // fp64 pass gathers the records into the per-pair outputs (Seg64Args).
     uint4* rec;
     int prio;   // 1: issue priority by remaining steps (seg_common.hpp set_prio_by_remaining)
-    int prio_from;   // prio 2: only waves wid >= prio_from (the last round of slots) take it
     const PairDesc* sdesc;   // seg slots' pair descriptors in slot order (pairs[order[slot]])
     // No fp64 launch after this pass (run.cpp: small parts of seg waves only,
     // every hap within kInWaveRescueMaxH): each flagged pair is rescued in its
@@ -222,35 +195,7 @@ struct LaneArgs {
     // fp64 launch follows.
     int* solo_counters;   // the part's counter block
     int solo_other;       // the other run parity
-    // Stealable rescues (seg waves, with an fp64 launch after the pass): a
-    // flagged pair of H <= kInWaveRescueMaxH its wave does not rescue goes to
-    // steal_list as pid + 1 (entries zero before the run); a seg wave done with
-    // its own pairs takes entries (seg_common.hpp steal_rescues) and rescues
-    // them in fp64 itself, so rescues listed while the pass drains run beside
-    // it instead of after it. The fp64 launch plans the entries left untaken.
-    // null = off (every deferred rescue to rescue_list).
-    int* steal_list;
-    int* steal_count;
-    // Fused pass (phmm_seg_kernel<OCC, true, MAXWI>; run.cpp): no fp64 launch.
-    // A wave appends its flagged pairs to rescue_list (pid + 1; the entries
-    // are zero before the run and the consumer zeroes them again), then, once
-    // every wave of the launch has started (fz_started), takes listed rescues
-    // through the kFusedQueues heads and recomputes each in fp64 over its 64
-    // lanes until none is listed (seg_common.hpp fused_rescues). null = off.
-    int* fz_started;      // launches the fused form of phmm_seg_kernel when set
-    int* fz_head;         // kFusedQueues heads of this run's parity
-    int fz_wide;          // 1: fp64 blocks up to 32 columns (H <= kSeg64MaxH) at kFusedOcc waves per
-                          // SIMD; 0: 8 columns (H <= kInWaveRescueMaxH) at the fp32 pass's 3
-    int* err;             // the part's error word (kErrWord)
-    int force_wait_timeout;   // test hook (HC_PHMM_TEST_PLAN_TIMEOUT=1): a wave reaching the queue gives up at once
-    int prio64;           // the fused pass's fp64 rescues: issue priority by remaining steps (as Seg64Args::prio)
-    int fz_prio;          // 1: fp32 work at issue priority 2, queued rescues at 0 (they fill the issue
-                          // cycles the pass's waves leave idle instead of slowing its last waves)
 };
-// Waves per SIMD of the wide fused pass (fp64 blocks up to 32 columns in the
-// same waves: 256 VGPRs); run.cpp takes it only when every wave of a part is
-// resident at once at this occupancy.
-constexpr int kFusedOcc = 2;
 // Result record of one seg slot: {raw f32 bits, state, raw f64 low word, high
 // word}; state 0 = not rescued, 1 = rescued in the fp32 pass (raw f64 here),
 // 2 = rescued by the fp64 pass (raw f64 written there, by pair id).
@@ -267,10 +212,7 @@ const LaneVariant& lane_variant(int id);
 hipError_t launch_lane_f32(int variant, const LaneArgs& a, hipStream_t s);
 // Column-segmented waves only (lane_kernel.hip run_seg): a pair of hap length H
 // takes ceil(H / BC) lanes; BC per wave, one of the compiled block widths.
-// max_waves > 0: at most that many resident waves, persistent waves fetching
-// the rest (a.seg_counters must be set).
-// queues: 8 = per-XCD queues + tail queue, 1 = one queue (persistent only).
-hipError_t launch_lane_seg_f32(const LaneArgs& a, int max_waves, int queues, hipStream_t s);
+hipError_t launch_lane_seg_f32(const LaneArgs& a, hipStream_t s);
 bool seg_width_ok(int bc);
 int seg_width_ceil(int bc);   // narrowest compiled width >= bc (-1: none)
 constexpr int kSegMaxBC = 64;
@@ -323,10 +265,6 @@ struct PackArgs {
     const int* order;
     int nslots;
     int4* sdesc;
-    int* steal;   // the part's stealable rescue list, zeroed here (n_steal entries)
-    int n_steal;
-    int* list;    // the part's rescue list, zeroed here (n_list entries; the fused pass's queue)
-    int n_list;
 };
 hipError_t launch_pack_batch(const PackArgs& a, hipStream_t s);
 // Pair descriptors of a structured (cross-product) plan, built on the device
@@ -393,22 +331,6 @@ struct FlatDesc {
 // uploads ~250 instead of ~416 bytes per pair.
 constexpr int kFmtRead1B = 1;
 constexpr int kFmtHap2b = 2;
-// Dispatch position of the wave of rank r (descending modelled duration) in a
-// plan of W waves that are all resident at once (S < W <= 3 S, S = SIMDs):
-// one-wave workgroups are dealt to the SIMDs in order, position p and p + S
-// sharing one (per-wave HW_ID, tools/timeline.py), so a SIMD's waves are ranks
-// of rounds q = 0, 1, 2 and the pass lasts as long as its heaviest SIMD's sum.
-// Snake order: round 0 heaviest first, round 1 lightest first, round 2 heaviest
-// first again (the heaviest wave shares its SIMD with the lightest); a partial
-// last odd round puts its lightest waves on the lowest SIMDs (positions must
-// stay below W).
-__host__ __device__ inline int one_round_pos(int r, int W, int S)
-{
-    const int q = r / S, i = r - q * S;
-    if ((q & 1) == 0) return r;
-    return (q + 1) * S <= W ? q * S + (S - 1 - i) : q * S + (W - 1 - r);
-}
-
 struct FlatPlanArgs {
     const uint8_t* img;
     const FlatDesc* desc;
@@ -434,10 +356,7 @@ struct FlatPlanArgs {
     int max_waves;         // waves the launch covers (upper bound of the plan's)
     int* nwaves;           // the plan's wave count; [1]: its largest modelled wave cost (with the tail)
     int tail;              // waves dispatched last, longest first (0: packing order)
-    int n_simd;            // one-round plans (waves within the resident slots): snake order over
-                           // the SIMDs (one_round_pos), 0 = off (default: measured no faster)
     int* counters;         // kNumCounters run counters, zeroed
-    int* list;             // the rescue list (n entries), zeroed (the fused pass's queue)
     int prep_blocks;       // flat_prep_kernel's grid bound (0: a wave per pair, up to 65 536 blocks)
 };
 hipError_t launch_flat_plan(const FlatPlanArgs& a, hipStream_t s);

@@ -390,26 +390,29 @@ __device__ void plan_rescue(const Seg64Args& a, int n, PlanLds& L)
     const int S = a.n_simd;
     for (int w = t; w < W; w += kPlanThreads) {
         const int r = atomicAdd(&L.hist[bucket(L.cost[w])], 1);   // rank in descending cost
-        // two waves per SIMD at most: positions S.. pair the heaviest with the lightest
-        const int pos = (W <= 2 * S && r >= S) ? S + (W - 1 - r) : r;
+        // At most two waves per SIMD (positions p and p + S share one): the
+        // 2S - W heaviest waves alone on a SIMD (positions W - S .. S - 1),
+        // then the rest paired heaviest with lightest.
+        int pos = r;
+        if (W > S && W <= 2 * S) {
+            const int solo = 2 * S - W;
+            if (a.order_mode == 2)
+                pos = r < solo ? (W - S) + r : (r < S ? r - solo : S + (W - 1 - r));
+            else if (r >= S)
+                pos = S + (W - 1 - r);
+        }
         a.wave_order[pos] = w;
     }
 }
 
-// One column-segmented wave (wid) of the fp32 pass. FUSED: the fused pass
-// (LaneArgs::fz_*): flagged pairs go to the queue, then the wave takes queued
-// rescues (seg_common.hpp fused_rescues); nw = the launch's waves.
-template <bool FUSED = false, int MAXWI = 0>
-__device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float* __restrict__ slut, int nw = 0,
-                                         double* __restrict__ slut64 = nullptr)
+// One column-segmented wave (wid) of the fp32 pass.
+__device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float* __restrict__ slut)
 {
     // Lane id and the wave's LDS tables in forms the compiler can recompute
     // (mbcnt) or keep in SGPRs (wave-uniform): values live across the step
     // loop that it would otherwise spill at every wave's start.
     const int lane = __lane_id();
     const unsigned long long t_start = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
-    if (FUSED && lane == 0) __hip_atomic_fetch_add(a.fz_started, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (FUSED && a.fz_prio) __builtin_amdgcn_s_setprio(2);
     const LaneWave wv = load_wave(a.waves, wid);
     const int bc = wv.ncols;
     __shared__ uint2 mtab[kSegWPB][5 * 64];
@@ -447,8 +450,7 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
     const uint32_t w1 = row_word(cx, 0);
     const float T0 = row0_t<float>(a.lut, w1, cx.H);
     const bool wave_eq = __builtin_amdgcn_ballot_w64(!read_eq(w1)) == 0;
-    const int prio = a.prio == 2 ? (wid >= a.prio_from ? 1 : 0) : a.prio;   // (wave-uniform)
-    const SegSteps st{wv.rmax, wv.rmin, wv.nsteps, prio};
+    const SegSteps st{wv.rmax, wv.rmin, wv.nsteps, a.prio};
     float sumM = 0.f, sumX = 0.f;
     switch (bc) {
 #define HC_SEG_CASE(W) \
@@ -474,20 +476,8 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
             if (!resc) a.raw64_zero[pid] = 0.0;
         }
     }
-    if constexpr (FUSED) {
-        // pair id + 1 (a zero entry: not yet published), published by an
-        // atomic swap: an atomic is performed past the XCD's L2, where a wave
-        // of another XCD sees it. (A plain or relaxed atomic store stays in
-        // this XCD's L2 until the line is evicted: claimants on the other
-        // seven XCDs waited milliseconds for it, 2.6-3.9 ms per rescue in
-        // tools/timeline.py; a release fence instead — buffer_wbl2, a
-        // write-back of the whole L2 — in every wave made the pass 5x slower.)
-        if (resc) (void)__hip_atomic_exchange(a.rescue_list + atomicAdd(a.rescue_count, 1), pid + 1,
-                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        const uint64_t todo = __builtin_amdgcn_ballot_w64(resc);
-        if (todo) rescue_in_wave(a, todo, pid, slot, cx.H, lane, mt);
-    }
+    const uint64_t todo = __builtin_amdgcn_ballot_w64(resc);
+    if (todo) rescue_in_wave(a, todo, pid, slot, cx.H, lane, mt);
     if (a.timeline && lane == 0) {
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
         a.timeline[3 * size_t(wid)] = t_start;
@@ -496,45 +486,9 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
         a.timeline[3 * size_t(wid) + 2] = (unsigned long long)unsigned(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))) |
                                           ((unsigned long long)unsigned(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11))) << 32);
     }
-    if constexpr (FUSED) {
-        __builtin_amdgcn_wave_barrier();   // the rescues below rewrite mt
-        const int nres = fused_rescues<MAXWI>(a, nw, wid, lane, mt, slut64);
-        if (a.timeline && lane == 0) {   // fused: (time in rescues << 16) | rescues taken (0xffff: not started)
-            const unsigned long long t_fin = __builtin_amdgcn_s_memrealtime();
-            a.timeline[3 * size_t(wid) + 2] = ((t_fin - a.timeline[3 * size_t(wid) + 1]) << 16) | unsigned(nres & 0xffff);
-        }
-    } else if (a.steal_list) {
-        steal_rescues(a, wid, lane, mt);
-    }
 }
 
-
-// Persistent form of the pass (more waves than the launch's wave slots): the
-// reference's schedule(dynamic, 1) over the pairs (intel_pairhmm.hpp:128-130)
-// at wave granularity, with XCD locality. The order (packing order: one block
-// width's waves together; the shortest waves last, longest first) is cut into
-// 8 contiguous ranges, one per XCD group (workgroup b serves group b % 8:
-// workgroups are dealt round-robin over the 8 XCDs, so a group is one XCD, for
-// speed only), and the last n_tail waves form a shared tail queue. A wave
-// takes its group's range first — the first round statically (its own
-// position, no atomic), then from the group's head counter — then the other
-// groups' ranges in turn, then the tail. Each XCD thus works through a
-// window of the order 8x narrower than the whole chip's, so the waves
-// resident on a CU pair share few block widths' code (at 125k pairs the
-// chip's window of 3 072 waves spans ~8 widths of ~10 KB of unrolled step
-// code each). The wave that finishes last zeroes the counters for the next
-// run (every other wave has fetched its last by then).
-__device__ __forceinline__ int seg_fetch(int* head)
-{
-    int v = 0;
-    if ((threadIdx.x & 63) == 0) v = atomicAdd(head, 1);
-    return __builtin_amdgcn_readfirstlane(v);
-}
-
-// FUSED: the fused pass (LaneArgs::fz_*); its rescues take fp64 blocks up to
-// seg64_width(MAXWI) columns: 32 at 2 waves per SIMD (haps up to 2 048), 8 at
-// the fp32 pass's 3 (haps up to 512, the in-wave rescue's registers).
-template <int OCC, bool FUSED = false, int MAXWI = 0>
+template <int OCC>
 __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
 {
     // Each wave fills its own copy of the prior tables: no workgroup barrier
@@ -542,7 +496,6 @@ __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
     // overlaps the wave's descriptor loads (small batches are one round of
     // waves: every wave's start-up latency is on the pass's critical path).
     __shared__ float sluts[kSegWPB][kSlutLen];
-    __shared__ double sluts64[FUSED ? kSegWPB : 1][FUSED ? kSlutLen : 1];   // the fused pass's fp64 priors
     const int n_waves = a.n_waves_dev ? __builtin_amdgcn_readfirstlane(*a.n_waves_dev) : a.n_waves;
     const int wib = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
     const int wid = blockIdx.x * kSegWPB + wib;
@@ -555,61 +508,12 @@ __global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_kernel(LaneArgs a)
         c[2 + o] = 0;             // in-wave rescues
         c[kPlanTicket + o] = 0;
         c[kPlanReady + o] = 0;
-        c[kStealCount + o] = 0;
-        c[kFusedStarted + o] = 0;
     }
-    if (a.fz_head && blockIdx.x == 0 && threadIdx.x < kFusedQueues)
-        a.solo_counters[kFusedHeads + a.solo_other * kFusedQueues + threadIdx.x] = 0;
     if (wid >= n_waves) return;   // wave-uniform (device-planned parts launch an upper bound)
     float* slut = sluts[wib];
     for (int t = __lane_id(); t < kSlutLen; t += 64) slut[t] = a.lut[t];
     __builtin_amdgcn_wave_barrier();
-    seg_wave<FUSED, MAXWI>(a, wid, slut, n_waves, FUSED ? sluts64[wib] : nullptr);
-}
-
-// The persistent form (a separate instance: its fetch loop around the width
-// switch costs registers that the one-wave-per-slot kernel does not pay).
-// NQ = 8: per-XCD ranges + the tail queue (above); NQ = 1: one queue over the
-// whole order (the planner's order, fetched from one counter).
-template <int OCC, int NQ>
-__global__ __launch_bounds__(64 * kSegWPB, OCC) void phmm_seg_persist_kernel(LaneArgs a)
-{
-    __shared__ float slut[kSlutLen];
-    const int n_waves = a.n_waves_dev ? __builtin_amdgcn_readfirstlane(*a.n_waves_dev) : a.n_waves;
-    const int launched = int(gridDim.x) * kSegWPB;
-    load_slut(slut, a.lut);
-    int* const heads = a.seg_counters + kSegHeads;
-    const int G = int(gridDim.x);
-    const int bulk = NQ == 1 ? n_waves : n_waves - min(a.n_tail, n_waves);
-    const int q0 = NQ == 1 ? 0 : int(blockIdx.x) & 7;
-    // Range of group r: [r * bulk / NQ, (r + 1) * bulk / NQ); queue NQ = the tail.
-    auto lo_of = [&](int r) { return r < NQ ? int((long long)r * bulk / NQ) : bulk; };
-    auto hi_of = [&](int r) { return r < NQ ? int((long long)(r + 1) * bulk / NQ) : n_waves; };
-    // waves launched in group r (workgroups r, r + NQ, ...): its static round
-    auto nstat_of = [&](int r) { return r < NQ && r < G ? ((G - 1 - r) / NQ + 1) * kSegWPB : 0; };
-    // k = -1: the static position; k = 0 .. NQ-1: group (q0 + k) % NQ's
-    // range; k = NQ: the tail queue. One call site of seg_wave.
-    for (int k = -1; k <= NQ;) {
-        int pos;
-        if (k < 0) {
-            k = 0;
-            pos = lo_of(q0) + (int(blockIdx.x) / NQ) * kSegWPB + (threadIdx.x >> 6);
-            if (pos >= hi_of(q0)) continue;
-        } else {
-            const int r = k < NQ ? (q0 + k) % NQ : NQ;
-            pos = lo_of(r) + nstat_of(r) + seg_fetch(heads + r * kSegHeadStride);
-            if (pos >= hi_of(r)) {
-                ++k;
-                continue;
-            }
-            __builtin_amdgcn_wave_barrier();   // the previous wave's last use of its LDS slots
-        }
-        seg_wave(a, pos, slut);
-    }
-    if (seg_fetch(a.seg_counters + kSegDone) == launched - 1 && (threadIdx.x & 63) < kSegQueues) {
-        heads[(threadIdx.x & 63) * kSegHeadStride] = 0;
-        if ((threadIdx.x & 63) == 0) a.seg_counters[kSegDone] = 0;
-    }
+    seg_wave(a, wid, slut);
 }
 
 // Wave-uniform max / min of a per-lane int (once per wave).
@@ -639,39 +543,19 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
     // none, and otherwise the first workgroup to arrive plans while the others
     // gather the seg records, then wait for its flag (they never wait on a
     // workgroup that is not running: the planner is the first one running).
-    const int n_list = __builtin_amdgcn_readfirstlane(*a.count);
-    // Stealable rescues no seg wave took join the list: the planner keeps the
-    // entries [0, s_count) still holding a pair id + 1. Until it has, n is an
-    // upper bound (an all-taken list plans zero waves).
-    const int s_count = a.steal_list ? __builtin_amdgcn_readfirstlane(*a.steal_count) : 0;
-    int n = n_list + s_count;
+    const int n = __builtin_amdgcn_readfirstlane(*a.count);
     if (blockIdx.x == 0 && t == 0) {   // the other run parity's counters, zeroed for the next run
         *a.count_reset = 0;
         *a.inker_reset = 0;
         *a.ticket_reset = 0;
         *a.ready_reset = 0;
-        *a.steal_count_reset = 0;
         if (n == 0) *a.big_count = 0;   // the wide fp64 kernel's list (the plan writes it otherwise)
     }
     if (t == 0) role = n > 0 ? atomicAdd(a.ticket, 1) : 1;
     __syncthreads();
     const bool planner = role == 0;
     if (planner) {
-        if (s_count > 0) {
-            if (t == 0) plan_lds.lanes = 0;
-            __syncthreads();
-            for (int i = t; i < s_count; i += 256) {   // untaken into the list; every entry zeroed for the next run
-                const int v = a.steal_list[i];
-                a.steal_list[i] = 0;
-                if (v > 0) a.list[n_list + int(atomicAdd(&plan_lds.lanes, 1ull))] = v - 1;
-            }
-            __syncthreads();
-            n = n_list + int(plan_lds.lanes);
-            // Every thread holds n before plan_rescue reuses plan_lds.lanes
-            // (its thread 0 resets it first thing): without this barrier a
-            // slower wave could read the reset value (advisor round 4).
-            __syncthreads();
-        }
+        const unsigned long long t_plan0 = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
         plan_rescue(a, n, plan_lds);
         // Publish (MI355X_MICROARCH.md, inter-workgroup visibility): every
         // storing wave drains its stores, then one lane releases and flags.
@@ -681,6 +565,11 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(a.ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (a.timeline) {   // (diagnostics) the plan's span
+                a.timeline[3 * size_t(a.n_pairs)] = t_plan0;
+                a.timeline[3 * size_t(a.n_pairs) + 1] = __builtin_amdgcn_s_memrealtime();
+                a.timeline[3 * size_t(a.n_pairs) + 2] = (unsigned long long)n;
+            }
         }
     }
     if (a.rec) {
@@ -737,6 +626,7 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
             pos = __builtin_amdgcn_readfirstlane(v);
         }
         if (pos >= total) break;
+        const unsigned long long t_start = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
         const int w = (total > 1 && a.wave_order) ? __builtin_amdgcn_readfirstlane(a.wave_order[pos]) : pos;
         const int c = __popcll(__builtin_amdgcn_ballot_w64(next_base <= w));
         const int k = 6 - c / kSeg64Widths;
@@ -767,6 +657,14 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
         default: break;
         }
         if (owner) a.raw_out[pid] = sumM + sumX;
+        if (a.timeline && lane == 0) {   // (diagnostics) start, end, HW_ID | XCC_ID << 32 | first pair << 40
+            a.timeline[3 * size_t(w)] = t_start;
+            a.timeline[3 * size_t(w) + 1] = __builtin_amdgcn_s_memrealtime();
+            a.timeline[3 * size_t(w) + 2] =
+                (unsigned long long)unsigned(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))) |
+                ((unsigned long long)unsigned(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11))) << 32) |
+                ((unsigned long long)unsigned(pid) << 40);
+        }
         __builtin_amdgcn_wave_barrier();   // the next wave's match table reuses mt
         if (!dyn) pos += gridDim.x * 4;
     }
@@ -834,29 +732,11 @@ int seg_width_ceil(int bc)
     return -1;
 }
 
-hipError_t launch_lane_seg_f32(const LaneArgs& a, int max_waves, int queues, hipStream_t s)
+hipError_t launch_lane_seg_f32(const LaneArgs& a, hipStream_t s)
 {
     if (a.n_waves <= 0) return hipSuccess;
     const int grid = (a.n_waves + kSegWPB - 1) / kSegWPB;
-    if (a.fz_started) {
-        if (a.fz_wide)
-            hipLaunchKernelGGL((phmm_seg_kernel<kFusedOcc, true, kSeg64Widths - 1>), dim3(grid), dim3(64 * kSegWPB), 0,
-                               s, a);
-        else
-            hipLaunchKernelGGL((phmm_seg_kernel<kSegOcc, true, 0>), dim3(grid), dim3(64 * kSegWPB), 0, s, a);
-        return hipGetLastError();
-    }
-    const int max_blocks = max_waves / kSegWPB;
-    // Persistent only when the waves outnumber the launch's slots (device-
-    // planned parts: their upper bound does; the kernel re-reads the count).
-    if (max_blocks > 0 && a.seg_counters && grid > max_blocks) {
-        if (queues == 8)
-            hipLaunchKernelGGL((phmm_seg_persist_kernel<kSegOcc, 8>), dim3(max_blocks), dim3(64 * kSegWPB), 0, s, a);
-        else
-            hipLaunchKernelGGL((phmm_seg_persist_kernel<kSegOcc, 1>), dim3(max_blocks), dim3(64 * kSegWPB), 0, s, a);
-    } else {
-        hipLaunchKernelGGL((phmm_seg_kernel<kSegOcc>), dim3(grid), dim3(64 * kSegWPB), 0, s, a);
-    }
+    hipLaunchKernelGGL((phmm_seg_kernel<kSegOcc>), dim3(grid), dim3(64 * kSegWPB), 0, s, a);
     return hipGetLastError();
 }
 

@@ -96,11 +96,6 @@ __device__ __forceinline__ uint4 rows_rec4(uint32_t q4, uint32_t c4, uint32_t i4
 // several HBM requests in flight instead of one dependent chain per read.
 __device__ __forceinline__ void pack_items(const PackArgs& a)
 {
-    // The stealable rescue list starts each part zeroed (its runs zero what they use).
-    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < a.n_steal; k += gridDim.x * blockDim.x) a.steal[k] = 0;
-    // the rescue list starts zeroed: the fused pass's entries are pair id + 1
-    // (its consumers zero them again after each run)
-    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < a.n_list; k += gridDim.x * blockDim.x) a.list[k] = 0;
     const int lane = threadIdx.x & 63;
     const int n = max(a.nreads, a.nhaps);
     const int stride = gridDim.x * 4;
@@ -384,7 +379,6 @@ __device__ __forceinline__ void prep_pack(const FlatPlanArgs& a, const PrepIn& x
 __global__ __launch_bounds__(256) void flat_prep_kernel(FlatPlanArgs a)
 {
     if (blockIdx.x == 0 && threadIdx.x < kNumCounters) a.counters[threadIdx.x] = 0;
-    for (int k = blockIdx.x * 256 + threadIdx.x; k < a.n; k += gridDim.x * 256) a.list[k] = 0;   // as pack_items
     const int lane = threadIdx.x & 63;
     const int stride = gridDim.x * 4;
     int p = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -584,10 +578,7 @@ __global__ __launch_bounds__(1024) void flat_tail_kernel(FlatPlanArgs a)
         acc_s = incl;
     }
     __syncthreads();
-    // One round (every wave resident at once, waves of unequal length): all
-    // waves in snake order over the SIMDs (kernels.hpp one_round_pos).
-    const bool snake = a.n_simd > 0 && nw > a.n_simd && nw <= 3 * a.n_simd;
-    const int thr = snake ? NB : (acc_s >= nw ? 0 : thr_s);   // nothing to gain when every wave is in the tail
+    const int thr = acc_s >= nw ? 0 : thr_s;   // nothing to gain when every wave is in the tail
     // tail buckets longest first: bucket b's first position is the count in buckets (b, thr)
     if (t < thr) cur[t] = part[thr - 1] - incl;
     const int nbulk = nw - (thr > 0 ? part[thr - 1] : 0);
@@ -621,7 +612,7 @@ __global__ __launch_bounds__(1024) void flat_tail_kernel(FlatPlanArgs a)
             if (bulk)
                 a.waves[base + off + __popcll(bal & ((1ull << lane) - 1))] = v[k];
             else if (bk >= 0)
-                a.waves[snake ? one_round_pos(atomicAdd(&cur[bk], 1), nw, a.n_simd) : nbulk + atomicAdd(&cur[bk], 1)] = v[k];
+                a.waves[nbulk + atomicAdd(&cur[bk], 1)] = v[k];
             base += tot;
         }
     }

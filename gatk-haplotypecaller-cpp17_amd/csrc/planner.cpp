@@ -886,7 +886,6 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         }
     }
     tm.mark("seg pack: greedy");
-    int seg_tail = 0;   // waves at the end of the order in LPT order (persistent tail queue)
     // Dispatch order: the bulk in packing order (co-resident waves share one
     // width's code), the shortest waves filling the last tail_rounds rounds of
     // wave slots last, longest first (LPT, duration ~ BC * nsteps), so the chip
@@ -899,7 +898,6 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
         const int64_t tail_rounds = std::max<int64_t>(0, env_i64("HC_PHMM_TAIL_ROUNDS", grid ? 0 : 2));
         const size_t nw = lw.size();
         const size_t K = std::min(nw, size_t(tail_rounds) * 4 * size_t(dv.n_cu) * kSegWavesPerSimd);
-        seg_tail = 0;
         std::vector<int64_t>& wc = S.wcost;
         wc.resize(nw);
         int64_t cmin = INT64_MAX, cmax = 0;
@@ -929,31 +927,11 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
                 if (!in_tail[k]) ordered.push_back(lw[k]);
             for (size_t k = 0; k < K; ++k) ordered.push_back(lw[key[k] & 0xffffffffu]);
             lw.swap(ordered);
-            seg_tail = int(K);   // the persistent pass's shared tail queue
         }
-        // One round (every wave resident at once) of unequal waves: snake order
-        // over the SIMDs by modelled duration (kernels.hpp one_round_pos).
-        // Opt-in (HC_PHMM_ONE_ROUND_SNAKE=1): it cut S4's busiest-SIMD modelled
-        // sum from 1.30x the mean to 1.10x but not the pass (0.278 vs 0.274 ms):
-        // two waves of this pass on one SIMD are latency-bound, so the SIMD
-        // lasts as long as its longest wave, not the sum of its waves.
-        const size_t nsimd = 4 * size_t(dv.n_cu);
-        if (!grid && nw > nsimd && nw <= kSegWavesPerSimd * nsimd && cmax * 20 > cmin * 21 &&
-            env_i64("HC_PHMM_ONE_ROUND_SNAKE", 0) != 0) {
-            std::vector<uint64_t>& key = S.wkey;
-            key.resize(nw);
-            for (size_t k = 0; k < nw; ++k) {
-                const uint64_t c = uint64_t(13 * lw[k].ncols + 26) * uint64_t(lw[k].nsteps);
-                key[k] = (~c & 0xffffffffull) << 32 | k;   // descending cost, ties in packing order
-            }
-            std::sort(key.begin(), key.end());
-            std::vector<LaneWave>& ordered = S.ordered;
-            ordered.resize(nw);
-            for (size_t r = 0; r < nw; ++r)
-                ordered[size_t(one_round_pos(int(r), int(nw), int(nsimd)))] = lw[key[r] & 0xffffffffu];
-            lw.swap(ordered);
-            seg_tail = 0;
-        }
+        // (A snake order over the SIMDs for one-round plans, heaviest wave
+        // beside the lightest, cut S4's busiest-SIMD modelled sum from 1.30x
+        // the mean to 1.10x but not the pass, 0.278 vs 0.274 ms: two waves of
+        // this pass on one SIMD are latency-bound. Removed)
     }
     tm.mark("seg pack");
     const int n_seg_waves = dev_plan ? int(gd.waves) : int(lw.size());
@@ -1098,7 +1076,6 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const size_t o_rec = L.take(sizeof(uint4) * std::max<size_t>(size_t(n_seg_slots), 1));   // seg slot records
     const size_t o_sdesc = L.take(sizeof(PairDesc) * std::max<size_t>(size_t(n_seg_slots), 1));   // slot -> descriptor
     const size_t o_list = L.take(sizeof(int) * n1);
-    const size_t o_steal = L.take(sizeof(int) * std::max<size_t>(size_t(n_seg_slots), 1));   // stealable rescues (seg pairs)
     const size_t o_sorted = L.take(sizeof(int) * n1);
     const size_t o_worder = L.take(sizeof(int) * n1);
     const size_t o_big = L.take(sizeof(int) * n1);
@@ -1154,7 +1131,6 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     b->Hmax = Hmax;
     b->n_lane = int(size_t(n_seg_slots) + one_ord.size());
     b->n_seg_waves = n_seg_waves;
-    b->seg_tail = seg_tail;
     b->lane_variant = lane_var;
     b->lane_waves = dev_plan ? n_seg_waves : int(lw.size());
     b->upload_bytes = dev_pairs ? (up_mid - up0) + (o_lw - o_bases) + (upload - o_gb) : upload - up0;
@@ -1189,7 +1165,6 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     b->d_rec = n_seg_slots > 0 ? reinterpret_cast<uint4*>(dev + o_rec) : nullptr;
     b->d_slot_of = reinterpret_cast<int*>(dev + o_slotof);
     b->d_sdesc = reinterpret_cast<PairDesc*>(dev + o_sdesc);
-    b->d_steal = n_seg_slots > 0 ? reinterpret_cast<int*>(dev + o_steal) : nullptr;
     b->n_wide = wide_a.load();
     b->wide_ring_blocks = wide_ring_blocks;
     b->d_carry = carry_rows ? reinterpret_cast<float2*>(dev + o_carry) : nullptr;
@@ -1229,10 +1204,6 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     pack.order = d_ord;
     pack.nslots = dev_pairs ? 0 : n_seg_slots;   // structured plans: grid_waves writes them
     pack.sdesc = b->d_sdesc;
-    pack.steal = b->d_steal;   // zeroed by the prep launch
-    pack.n_steal = b->d_steal ? int(n_seg_slots) : 0;
-    pack.list = b->d_list;   // zeroed by the prep launch (the fused pass's queue)
-    pack.n_list = int(npairs);
     auto enqueue = [&]() -> int {
         if (!b->slot_ev)
             for (auto& e : b->pack_ev) HIP_TRY(hipEventCreate(&e));

@@ -41,11 +41,11 @@ public:
         {
             std::lock_guard<std::mutex> lk(mu_);
             queue_.push_back(&b);
-            epoch_.fetch_add(1, std::memory_order_release);
         }
-        // Workers still spinning (below) see the epoch; only sleeping ones
-        // need the wake-up, and no more of them than the batch has tasks.
-        const int want = std::min(ntasks - 1, int(workers_.size())) - spinning_.load(std::memory_order_acquire);
+        // No more wake-ups than the batch has tasks (the 415 x 128 region call
+        // 1.00 -> 0.95 ms at 16 threads; workers spinning for the next batch
+        // measured no faster and were removed).
+        const int want = std::min(ntasks - 1, int(workers_.size()));
         if (want >= int(workers_.size()))
             cv_.notify_all();
         else
@@ -91,14 +91,6 @@ private:
         unsigned hw = std::max(1u, std::thread::hardware_concurrency());
         if (const char* e = std::getenv("HC_PHMM_THREADS"))
             if (std::atoi(e) > 0) hw = unsigned(std::atoi(e));
-        // HC_PHMM_POOL_SPIN_US: a worker done with a batch spins this long for
-        // the next before it sleeps. Default 0: measured no faster on the
-        // region call (0.95 ms at 0, 0.96 at 50 us, 0.98 at 200) and slower
-        // end to end (the spinning takes cores from the staging fill). What
-        // paid was waking only as many workers as a batch has tasks (above:
-        // the 415 x 128 region call 1.00 -> 0.95 ms at 16 threads).
-        if (const char* e = std::getenv("HC_PHMM_POOL_SPIN_US"))
-            if (std::atoi(e) >= 0) spin_us_ = std::atoi(e);
         const int nw = int(std::min(hw, 16u)) - 1;
         for (int k = 0; k < nw; ++k) workers_.emplace_back([this] { loop(); });
     }
@@ -135,22 +127,6 @@ private:
         std::unique_lock<std::mutex> lk(mu_);
         for (;;) {
             Batch* b = nullptr;
-            if (!stop_ && (b = pick()) == nullptr && spin_us_ > 0) {
-                // spin (unlocked) until a new batch is queued or the time is up
-                const uint64_t e0 = epoch_.load(std::memory_order_acquire);
-                lk.unlock();
-                spinning_.fetch_add(1, std::memory_order_acq_rel);
-                const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us_);
-                int k = 0;
-                while (epoch_.load(std::memory_order_acquire) == e0) {
-                    if ((++k & 63) == 0 && std::chrono::steady_clock::now() > t_end) break;
-#if defined(__x86_64__)
-                    __builtin_ia32_pause();
-#endif
-                }
-                spinning_.fetch_sub(1, std::memory_order_acq_rel);
-                lk.lock();
-            }
             cv_.wait(lk, [&] { return stop_ || (b = pick()) != nullptr; });
             if (stop_) return;
             ++b->users;
@@ -168,9 +144,6 @@ private:
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
     bool stop_ = false;
-    std::atomic<uint64_t> epoch_{0};   // batches queued so far
-    std::atomic<int> spinning_{0};     // workers spinning for the next batch
-    int spin_us_ = 0;
 };
 
 // f(lo, hi) over [0, n) in chunks of at least `grain`, on the pool.

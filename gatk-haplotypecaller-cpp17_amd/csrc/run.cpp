@@ -45,14 +45,14 @@ int run_part(Part* b, hipStream_t s)
     r.ticket_reset = b->d_count + kPlanTicket + (par ^ 1);
     r.ready = b->d_count + kPlanReady + par;
     r.ready_reset = b->d_count + kPlanReady + (par ^ 1);
-    r.steal_count_reset = b->d_count + kStealCount + (par ^ 1);
     r.sorted = b->d_sorted;
     r.big = b->d_big;
     r.big_count = b->d_big_count;
     r.plan = b->d_plan;
     r.raw_out = b->d_raw64;
     r.min_lanes = int64_t(2) * 4 * dv.n_cu * 64;
-    r.wave_order = env_i64("HC_PHMM_RESCUE_ORDER", 1) != 0 ? b->d_worder : nullptr;   // 0: class order (A/B)
+    r.order_mode = int(env_i64("HC_PHMM_RESCUE_ORDER", 1));   // 0: class order (A/B); 2: heaviest alone first
+    r.wave_order = r.order_mode != 0 ? b->d_worder : nullptr;
     r.next_wave = b->d_count + kNextWave;
     r.n_simd = 4 * dv.n_cu;
     r.n_pairs = int(b->n);
@@ -63,15 +63,16 @@ int run_part(Part* b, hipStream_t s)
     // priority makes finish together (415 x 64 0.63 -> 0.59 ms, x 128 0.98 ->
     // 0.94, x 144 1.09 -> 1.07; x 200, ten waves per SIMD: 1.37 -> 1.44,
     // profiles/r05_prio_ab.txt) — and off for flat batches (S2 8.66 -> 8.81 ms,
-    // 125k pairs 1.22 -> 1.25 ms). HC_PHMM_PRIO / HC_PHMM_PRIO64 override (A/B).
-    const int prio = int(env_i64("HC_PHMM_PRIO", !b->spec.flat && b->n_seg_waves > 0 &&
-                                                      int64_t(b->n_seg_waves) <= int64_t(8) * 4 * dv.n_cu
-                                                  ? 1 : 0));
+    // 125k pairs 1.22 -> 1.25 ms). HC_PHMM_PRIO / HC_PHMM_PRIO64 override (A/B,
+    // 0 or 1).
+    const int prio = env_i64("HC_PHMM_PRIO", !b->spec.flat && b->n_seg_waves > 0 &&
+                                                 int64_t(b->n_seg_waves) <= int64_t(8) * 4 * dv.n_cu
+                                             ? 1 : 0) != 0 ? 1 : 0;
     r.prio = int(env_i64("HC_PHMM_PRIO64", 1));
     r.raw32 = b->d_raw32;
     r.flag = b->d_flag;
     r.err = b->d_count + kErrWord;
-    r.force_plan_timeout = env_i64("HC_PHMM_TEST_PLAN_TIMEOUT", 0) != 0 ? 1 : 0;   // test hook
+    r.force_plan_timeout = test_plan_timeout() ? 1 : 0;   // test hook (hcx_test_plan_timeout), off in use
     // initNative(use_double = true): no fp32 pass, every pair to the fp64 one
     // (intel_pairhmm.hpp:71,81,135-140).
     const bool all_f64 = (b->spec.flags & HC_PHMM_FLAG_F64) != 0;   // the call's mode (PartSpec::flags)
@@ -106,19 +107,25 @@ int run_part(Part* b, hipStream_t s)
         b->inker_limit = a.inker_limit;
         if (env_i64("HC_PHMM_TIMELINE", 0) != 0 && b->n_seg_waves > 0) {
             // Diagnostics: this part's own record buffer (parts run concurrently
-            // on slot streams); hcx_timeline reads the last traced part.
-            if (b->timeline_n < b->n_seg_waves) {
+            // on slot streams); hcx_timeline reads the last traced part's fp32
+            // seg waves, hcx_timeline64 its fp64 waves (records after them).
+            const int need = b->n_seg_waves + int(b->n) + 1;   // + the fp64 plan's record
+            if (b->timeline_n < need) {
                 if (b->timeline) {
                     HIP_TRY(hipStreamSynchronize(s));
                     HIP_TRY(hipFree(b->timeline));
                     b->timeline = nullptr;
                 }
-                HIP_TRY(hipMalloc(&b->timeline, size_t(b->n_seg_waves) * 3 * sizeof(unsigned long long)));
-                b->timeline_n = b->n_seg_waves;
+                HIP_TRY(hipMalloc(&b->timeline, size_t(need) * 3 * sizeof(unsigned long long)));
+                b->timeline_n = need;
             }
+            b->timeline_n32 = b->n_seg_waves;
+            HIP_TRY(hipMemsetAsync(b->timeline + 3 * size_t(b->n_seg_waves), 0,
+                                   size_t(b->n + 1) * 3 * sizeof(unsigned long long), s));
             std::lock_guard<std::mutex> lk(g_tl.mu);
             g_tl.part = b;
             a.timeline = b->timeline;
+            r.timeline = b->timeline + 3 * size_t(b->n_seg_waves);
         }
         b->launch_waves += b->lane_waves;
         const int n_one = b->lane_waves - b->n_seg_waves;
@@ -131,20 +138,9 @@ int run_part(Part* b, hipStream_t s)
             g.n_waves = b->n_seg_waves;
             g.n_waves_dev = b->d_nwaves;
             g.sdesc = b->d_sdesc;
-            // HC_PHMM_PRIO=2: priority by remaining steps for the waves of the
-            // last round of slots only (the pass's drain).
-            g.prio_from = std::max(0, b->n_seg_waves - 3 * 4 * dv.n_cu);   // (3: phmm_seg_kernel occupancy)
-            // Persistent waves fetching from per-XCD queues
-            // (HC_PHMM_SEG_PERSIST=1) or one queue (=2); default 0: one wave
-            // per launched slot, the hardware dispatching them in order (the
-            // persistent forms measured no faster).
-            int max_waves = 0;
-            const int persist = int(env_i64("HC_PHMM_SEG_PERSIST", 0));
-            if (persist != 0) {
-                g.seg_counters = b->d_count;
-                g.n_tail = b->seg_tail;
-                max_waves = int(std::max<int64_t>(1, env_i64("HC_PHMM_SEG_WAVES_PER_SIMD", 3))) * 4 * dv.n_cu;
-            }
+            // One wave per launched slot, the hardware dispatching them in the
+            // plan's order (persistent waves fetching from per-XCD queues
+            // measured no faster and were removed).
             if (fork) {
                 HIP_TRY(hipEventRecord(b->fork, s));
                 HIP_TRY(hipStreamWaitEvent(b->side, b->fork, 0));
@@ -164,62 +160,19 @@ int run_part(Part* b, hipStream_t s)
             // launch follows (S1: that launch was ~6 us of a 73 us pass, for an
             // empty list). Larger parts keep the list: a region whose reads miss
             // many haps would serialise hundreds of rescues in its waves.
-            solo = !rec && persist == 0 && n_one == 0 && b->n_wide == 0 && b->cls[0].n == 0 && b->cls[1].n == 0 &&
+            solo = !rec && n_one == 0 && b->n_wide == 0 && b->cls[0].n == 0 && b->cls[1].n == 0 &&
                    a.inker_count != nullptr && b->Hmax <= kInWaveRescueMaxH &&
                    b->n <= env_i64("HC_PHMM_SOLO_MAX_PAIRS", 32768);
-            // Fused pass (kernels.hpp LaneArgs::fz_*): the part's rescues go on a
-            // queue that the waves done with their fp32 pairs drain while the
-            // others still run — no fp64 launch, no wait for the slowest fp32
-            // wave. Wide: every wave resident at once at kFusedOcc, haps up to
-            // kSeg64MaxH (S4: 2 000 pairs of 1-2 kb, 93 % rescued). Narrow: haps
-            // up to 512 in the fp32 pass's own registers, any part size (a wave
-            // takes queued rescues only once the launch's last wave has been
-            // dispatched: the 415 x 128 region's ~400 rescues run in its last
-            // round instead of a launch after it). Not with per-slot records
-            // (their gather is the fp64 launch's) or other fp32 kernels.
-            // HC_PHMM_FUSED: 0 (default) off; 1 where solo does not apply; 2
-            // also where solo would. Opt-in: measured slower than the fp64
-            // launch after the pass (S4 0.94 vs 0.74 ms, the 415 x 128 region
-            // call 1.10 vs 1.02 ms): the fp32 waves of the
-            // fused launch run at its occupancy beside fp64 rescues, and a
-            // rescue started by a late fp32 wave ends after the separate
-            // launch would have.
-            const int64_t fz = env_i64("HC_PHMM_FUSED", 0);
-            const bool fz_ok = fz != 0 && !rec && persist == 0 && n_one == 0 && b->n_wide == 0 && b->cls[0].n == 0 &&
-                               b->cls[1].n == 0 && (fz == 2 || !solo);
-            const bool fz_narrow = fz_ok && b->Hmax <= kInWaveRescueMaxH;
-            const bool fz_wide = fz_ok && !fz_narrow && b->Hmax <= kSeg64MaxH &&
-                                 int64_t(b->n_seg_waves) <= int64_t(kFusedOcc) * 4 * dv.n_cu;
-            if (fz_narrow || fz_wide) {
-                g.fz_wide = fz_wide ? 1 : 0;
-                solo = true;
-                g.solo_counters = b->d_count;
-                g.solo_other = par ^ 1;
-                g.fz_started = b->d_count + kFusedStarted + par;
-                g.fz_head = b->d_count + kFusedHeads + par * kFusedQueues;
-                g.err = b->d_count + kErrWord;
-                g.fz_prio = int(env_i64("HC_PHMM_FUSED_PRIO", 1));
-                g.prio64 = g.fz_prio ? 0 : r.prio;
-                g.force_wait_timeout = r.force_plan_timeout;
-                g.inker_count = nullptr;
-                b->inker_limit = 0;
-            } else if (solo) {
+            // (The fused pass — rescues drained by the fp32 launch's own waves —
+            // and stealable rescues measured slower than the fp64 launch after
+            // the pass and were removed)
+            if (solo) {
                 g.solo_counters = b->d_count;
                 g.solo_other = par ^ 1;
                 g.inker_limit = std::numeric_limits<int>::max();
                 b->inker_limit = g.inker_limit;
-            } else if (b->d_steal && a.inker_count != nullptr && env_i64("HC_PHMM_STEAL", 0) != 0) {
-                // Rescues a wave defers are taken by seg waves done with their
-                // own pairs before the fp64 launch plans the rest. Opt-in: the
-                // 415 x 128 region call measured 1.07 -> 1.18 ms with it (a
-                // stolen fp64 rescue holds a slot the pass's next fp32 wave
-                // needs, and the rescues of the last waves still leave the
-                // fp64 launch its one-rescue latency).
-                g.steal_list = r.steal_list = b->d_steal;
-                g.steal_count = b->d_count + kStealCount + par;
-                r.steal_count = g.steal_count;
             }
-            HIP_TRY(launch_lane_seg_f32(g, max_waves, persist == 2 ? 1 : 8, fork ? b->side : s));
+            HIP_TRY(launch_lane_seg_f32(g, fork ? b->side : s));
             if (fork) HIP_TRY(hipEventRecord(b->join, b->side));
         }
         if (n_one > 0) {
@@ -307,7 +260,6 @@ int check_device_error(const int* counters)
     if (e == 0) return HC_PHMM_OK;
     std::string m = "device pass incomplete (error word " + std::to_string(e) + ")";
     if (e & kErrPlanWait) m += ": fp64 rescue workgroups timed out waiting for the rescue plan";
-    if (e & kErrFusedWait) m += ": fused-pass waves timed out waiting for listed rescues";
     return fail(HC_PHMM_EHIP, m);
 }
 

@@ -469,51 +469,26 @@ __device__ __forceinline__ void run_seg_bc(const T* __restrict__ lut, const T* _
 // same run_seg in double) — so a batch with a few rescues (S2: ~2e-5 of
 // the pairs) needs no separate latency-bound pass after the fp32 kernel. The
 // others are appended to the rescue list for that pass.
-// fp64 recompute of pair rp by the whole wave (H <= kInWaveRescueMaxH: 64
-// lanes of 8 columns), raw f64 sum to raw64_zero[rp].
-// rs < 0 (a stolen rescue, another wave's pair): the raw f64 goes to
-// raw64_zero[rp] even with records (its record says kRecListed, which the
-// gather leaves to the rescue's own store).
-// MAXWI: the widest fp64 block width compiled in (seg64_width(MAXWI)): 0 =
-// 8 columns, H <= 512 (the in-wave rescue of the occupancy-3 fp32 kernel);
-// kSeg64Widths - 1 = 32 columns, H <= kSeg64MaxH (the fused pass). A pair
-// takes the narrowest width that covers its hap on 64 lanes.
-__device__ __forceinline__ int rescue_width_index(int H)
-{
-    const int need = (H + 63) >> 6;   // columns per lane on 64 lanes
-    return need <= 8 ? 0 : (need - 8 + 3) >> 2;
-}
-
-template <int MAXWI = 0>
+// fp64 recompute of pair rp (slot rs) by the whole wave: 64 lanes of 8
+// columns, raw f64 sum to the slot's record or raw64_zero[rp].
 __device__ __forceinline__ void rescue_one(const LaneArgs& a, const PairDesc pd, int rp, int rs, int lane,
-                                           uint2* __restrict__ mt, const double* __restrict__ slut64 = nullptr)
+                                           uint2* __restrict__ mt)
 {
-    const double* __restrict__ slut = slut64 ? slut64 : a.lut64;   // (compile-time at every call site)
     const int R = __builtin_amdgcn_readfirstlane(pd.y), H = __builtin_amdgcn_readfirstlane(pd.w);
     const int rx = __builtin_amdgcn_readfirstlane(pd.x);
     const LaneCtx cx{a.rows - kRowPadBefore, unsigned(rx + kRowPadBefore) * 4u, a.hapw,
                      unsigned(__builtin_amdgcn_readfirstlane(pd.z)) * 4u, R, H};
-    const int wi = MAXWI == 0 ? 0 : rescue_width_index(H);
-    const int bc = seg64_width(wi);
+    constexpr int bc = seg64_width(0);
     const int nb = (H + bc - 1) / bc;
-    const SegSteps st{R, R, R + nb - 1, MAXWI == 0 ? 0 : a.prio64};
+    const SegSteps st{R, R, R + nb - 1, 0};
     const uint32_t w1 = row_word(cx, 0);
     const double T0 = row0_t<double>(a.lut64, w1, H);
     const bool eq = read_eq(w1);
     double sM = 0.0, sX = 0.0;
-    switch (wi) {
-#define HC_RESCUE_CASE(WI) \
-    case WI: \
-        if constexpr (WI <= MAXWI) run_seg_bc<double, seg64_width(WI)>(a.lut64, slut, st, lane, lane, cx, T0, sM, sX, mt, eq); \
-        break;
-        HC_RESCUE_CASE(0) HC_RESCUE_CASE(1) HC_RESCUE_CASE(2) HC_RESCUE_CASE(3) HC_RESCUE_CASE(4) HC_RESCUE_CASE(5)
-        HC_RESCUE_CASE(6)
-#undef HC_RESCUE_CASE
-    default: break;
-    }
+    run_seg_bc<double, bc>(a.lut64, a.lut64, st, lane, lane, cx, T0, sM, sX, mt, eq);
     if (lane == nb - 1) {
         const double r = sM + sX;
-        if (a.rec && rs >= 0) {   // record of slot rs: state and raw f64 (after the owner's store: same wave, program order)
+        if (a.rec) {   // record of slot rs: state and raw f64 (after the owner's store: same wave, program order)
             const unsigned long long b = (unsigned long long)__double_as_longlong(r);
             uint4* q = a.rec + rs;
             q->y = kRecInWave;
@@ -526,28 +501,21 @@ __device__ __forceinline__ void rescue_one(const LaneArgs& a, const PairDesc pd,
 }
 
 // Rescue pair rp (slot rs, hap length H) in this wave if it qualifies and the
-// run's in-wave budget allows (wave-uniform), else append it to a list (lane
-// `owner_lane`): the stealable list if a wave can take it (H within reach),
-// else the fp64 launch's.
+// run's in-wave budget allows (wave-uniform), else append it to the fp64
+// launch's list (lane `owner_lane`).
 __device__ __forceinline__ void rescue_or_defer(const LaneArgs& a, bool few, int rp, int rs, int H, int lane,
                                                 int owner_lane, uint2* __restrict__ mt)
 {
-    const bool fits = H <= kInWaveRescueMaxH;
-    bool here = few && fits;
+    bool here = few && H <= kInWaveRescueMaxH;
     if (here) {
         int c = 0;
         if (lane == 0) c = atomicAdd(a.inker_count, 1);
         here = __builtin_amdgcn_readfirstlane(c) < a.inker_limit;
     }
-    if (here) {
+    if (here)
         rescue_one(a, a.sdesc[rs], rp, rs, lane, mt);   // sdesc[rs] = pairs[rp]
-    } else if (lane == owner_lane) {
-        if (a.steal_list && fits)   // (a swap: performed past this XCD's L2, seen by the other XCDs' waves)
-            (void)__hip_atomic_exchange(a.steal_list + atomicAdd(a.steal_count, 1), rp + 1, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-        else
-            a.rescue_list[atomicAdd(a.rescue_count, 1)] = rp;
-    }
+    else if (lane == owner_lane)
+        a.rescue_list[atomicAdd(a.rescue_count, 1)] = rp;
 }
 
 __device__ __forceinline__ void rescue_in_wave(const LaneArgs& a, uint64_t todo, int pid, int slot, int H, int lane,
@@ -563,113 +531,6 @@ __device__ __forceinline__ void rescue_in_wave(const LaneArgs& a, uint64_t todo,
         todo &= todo - 1;
         rescue_or_defer(a, few, __builtin_amdgcn_readlane(pid, l), __builtin_amdgcn_readlane(slot, l),
                         __builtin_amdgcn_readlane(H, l), lane, l, mt);
-    }
-}
-
-// A seg wave done with its own pairs rescues deferred pairs of other waves
-// (LaneArgs::steal_list). Lane 0 probes up to kStealProbes entries from a
-// per-wave pseudo-random start, swapping in kStealTaken: a pair id + 1 back
-// means the pair is this wave's to rescue; kStealTaken, another wave's; 0, a
-// slot reserved but not yet stored, whose writer's store then stands and the
-// fp64 launch plans it. No shared head, so waves finishing together do not
-// serialise on one atomic (a CAS-on-head first form made a 415 x 128 region
-// call 1.1 -> 9 ms).
-constexpr int kStealTaken = -1;
-constexpr int kStealProbes = 4;
-__device__ __forceinline__ void steal_rescues(const LaneArgs& a, int wid, int lane, uint2* __restrict__ mt)
-{
-    unsigned seed = unsigned(wid) * 2654435761u + 12345u;
-    for (;;) {
-        int v = 0;
-        if (lane == 0) {
-            const int c = __hip_atomic_load(a.steal_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (c > 0) {
-                int i = int(seed % unsigned(c));
-                for (int p = 0; p < kStealProbes && v <= 0; ++p) {
-                    v = __hip_atomic_exchange(a.steal_list + i, kStealTaken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (++i == c) i = 0;
-                }
-            }
-        }
-        v = __builtin_amdgcn_readfirstlane(v);
-        if (v <= 0) return;
-        rescue_one(a, a.pairs[v - 1], v - 1, -1, lane, mt);   // (uniform: rescue_one reads it with readfirstlane)
-        seed = seed * 1664525u + 1013904223u;
-    }
-}
-
-// The fused pass's rescue queue (LaneArgs::fz_*): this wave has appended its
-// flagged pairs; once every one of the launch's nw waves has been dispatched
-// (before that, a wave that stays for rescues holds a slot an undispatched
-// fp32 wave needs), it takes listed rescues, each recomputed in fp64 over its
-// 64 lanes (rescue_one: the rescue of intel_pairhmm.hpp:137-139, as the fp64
-// launch would), until none is listed. No wave ever waits for more: a wave
-// that lists a rescue checks the queue after listing it, so every listed pair
-// is taken by its own wave if by no other (the last waves' rescues run in
-// those waves). List index i is entry i / Q of queue i % Q (Q =
-// kFusedQueues): lanes 0..Q-1 read the Q heads in one load, and the wave
-// takes the first queue with an entry below the list length, starting from
-// its own (wid % Q), by compare-and-swap on that queue's head. (One head for
-// all: the hundreds of waves finishing together retried their CAS on one
-// word, each claim ~12 us, S4's pass 22 ms. A first form let idle waves poll
-// until every wave had finished its fp32 pairs: 2-30x slower.) The one wait,
-// for a claimed entry's swap to land, is bounded; giving up sets the part's
-// error word (the host fails the call). Returns the rescues taken (-1: left
-// before every wave had started), for the timeline.
-constexpr int kFusedWaitIters = 1 << 20;
-template <int MAXWI>
-__device__ __forceinline__ int fused_rescues(const LaneArgs& a, int nw, int wid, int lane, uint2* __restrict__ mt,
-                                             double* __restrict__ slut64)
-{
-    constexpr auto AG = __HIP_MEMORY_SCOPE_AGENT;
-    constexpr int Q = kFusedQueues;
-    static_assert(Q == 32, "the queue choice below rotates a 32-bit mask");
-    if (a.force_wait_timeout) {   // (test hook: as a wait that timed out)
-        if (lane == 0) __hip_atomic_fetch_or(a.err, kErrFusedWait, __ATOMIC_RELAXED, AG);
-        return 0;
-    }
-    int go = 0;
-    if (lane == 0) go = __hip_atomic_load(a.fz_started, __ATOMIC_RELAXED, AG) >= nw;
-    if (!__builtin_amdgcn_readfirstlane(go)) return -1;
-    int pref = wid & (Q - 1);
-    for (int n = 0;; ++n) {
-        const int c = __hip_atomic_load(a.rescue_count, __ATOMIC_RELAXED, AG);
-        const int h = lane < Q ? __hip_atomic_load(a.fz_head + lane, __ATOMIC_RELAXED, AG) : 0;
-        const uint32_t avail = uint32_t(__builtin_amdgcn_ballot_w64(lane < Q && h * Q + lane < c));
-        if (avail == 0) return n;
-        const uint32_t rot = pref == 0 ? avail : (avail >> pref) | (avail << (Q - pref));
-        const int q = (pref + __builtin_ctz(rot)) & (Q - 1);
-        const int hq = __builtin_amdgcn_readlane(h, q);
-        int v = 0;   // > 0: a claimed pair id + 1; -2: lost the race, retry
-        if (lane == 0) {
-            int hh = hq;
-            if (__hip_atomic_compare_exchange_strong(a.fz_head + q, &hh, hq + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED, AG)) {
-                // List index hq * Q + q: the appender has it; its swap of the
-                // entry follows. Taken by a swap with 0 (clean for the next
-                // run), performed where the appender's swap is.
-                const int idx = hq * Q + q;
-                int e = 0;
-                for (int it = 0; it < kFusedWaitIters; ++it) {
-                    e = __hip_atomic_exchange(a.rescue_list + idx, 0, __ATOMIC_RELAXED, AG);
-                    if (e != 0) break;
-                    __builtin_amdgcn_s_sleep(2);
-                }
-                if (e == 0) __hip_atomic_fetch_or(a.err, kErrFusedWait, __ATOMIC_RELAXED, AG);
-                v = e;
-            } else {
-                v = -2;
-            }
-        }
-        v = __builtin_amdgcn_readfirstlane(v);
-        pref = q;
-        if (v == -2) { --n; pref = (q + 1) & (Q - 1); continue; }
-        if (v == 0) return n;   // (gave up waiting: error word set)
-        if (n == 0) {   // this wave's fp64 prior table in LDS, as the fp64 launch has it
-            if (a.fz_prio) __builtin_amdgcn_s_setprio(0);
-            for (int t = lane; t < kSlutLen; t += 64) slut64[t] = a.lut64[t];
-            __builtin_amdgcn_wave_barrier();
-        }
-        rescue_one<MAXWI>(a, a.pairs[v - 1], v - 1, -1, lane, mt, slut64);   // inputs from earlier launches: no acquire
     }
 }
 

@@ -140,6 +140,7 @@ def lib():
     L.hc_phmm_batch_bind_outputs.argtypes = [C.c_void_p] * 4
     L.hc_phmm_batch_destroy.argtypes = [C.c_void_p]
     L.hc_phmm_get_luts.argtypes = [_f32p, _f64p, _f32p, _f64p]
+    L.hcx_test_plan_timeout.argtypes = [C.c_int]   # test hook (tests only)
     _lib = L
     return L
 

@@ -44,7 +44,9 @@
  * error is available from hc_phmm_last_error(). There is no CPU fallback:
  * without a usable MI355X the calls fail with HC_PHMM_ENODEV, and a device
  * pass that could not complete (a kernel reports it in the part's device
- * error word) fails with HC_PHMM_EHIP instead of returning partial results.
+ * error word) fails with HC_PHMM_EHIP. The contents of a failed call's
+ * output arrays are then unspecified (some pairs may already have been
+ * written): a caller must not use them.
  */
 #ifndef HC_PAIRHMM_H
 #define HC_PAIRHMM_H

@@ -165,16 +165,15 @@ def test_early_finish(engine, oracle_lib, monkeypatch, early):
         assert_same(engine.pairs(b), ref, f"early={early}")
 
 
-@pytest.mark.parametrize("order", ["tail", "snake", "tail_blocks"])
+@pytest.mark.parametrize("order", ["tail", "one_round", "tail_blocks"])
 def test_flat_dispatch_order_vs_oracle(engine, oracle_lib, monkeypatch, order):
     """The device-planned flat part's dispatch order (pack_kernels.hip
     flat_tail_kernel: coalesced passes, block-scanned bucket cursors, stable
     bulk compaction): a tail of shortest waves after the bulk (one round of
-    tail at ~6 000 waves), the one-round snake order (1 024 < waves <= 3 072),
-    and the tail with flat_prep_kernel on a bounded grid (several pairs per
-    wave); every pair against the oracle."""
-    if order == "snake":
-        monkeypatch.setenv("HC_PHMM_ONE_ROUND_SNAKE", "1")
+    tail at ~6 000 waves), a one-round plan (1 024 < waves <= 3 072), and the
+    tail with flat_prep_kernel on a bounded grid (several pairs per wave);
+    every pair against the oracle."""
+    if order == "one_round":
         b = W.generate(9000, (100, 500), (40, 250), 0.01, seed=61)
     else:
         monkeypatch.setenv("HC_PHMM_TAIL_ROUNDS", "1")
@@ -261,3 +260,33 @@ def test_submit_unwinds_on_exception(engine, oracle_lib, many_parts):
     engine.shutdown()            # refused if any part had leaked
     engine.init(0)
     assert_same(engine.pairs(b), ref, "after unwinding")
+
+
+@pytest.mark.parametrize("case", ["read_n_unsampled", "hap_n_unsampled", "low_qual", "n_and_gaps", "many_n"])
+def test_flat_compact_fallbacks(engine, oracle_lib, case):
+    """The flat call's compact record fields (one byte per read base, 2-bit
+    hap codes) cannot hold an 'N' or a quality below 33: a part whose sample
+    shows one starts with the nibble fields; one the sample misses (a single
+    'N' read, 'N' hap or low quality between the sampled pairs) is refused in
+    pass 2 and planned again with the nibble fields, and one that also has a
+    read with varying gap qualities is planned again scanning every read
+    (flat_plan.cpp plan_flat_device). Every case against the oracle."""
+    b = W.config("S2", 20000)
+    rs, q, hap = b["rs"].copy(), b["q"].copy(), b["hap"].copy()
+    ro, ho = b["read_off"], b["hap_off"]
+    if case in ("read_n_unsampled", "n_and_gaps"):
+        rs[ro[7] + 3] = ord("N")        # pair 7: not on the 1-in-19 sample
+    if case == "hap_n_unsampled":
+        hap[ho[13] + 5] = ord("N")
+    if case == "low_qual":
+        q[ro[11] + 2] = 32 + 128        # (& 127) = 32: below the compact quality base
+    if case == "many_n":
+        rng = np.random.default_rng(3)
+        for p in rng.choice(len(b["R"]), 300, replace=False):
+            rs[ro[p] + rng.integers(0, b["R"][p])] = ord("N")
+    b = dict(b, rs=rs, q=q, hap=hap)
+    if case == "n_and_gaps":
+        ins = b["ins"].copy()
+        ins[ro[29] + 1] = ord("J")      # pair 29's gap qualities vary
+        b = dict(b, ins=ins)
+    assert_same(engine.pairs(b), oracle_lib.pairs(b, nthreads=16), case)

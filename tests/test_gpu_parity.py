@@ -304,20 +304,16 @@ def test_repeated_runs_reuse_rescue_counters(engine, oracle_lib):
     bt.close()
 
 
-@pytest.mark.parametrize("in_wave", ["on", "off", "fused-off"])
+@pytest.mark.parametrize("in_wave", ["on", "off"])
 @pytest.mark.parametrize("shape", ["short_list", "mid_list", "long_list", "wide_haps"])
 def test_fp64_rescue_tiers(engine, oracle_lib, monkeypatch, shape, in_wave):
     """The fp64 rescue pass is planned on the device: block width 8 / 16 / 32
     by rescue-list size (a short list is latency-bound), pairs binned into
     2^k-lane classes, haps too wide for 64 blocks of 32 on the anti-diagonal
     fp64 kernel. High substitution rates force most pairs into rescue. With
-    in_wave on, fp32 waves holding one or two rescued pairs (H <= 1024)
-    recompute them themselves (short_list is mostly that path). Small parts
-    with haps past 512 take the fused pass by default (short / mid lists);
-    fused-off sends them through the fp64 launch's tiers as well."""
+    in_wave on, fp32 waves holding one or two rescued pairs (H <= 512)
+    recompute them themselves (short_list is mostly that path)."""
     monkeypatch.setenv("HC_PHMM_RESCUE_IN_WAVE", "0" if in_wave == "off" else "1")
-    if in_wave == "fused-off":
-        monkeypatch.setenv("HC_PHMM_FUSED", "0")
     n, h, r = {"short_list": (40, (300, 900), (100, 250)),
                "mid_list": (1500, (600, 1100), (150, 250)),
                "long_list": (4500, (1000, 1200), (150, 250)),
@@ -447,15 +443,13 @@ def test_use_double_every_golden_pair(engine, golden, golden_batch):
     assert np.array_equal(res["rescued"], golden["rescued"])
 
 
-@pytest.mark.parametrize("variant", ["persist-xcd", "persist-one", "prio32", "prio64-off", "records"])
+@pytest.mark.parametrize("variant", ["prio32", "prio64-off", "records"])
 def test_schedule_variants_are_bit_identical(engine, golden, golden_batch, variant, monkeypatch):
-    """How waves are scheduled never changes a result: the persistent fp32
-    pass (per-XCD queues / one queue, HC_PHMM_SEG_PERSIST=1/2)
-    and the issue-priority switches give the default's bits on a 125k-pair S2
-    shard (more waves than wave slots, so the persistent kernel really fetches)
-    run twice (the counters it zeroes for the next run), and on the golden set."""
-    env = {"persist-xcd": ("HC_PHMM_SEG_PERSIST", "1"), "persist-one": ("HC_PHMM_SEG_PERSIST", "2"),
-           "prio32": ("HC_PHMM_PRIO", "1"), "prio64-off": ("HC_PHMM_PRIO64", "0"),
+    """How waves are scheduled never changes a result: the issue-priority
+    switches and per-slot records give the default's bits on a 125k-pair S2
+    shard (more waves than wave slots) run twice (the counters it zeroes for
+    the next run), and on the golden set."""
+    env = {"prio32": ("HC_PHMM_PRIO", "1"), "prio64-off": ("HC_PHMM_PRIO64", "0"),
            "records": ("HC_PHMM_REC_MIN_PAIRS", "0")}[variant]
     b = W.config("S2", 125_000)
     ref = engine.pairs(b)
@@ -502,18 +496,14 @@ def test_small_part_rescues_in_its_waves(engine, oracle_lib, monkeypatch, solo):
     bt.close()
 
 
-@pytest.mark.parametrize("mode", ["steal", "steal-records", "no-steal"])
-def test_stolen_rescues(engine, oracle_lib, monkeypatch, mode):
-    """Rescues a seg wave defers (past the in-wave limits) with H <= 512 go to
-    the stealable list; seg waves done with their own pairs take entries and
-    rescue them in fp64, the fp64 launch plans the untaken ones with the
-    list's (haps past 512). A batch above the solo size with most pairs
-    rescued (H 100-900), three runs through one prepared batch (the list is
-    zeroed for the next run, its counters by run parity), against the oracle;
-    with per-slot records (a stolen rescue writes its pair's raw f64 itself)
-    and with stealing off."""
-    monkeypatch.setenv("HC_PHMM_STEAL", "0" if mode == "no-steal" else "1")
-    if mode == "steal-records":
+@pytest.mark.parametrize("mode", ["list", "records"])
+def test_rescue_heavy_part(engine, oracle_lib, monkeypatch, mode):
+    """Rescues a seg wave defers (past the in-wave limits) go to the fp64
+    launch's list. A batch above the solo size with most pairs rescued (H
+    100-900), three runs through one prepared batch (the counters go by run
+    parity), against the oracle; with per-slot records (the in-wave rescues
+    write their pair's raw f64 into the record) and without."""
+    if mode == "records":
         monkeypatch.setenv("HC_PHMM_REC_MIN_PAIRS", "0")
     b = W.generate(40000, (100, 900), (60, 200), 0.08, seed=29)
     ref = oracle_lib.pairs(b, nthreads=16)
@@ -568,37 +558,40 @@ def test_seg_records_and_gather_with_mixed_kernels(engine, oracle_lib, monkeypat
     bt.close()
 
 
-@pytest.mark.parametrize("plan", ["static", "dynamic", "fused"])
+@pytest.mark.parametrize("plan", ["static", "dynamic"])
 def test_rescue_plan_timeout_is_an_error(engine, oracle_lib, monkeypatch, plan):
     """A fp64 workgroup that gives up waiting for the device-made rescue plan
     (lane_kernel.hip phmm_seg64_kernel, bounded wait) sets the part's device
     error word, and the call fails with HC_PHMM_EHIP instead of returning
-    results (verdict round 4). HC_PHMM_TEST_PLAN_TIMEOUT=1 makes every
-    non-planner workgroup time out at once: a static plan (S4-200: fewer waves
-    than two per SIMD) and a dynamic one (thousands of long rescued pairs),
-    through a flat call and a prepared batch; the batch then runs correctly
-    once the hook is off (the error word is cleared when reported). fused:
-    S4-200 through the fused pass, where the hook makes every wave give up at
-    the rescue queue (a wait that timed out: kErrFusedWait); static: the same
-    pairs through the fp64 launch (HC_PHMM_FUSED=0)."""
+    results (verdict round 4). The test-only entry point hcx_test_plan_timeout
+    (no environment variable: the release library never reads one for it)
+    makes every non-planner workgroup time out at once: a static plan (S4-200:
+    fewer waves than two per SIMD) and a dynamic one (thousands of long
+    rescued pairs), through a flat call and a prepared batch; the batch then
+    runs correctly once the hook is off (the error word is cleared when
+    reported)."""
     import hcphmm
-    monkeypatch.setenv("HC_PHMM_FUSED", "1" if plan == "fused" else "0")
-    if plan in ("static", "fused"):
+    if plan == "static":
         b = W.subset(W.config("S4"), np.arange(200))
     else:
         b = W.generate(4000, (1000, 1500), (150, 250), 0.08, seed=71)
     ref = oracle_lib.pairs(b, nthreads=16)
     assert ref["rescued"].sum() > (3000 if plan == "dynamic" else 100)
     bt = engine.Batch(b)
-    monkeypatch.setenv("HC_PHMM_TEST_PLAN_TIMEOUT", "1")
-    with pytest.raises(hcphmm.PairHMMError) as e:
-        engine.pairs(b)
-    assert e.value.code == hcphmm.EHIP and ("listed rescues" if plan == "fused" else "rescue plan") in str(e.value)
-    bt.run()
-    with pytest.raises(hcphmm.PairHMMError) as e:
-        bt.results()
-    assert e.value.code == hcphmm.EHIP
-    monkeypatch.delenv("HC_PHMM_TEST_PLAN_TIMEOUT")
+    L = hcphmm.lib()
+    monkeypatch.setenv("HC_PHMM_TEST_PLAN_TIMEOUT", "1")   # (ignored: no release path reads it)
+    assert_same(engine.pairs(b), ref, f"{plan}: env var ignored")
+    L.hcx_test_plan_timeout(1)
+    try:
+        with pytest.raises(hcphmm.PairHMMError) as e:
+            engine.pairs(b)
+        assert e.value.code == hcphmm.EHIP and "rescue plan" in str(e.value)
+        bt.run()
+        with pytest.raises(hcphmm.PairHMMError) as e:
+            bt.results()
+        assert e.value.code == hcphmm.EHIP
+    finally:
+        L.hcx_test_plan_timeout(0)
     bt.run()
     assert_same(bt.results(), ref, f"{plan}: after the hook")
     bt.close()
@@ -634,21 +627,17 @@ def test_mode_is_per_call_and_fixed_at_submit(engine, golden, golden_batch):
     assert L.shape[1] == len(haps) and len(kept) == L.shape[0]
 
 
-@pytest.mark.parametrize("mode", ["on", "forced", "off"])
 @pytest.mark.parametrize("shape", ["S4", "S4-300", "many-per-wave", "short-haps", "big-narrow"])
-def test_fused_pass(engine, oracle_lib, monkeypatch, shape, mode):
-    """The fused pass (run.cpp, kernels.hpp LaneArgs::fz_*): a small part's
-    waves list their rescues on a queue and drain it themselves, no fp64
-    launch (HC_PHMM_FUSED, opt-in: on = where the solo path does not apply,
-    forced = whenever it applies, off = the default fp64 launch). configs[4] (S4, 2 000 pairs, 93 % rescued) and a
-    subset; 8 000 pairs of 520-700 bases four to a wave, most rescued (a wave
-    lists several, other waves take them); short haps (the solo path's domain
-    unless forced); a 60k-pair part of 300-500-base haps (the narrow form at
-    the fp32 pass's occupancy: more waves than slots, rescues taken once the
-    last wave is dispatched). Flat call and a prepared batch run three times (the queue
-    counters go by run parity, the entries are zeroed by their consumers),
-    against the oracle; the rescued count is the oracle's."""
-    monkeypatch.setenv("HC_PHMM_FUSED", {"on": "1", "forced": "2", "off": "0"}[mode])
+def test_rescue_shapes(engine, oracle_lib, shape):
+    """Rescue-heavy parts through the default schedule (the fp64 launch after
+    the fp32 pass, or the solo path for small parts of short haps):
+    configs[4] (S4, 2 000 pairs, 93 % rescued) and a subset; 8 000 pairs of
+    520-700 bases four to a wave, most rescued; short haps (the solo path); a
+    60k-pair part of 300-500-base haps (more waves than slots). Flat call and
+    a prepared batch run three times (the counters go by run parity), against
+    the oracle; the rescued count is the oracle's. (These were the fused
+    pass's cases; that opt-in schedule measured slower and was removed,
+    DESIGN.md §16.1.)"""
     b = {"S4": lambda: W.config("S4"),
          "S4-300": lambda: W.subset(W.config("S4"), np.arange(300)),
          "many-per-wave": lambda: W.generate(8000, (520, 700), (60, 200), 0.08, seed=41),
@@ -657,15 +646,13 @@ def test_fused_pass(engine, oracle_lib, monkeypatch, shape, mode):
     ref = oracle_lib.pairs(b, nthreads=16)
     n_resc = int(ref["rescued"].sum())
     assert n_resc > (500 if shape == "big-narrow" else len(b["R"]) // 3)
-    assert_same(engine.pairs(b), ref, f"{shape}/{mode} flat")
+    assert_same(engine.pairs(b), ref, f"{shape} flat")
     bt = engine.Batch(b)
     for k in range(3):
         bt.run()
         got = bt.results()
-        assert_same(got, ref, f"{shape}/{mode} run {k}")
+        assert_same(got, ref, f"{shape} run {k}")
         assert (got["raw_f64"][~ref["rescued"].astype(bool)] == 0).all()
     st = bt.stats()
     assert st.n_rescued == n_resc
-    if mode != "off":
-        assert st.kernel_ms_f64 == 0   # no fp64 launch: the fused (or solo) pass did every rescue
     bt.close()

@@ -1,4 +1,4 @@
-"""One line from a bench.py JSON output: headline, roofline and the secondary
+"""One line from a bench.py detail file (HC_BENCH_DETAIL): headline, roofline and the secondary
 configs' device times (tools/gpu_run.sh prints it after each bench step)."""
 import json
 import sys

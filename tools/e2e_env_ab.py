@@ -2,7 +2,7 @@
 log10 likelihoods out) under HC_PHMM_* settings in one process: per setting a
 first call, then the median of 5, alternating settings over 3 rounds so host
 drift hits each alike; results checked identical across settings.
-    python tools/e2e_env_ab.py HC_PHMM_FLAT_COMPACT=0,1 [HC_PHMM_PART_TAPER_PCT=50,100]
+    python tools/e2e_env_ab.py HC_PHMM_FLAT_COMPACT=0,1 [HC_PHMM_PART_GROWTH_PCT=100,125]
 Several VAR=... arguments form their cross product."""
 import itertools
 import json

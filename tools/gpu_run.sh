@@ -41,9 +41,10 @@ for step in "$@"; do
       rc=$?; tail -2 $OUT/smoke.log ;;
     bench)
       n=$(ls $OUT | grep -c '^bench')
-      timeout -k 10 600 python3 bench.py ${arg//,/ } > $OUT/bench_$n.json 2> $OUT/bench_$n.err
+      HC_BENCH_DETAIL=$PWD/$OUT/bench_${n}_detail.json timeout -k 10 600 python3 bench.py ${arg//,/ } \
+          > $OUT/bench_$n.json 2> $OUT/bench_$n.err
       rc=$?
-      [ $rc -eq 0 ] && python3 tools/bench_brief.py $OUT/bench_$n.json ;;
+      [ $rc -eq 0 ] && python3 tools/bench_brief.py $OUT/bench_${n}_detail.json && wc -c $OUT/bench_$n.json ;;
     profile)
       timeout -k 10 900 bash tools/profile_cfg.sh ${arg//,/ } > $OUT/profile_${arg//,/_}.log 2>&1
       rc=$?; tail -1 $OUT/profile_${arg//,/_}.log | cut -c1-600 ;;

@@ -32,7 +32,7 @@ def role(op, txt):
         return "handoff (DPP)"
     if op in ("v_mul_f32", "v_add_f32", "v_mul_f64", "v_add_f64"):
         return "cell arithmetic"
-    if op in ("v_bfe_i32", "v_bitop3_b32", "v_bitop3_b16"):
+    if op in ("v_bfe_i32", "v_bitop3_b32", "v_bitop3_b16", "v_bfi_b32"):
         return "prior select"
     if op.startswith("v_cndmask") or op == "v_and_b32" and ("v" in txt.split(",")[-1] and "0x" not in txt):
         return "hand-off mask"
@@ -66,18 +66,27 @@ def main():
     end = next(i for i in range(start + 1, len(lines)) if lines[i].startswith(".Lfunc_end"))
     loops = collections.defaultdict(list)   # header -> [(op, txt)]
     cur = None
+    lab = None   # the last label: its loop-header note may follow on a comment line
     for ln in lines[start:end]:
         m = re.match(r"^\.(LBB\w+):\s*;?\s*(.*)$", ln)
         if m:
             lab, com = m.group(1), m.group(2)
             h = re.search(r"Header=(BB\w+)", com)
             if "Loop Header" in com:
-                cur = lab[1:] if lab.startswith("L") else lab
+                cur = lab[1:]
             elif h:
                 cur = h.group(1)
             else:
                 cur = None
             continue
+        if lab is not None and re.match(r"^\s+;.*Loop Header", ln):
+            # ".LBBx:  ; Parent Loop BBy" then ";  =>  This Inner Loop Header":
+            # the label heads an inner loop (a one-block step loop has no
+            # other member blocks, so without this it was missed).
+            cur = lab[1:]
+            continue
+        if not ln.lstrip().startswith(";"):
+            lab = None
         s = ln.strip()
         if cur is None or not s or s.startswith(";") or s.startswith("."):
             continue

@@ -1,6 +1,6 @@
 # A/B on one box: a saved library (ab_libs/libhcpairhmm_$BASE.so, default r3) against
 # this tree's library under the variants in VARIANTS ("tag:ENV=V[,ENV=V]" ...;
-# default: the persistent seg pass off / per-XCD queues / one queue), at S2
+# default: this tree's defaults only), at S2
 # and its shards (PAIRS); 20 timed steps each, bench.py's HIP-event times.
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -15,7 +15,7 @@ run() {  # tag n env...
 for rep in 1 2; do
   for n in ${PAIRS:-125000 250000 1000000}; do
     [ -n "$NO_R3" ] || run ${BASE:-r3}_$rep $n HC_PHMM_LIB=$PWD/ab_libs/libhcpairhmm_${BASE:-r3}.so || exit 1
-    for v in ${VARIANTS:-p0:HC_PHMM_SEG_PERSIST=0 p1:HC_PHMM_SEG_PERSIST=1 p2:HC_PHMM_SEG_PERSIST=2}; do
+    for v in ${VARIANTS:-tree:HC_PHMM_TRACE_UNSET=1}; do
       tag=${v%%:*}; envs=${v#*:}
       run ${tag}_$rep $n ${envs//,/ } || exit 1
     done

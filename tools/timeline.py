@@ -5,9 +5,6 @@ last wave starts, how busy the wave slots are over time (tenths of the span),
 the idle slot-time at the end, wave duration spread.
     HC_PHMM_TIMELINE=1 python tools/timeline.py S2:125000 [out.npy]
     HC_PHMM_TIMELINE=1 python tools/timeline.py cross:415:128     (the region call's own plan)
-With the fused pass (HC_PHMM_FUSED, LaneArgs::fz_*) the third word is instead
-(time in queued rescues << 16) | rescues taken (0xffff: the wave left before
-every wave had started); the summary then describes the rescue phase.
 """
 import ctypes as C
 import json
@@ -78,21 +75,6 @@ out["simd_last_end_us"] = dict(p10=round(float(np.percentile(se_arr, 10)), 1), p
 out["start_us_first_3072"] = dict(p50=round(float(np.median(np.sort(start)[:3072])), 2),
                                   max=round(float(np.sort(start)[min(3071, nw - 1)]), 2))
 out["in_order_start_corr"] = round(float(np.corrcoef(order, start)[0, 1]), 3)
-if os.environ.get("FUSED_WORDS"):
-    nres = (hw & 0xFFFF).astype(np.int64)
-    gone = nres == 0xFFFF
-    tres = (hw >> 16) / 100.0
-    fin = end + tres
-    took = ~gone & (nres > 0)
-    out = {k: out[k] for k in ("workload", "waves", "kernel_ms_f32", "last_start_us", "first_end_us", "dur_us")}
-    out.update(fp32_end_us=dict(p50=round(float(np.median(end)), 1), max=round(float(end.max()), 1)),
-               left_before_all_started=int(gone.sum()), took_none=int((~gone & (nres == 0)).sum()),
-               took_some=int(took.sum()), rescues_taken=int(nres[~gone].sum()),
-               per_taker=dict(p50=float(np.median(nres[took])) if took.any() else 0, max=int(nres[~gone].max())),
-               rescue_us_per_rescue=round(float(tres[took].sum() / max(1, nres[took].sum())), 1),
-               final_end_us=round(float(fin.max()), 1))
-    tt = np.linspace(0, fin.max(), 21)[1:-1]
-    out["in_rescues"] = [int(((end <= t) & (fin > t) & took).sum()) for t in tt]
 print(json.dumps(out), flush=True)
 if len(sys.argv) > 2:
     np.save(sys.argv[2], rec)
