@@ -135,6 +135,10 @@ extern int64_t g_active_calls;
 extern std::atomic<uint32_t> g_flags;
 
 int init_devices_locked(const int32_t* devices, int32_t n, bool any_ok);
+// Slots made at hc_phmm_init per device (a flat call of S2's size runs 8
+// parts; more are made on demand).
+constexpr int kInitSlots = 8;
+Slot* make_slot();   // a new idle slot of the current device (streams, events)
 Slot* take_slot(Device& d);
 void give_slot(Slot* s);
 int slot_reserve(Slot& s, size_t dev_bytes, size_t host_bytes);

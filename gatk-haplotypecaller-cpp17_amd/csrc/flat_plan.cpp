@@ -666,7 +666,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     const size_t o_rec = L.take(sizeof(uint4) * n1);   // seg slot records (every pair is a seg pair)
     const size_t o_slotof = L.take(sizeof(int) * n1);
     const size_t o_sdesc = L.take(sizeof(PairDesc) * n1);
-    const size_t o_sorted = L.take(sizeof(int) * n1);
+    const size_t o_sorted = L.take(2 * sizeof(int) * n1);   // pair ids, then their R (Seg64Args::sorted_r)
     const size_t o_worder = L.take(sizeof(int) * n1);
     const size_t o_big = L.take(sizeof(int) * n1);
     const size_t o_bigc = L.take(sizeof(int));
@@ -806,7 +806,10 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
             }
         }
         tm.mark("flat: fill + H2D");
-        if (record_rate && spec.cells > 0) {   // running mean over calls (weight 1/2 to the newest part)
+        // Running mean over calls (weight 1/2 to the newest part), of parts
+        // large enough to be pipeline parts (a small call's rate is its fixed
+        // costs': hc_phmm_init's warm-up call would read as slow staging).
+        if (record_rate && spec.cells >= 5e8) {
             const double ps = std::chrono::duration<double, std::pico>(t_stage).count() / spec.cells;
             double old_ps = dv.stage_ps_per_cell.load(std::memory_order_relaxed);
             while (!dv.stage_ps_per_cell.compare_exchange_weak(old_ps, old_ps > 0 ? 0.5 * (old_ps + ps) : ps,

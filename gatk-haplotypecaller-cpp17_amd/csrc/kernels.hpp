@@ -114,13 +114,13 @@ struct Seg64Args {
     int* ticket_reset;        // the other run parity's ticket and flag, zeroed for the next run
     int* ready_reset;
     int* sorted;              // list in class order (n entries)
+    int* sorted_r;            // each sorted entry's R (n entries; the wave costs read it)
     int* big;                 // last-class pairs (anti-diagonal fp64 kernel)
     int* big_count;
     Seg64Plan* plan;
     double* raw_out;          // raw f64 sums by pair id
     long long min_lanes;      // narrower blocks below this many lanes at bc = 32
     int* wave_order;          // dispatch position -> wave (n entries), see rescue_plan_kernel
-    int order_mode;           // one-round plans: 1 heaviest with lightest per SIMD; 2 the heaviest alone first
     int* next_wave;           // dynamic wave counter (zeroed by the plan)
     int n_simd;               // SIMDs of the device (4 per CU)
     // Gather of the seg slots' result records (LaneArgs::rec) into the

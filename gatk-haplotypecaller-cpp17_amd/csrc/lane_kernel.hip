@@ -228,12 +228,15 @@ __device__ __forceinline__ int rescue_class(int H, int bc0)
 // counting sort over 256 cost buckets (order inside a bucket is arbitrary).
 constexpr int kMaxSortWaves = 8192;
 constexpr int kPlanThreads = 256;   // the planning workgroup (a phmm_seg64_kernel workgroup)
+constexpr int kPlanPhases = 6;      // (diagnostics) the planner's phase stamps
 
 struct PlanLds {
     int cnt[kSeg64Classes], fill[kSeg64Classes], wbase[kSeg64Classes];
-    int hist[256];
+    int cnt3[3][kSeg64Classes];   // class counts at bc0 = 32, 16, 8 (one walk counts all three)
+    alignas(16) int hist[256];
     unsigned long long lanes;
     unsigned cmax;
+    unsigned long long phase[kPlanPhases];
     unsigned cost[kMaxSortWaves];
 };
 
@@ -260,67 +263,86 @@ __device__ __forceinline__ WaveSpan wave_span(const PlanLds& L, int w)
 
 // The planner is one workgroup walking the list, so its time is load
 // latency: each thread takes kPlanBatch entries at a time and issues their
-// independent loads together (the list entries, then their pairs' H) instead
-// of one dependent pair per step (S4's 1 861 rescues: one round of loads).
+// independent loads together (the list entries, then their pairs' R and H)
+// instead of one dependent pair per step (S4's 1 861 rescues: one round of
+// loads). f(pid, R, H) per listed pair.
 constexpr int kPlanBatch = 8;
 template <typename F>
 __device__ __forceinline__ void plan_walk(const Seg64Args& a, int n, F&& f)
 {
     for (int b = threadIdx.x; b < n; b += kPlanBatch * kPlanThreads) {
-        int pid[kPlanBatch], h[kPlanBatch];
+        int pid[kPlanBatch];
+        int2 rh[kPlanBatch];
 #pragma unroll
         for (int k = 0; k < kPlanBatch; ++k) {
             const int i = b + k * kPlanThreads;
             pid[k] = i < n ? a.list[i] : -1;
         }
 #pragma unroll
-        for (int k = 0; k < kPlanBatch; ++k) h[k] = pid[k] >= 0 ? a.pairs[pid[k]].w : 0;
+        for (int k = 0; k < kPlanBatch; ++k) {   // the descriptor {rows, R, table, H}: R and H
+            const int2* d = reinterpret_cast<const int2*>(a.pairs + (pid[k] >= 0 ? pid[k] : 0));
+            rh[k] = pid[k] >= 0 ? make_int2(d[0].y, d[1].y) : make_int2(0, 0);
+        }
 #pragma unroll
         for (int k = 0; k < kPlanBatch; ++k)
-            if (pid[k] >= 0) f(pid[k], h[k]);
+            if (pid[k] >= 0) f(pid[k], rh[k].x, rh[k].y);
     }
 }
 
 // Modelled costs of waves [0, W) into L.cost (and their maximum into L.cmax):
-// (rows + skew) steps x (14 ops per column + ~40 per step); batched like
-// plan_walk (the first pair of kPlanBatch waves at once, then the rest).
+// (rows + skew) steps x (14 ops per column + ~40 per step), the rows from
+// sorted_r (written by the scatter: no dependent load of the descriptors).
 __device__ __forceinline__ void wave_costs(const Seg64Args& a, PlanLds& L, int W)
 {
     for (int b = threadIdx.x; b < W; b += kPlanBatch * kPlanThreads) {
         WaveSpan sp[kPlanBatch];
-        int s0[kPlanBatch], r[kPlanBatch];
+        int r[kPlanBatch];
 #pragma unroll
         for (int k = 0; k < kPlanBatch; ++k) {
             const int w = b + k * kPlanThreads;
             sp[k] = w < W ? wave_span(L, w) : WaveSpan{0, 0, 0, 0};
-            s0[k] = sp[k].e0 < sp[k].e1 ? a.sorted[sp[k].e0] : -1;
         }
 #pragma unroll
-        for (int k = 0; k < kPlanBatch; ++k) r[k] = s0[k] >= 0 ? a.pairs[s0[k]].y : 0;
+        for (int k = 0; k < kPlanBatch; ++k) r[k] = sp[k].e0 < sp[k].e1 ? a.sorted_r[sp[k].e0] : 0;
+        unsigned cm = 0;
 #pragma unroll
         for (int k = 0; k < kPlanBatch; ++k) {
 #pragma unroll 4
-            for (int e = sp[k].e0 + 1; e < sp[k].e1; ++e) r[k] = max(r[k], a.pairs[a.sorted[e]].y);
+            for (int e = sp[k].e0 + 1; e < sp[k].e1; ++e) r[k] = max(r[k], a.sorted_r[e]);
             const int w = b + k * kPlanThreads;
             if (w < W) {
                 const unsigned c = unsigned(r[k] + (1 << sp[k].kk) - 1) * unsigned(sp[k].bc * 14 + 40);
                 L.cost[w] = c;
-                atomicMax(&L.cmax, c);
+                cm = max(cm, c);
             }
         }
+        if (cm) atomicMax(&L.cmax, cm);
     }
+}
+
+// (diagnostics) phase stamp i of the planner, after a barrier
+__device__ __forceinline__ void plan_stamp(const Seg64Args& a, PlanLds& L, int i)
+{
+    if (a.timeline && threadIdx.x == 0) L.phase[i] = __builtin_amdgcn_s_memrealtime();
 }
 
 // The fp64 pass's plan over the n > 0 listed pairs, by one workgroup of the
 // fp64 launch (the first to arrive; the others wait for its flag): the width
 // bound bc0 (32 unless the lanes at width 32 give fewer than min_lanes, 2
 // waves per SIMD, then 16, then 8), the classes, the list scattered into class
-// order (`sorted`; the last class into `big`), and the dispatch order.
+// order (`sorted`, with each pair's R in `sorted_r`; the last class into
+// `big`), and the dispatch order. Its time is on the pass's critical path
+// (every other workgroup waits) and it is load latency, so the list is walked
+// twice only: once counting the classes at all three candidate bc0 together
+// (with the lanes that choose bc0), once scattering; the wave costs read R
+// from sorted_r. (Three walks and the costs' dependent descriptor loads:
+// 55 us from the fp32 pass's last wave to the first fp64 wave on S4, 91 us on
+// S4-20k, profiles/r06_timeline_*.)
 __device__ void plan_rescue(const Seg64Args& a, int n, PlanLds& L)
 {
     constexpr int NC = kSeg64Classes;
     const int t = threadIdx.x;
-    if (t < NC) L.cnt[t] = 0;
+    for (int q = t; q < 3 * NC; q += kPlanThreads) (&L.cnt3[0][0])[q] = 0;
     if (t == 0) {
         L.lanes = 0;
         L.cmax = 1;
@@ -328,42 +350,55 @@ __device__ void plan_rescue(const Seg64Args& a, int n, PlanLds& L)
     }
     __syncthreads();
     unsigned long long mine = 0;
-    plan_walk(a, n, [&](int, int H) { mine += (H + 31) / 32; });
-    if (mine) atomicAdd(&L.lanes, mine);
+    plan_walk(a, n, [&](int, int, int H) {
+        mine += (H + 31) / 32;
+        atomicAdd(&L.cnt3[0][rescue_class(H, 32)], 1);
+        atomicAdd(&L.cnt3[1][rescue_class(H, 16)], 1);
+        atomicAdd(&L.cnt3[2][rescue_class(H, 8)], 1);
+    });
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) mine += __shfl_xor(mine, d, 64);
+    if (__lane_id() == 0 && mine) atomicAdd(&L.lanes, mine);
     __syncthreads();
+    plan_stamp(a, L, 0);
     const long long l32 = (long long)L.lanes;
-    const int bc0 = l32 >= a.min_lanes ? 32 : (2 * l32 >= a.min_lanes ? 16 : 8);
-    plan_walk(a, n, [&](int, int H) { atomicAdd(&L.cnt[rescue_class(H, bc0)], 1); });
-    __syncthreads();
+    const int b3 = l32 >= a.min_lanes ? 0 : (2 * l32 >= a.min_lanes ? 1 : 2);
+    const int bc0 = 32 >> b3;
     if (t == 0) {
         Seg64Plan* __restrict__ p = a.plan;   // written in place (a local copy would live in registers)
         p->bc0 = bc0;
         int off = 0, wb = 0;
         for (int c = 0; c < NC; ++c) {
-            p->n_class[c] = L.cnt[c];
+            const int nc = L.cnt3[b3][c];
+            L.cnt[c] = nc;
+            p->n_class[c] = nc;
             p->off_class[c] = off;
             L.fill[c] = off;
-            off += L.cnt[c];
+            off += nc;
             p->wave_base[c] = wb;
             L.wbase[c] = wb;
             if (c < NC - 1) {
                 const int per = 64 >> (6 - c / kSeg64Widths);
-                wb += (L.cnt[c] + per - 1) / per;
+                wb += (nc + per - 1) / per;
             }
         }
         p->dynamic = a.wave_order != nullptr && wb > 2 * a.n_simd;
         *a.big_count = L.cnt[NC - 1];
     }
     __syncthreads();
-    plan_walk(a, n, [&](int pid, int H) {
+    plan_stamp(a, L, 1);
+    plan_walk(a, n, [&](int pid, int R, int H) {
         const int c = rescue_class(H, bc0);
         const int pos = atomicAdd(&L.fill[c], 1);
-        if (c < NC - 1)
+        if (c < NC - 1) {
             a.sorted[pos] = pid;
-        else
+            a.sorted_r[pos] = R;
+        } else {
             a.big[pos - (n - L.cnt[NC - 1])] = pid;
+        }
     });
     __syncthreads();
+    plan_stamp(a, L, 2);
     const int W = L.wbase[NC - 1];   // segmented waves
     if (W <= 1 || !a.wave_order) return;
     if (W > kMaxSortWaves) {   // classes longest first, fetched in that order
@@ -374,33 +409,33 @@ __device__ void plan_rescue(const Seg64Args& a, int n, PlanLds& L)
     wave_costs(a, L, W);
     L.hist[t] = 0;
     __syncthreads();
+    plan_stamp(a, L, 3);
     const unsigned cmax = L.cmax;
     auto bucket = [&](unsigned c) { return 255 - int((unsigned long long)c * 255 / cmax); };   // 0: costliest
     for (int w = t; w < W; w += kPlanThreads) atomicAdd(&L.hist[bucket(L.cost[w])], 1);
     __syncthreads();
-    if (t == 0) {   // exclusive prefix over the buckets
-        int acc = 0;
-        for (int b = 0; b < 256; ++b) {
-            const int v = L.hist[b];
-            L.hist[b] = acc;
-            acc += v;
+    if (t < 64) {   // exclusive prefix over the buckets: one wave, 4 buckets a lane
+        const int4 h = reinterpret_cast<const int4*>(L.hist)[t];
+        const int s4 = h.x + h.y + h.z + h.w;
+        int inc = s4;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int v = __shfl_up(inc, d, 64);
+            if (t >= d) inc += v;
         }
+        const int ex = inc - s4;
+        reinterpret_cast<int4*>(L.hist)[t] = make_int4(ex, ex + h.x, ex + h.x + h.y, ex + h.x + h.y + h.z);
     }
     __syncthreads();
+    plan_stamp(a, L, 4);
     const int S = a.n_simd;
     for (int w = t; w < W; w += kPlanThreads) {
         const int r = atomicAdd(&L.hist[bucket(L.cost[w])], 1);   // rank in descending cost
         // At most two waves per SIMD (positions p and p + S share one): the
-        // 2S - W heaviest waves alone on a SIMD (positions W - S .. S - 1),
-        // then the rest paired heaviest with lightest.
-        int pos = r;
-        if (W > S && W <= 2 * S) {
-            const int solo = 2 * S - W;
-            if (a.order_mode == 2)
-                pos = r < solo ? (W - S) + r : (r < S ? r - solo : S + (W - 1 - r));
-            else if (r >= S)
-                pos = S + (W - 1 - r);
-        }
+        // heaviest S waves first, then the rest paired heaviest with lightest.
+        // (The 2S - W heaviest alone on a SIMD first measured slower: S4's fp64
+        // pass 0.490 vs 0.441 ms; class order without the sort 0.488.)
+        const int pos = (W > S && W <= 2 * S && r >= S) ? S + (W - 1 - r) : r;
         a.wave_order[pos] = w;
     }
 }
@@ -530,6 +565,17 @@ __device__ __forceinline__ int wave_min(int v)
     return __builtin_amdgcn_readfirstlane(v);
 }
 
+// Diagnostics (Seg64Args::timeline): wave w's record.
+__device__ __forceinline__ void wave_record(const Seg64Args& a, int w, unsigned long long t_start, int pid)
+{
+    a.timeline[3 * size_t(w)] = t_start;
+    a.timeline[3 * size_t(w) + 1] = __builtin_amdgcn_s_memrealtime();
+    a.timeline[3 * size_t(w) + 2] =
+        (unsigned long long)unsigned(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))) |
+        ((unsigned long long)unsigned(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11))) << 32) |
+        ((unsigned long long)unsigned(pid) << 40);
+}
+
 template <int OCC>
 __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
 {
@@ -557,6 +603,8 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
     if (planner) {
         const unsigned long long t_plan0 = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
         plan_rescue(a, n, plan_lds);
+        __syncthreads();
+        plan_stamp(a, plan_lds, 5);
         // Publish (MI355X_MICROARCH.md, inter-workgroup visibility): every
         // storing wave drains its stores, then one lane releases and flags.
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -569,6 +617,7 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
                 a.timeline[3 * size_t(a.n_pairs)] = t_plan0;
                 a.timeline[3 * size_t(a.n_pairs) + 1] = __builtin_amdgcn_s_memrealtime();
                 a.timeline[3 * size_t(a.n_pairs) + 2] = (unsigned long long)n;
+                for (int i = 0; i < kPlanPhases; ++i) a.timeline[3 * size_t(a.n_pairs + 1) + i] = plan_lds.phase[i];
             }
         }
     }
@@ -617,6 +666,7 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
     const int lane = threadIdx.x & 63;
     // Lane l holds the first wave of class l + 1: a wave's class is the number
     // of class starts at or below it (wave_base is non-decreasing).
+    static_assert(kSeg64Classes <= 65, "one ballot covers the classes");
     const int next_base = lane < kSeg64Classes - 1 ? p->wave_base[lane + 1] : INT32_MAX;
     const bool dyn = __builtin_amdgcn_readfirstlane(p->dynamic) != 0;
     for (int pos = blockIdx.x * 4 + (threadIdx.x >> 6);;) {
@@ -657,14 +707,7 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
         default: break;
         }
         if (owner) a.raw_out[pid] = sumM + sumX;
-        if (a.timeline && lane == 0) {   // (diagnostics) start, end, HW_ID | XCC_ID << 32 | first pair << 40
-            a.timeline[3 * size_t(w)] = t_start;
-            a.timeline[3 * size_t(w) + 1] = __builtin_amdgcn_s_memrealtime();
-            a.timeline[3 * size_t(w) + 2] =
-                (unsigned long long)unsigned(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))) |
-                ((unsigned long long)unsigned(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11))) << 32) |
-                ((unsigned long long)unsigned(pid) << 40);
-        }
+        if (a.timeline && lane == 0) wave_record(a, w, t_start, pid);   // (diagnostics)
         __builtin_amdgcn_wave_barrier();   // the next wave's match table reuses mt
         if (!dyn) pos += gridDim.x * 4;
     }

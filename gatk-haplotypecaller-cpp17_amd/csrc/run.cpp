@@ -46,13 +46,13 @@ int run_part(Part* b, hipStream_t s)
     r.ready = b->d_count + kPlanReady + par;
     r.ready_reset = b->d_count + kPlanReady + (par ^ 1);
     r.sorted = b->d_sorted;
+    r.sorted_r = b->d_sorted + b->n;
     r.big = b->d_big;
     r.big_count = b->d_big_count;
     r.plan = b->d_plan;
     r.raw_out = b->d_raw64;
     r.min_lanes = int64_t(2) * 4 * dv.n_cu * 64;
-    r.order_mode = int(env_i64("HC_PHMM_RESCUE_ORDER", 1));   // 0: class order (A/B); 2: heaviest alone first
-    r.wave_order = r.order_mode != 0 ? b->d_worder : nullptr;
+    r.wave_order = env_i64("HC_PHMM_RESCUE_ORDER", 1) != 0 ? b->d_worder : nullptr;   // 0: class order (A/B)
     r.next_wave = b->d_count + kNextWave;
     r.n_simd = 4 * dv.n_cu;
     r.n_pairs = int(b->n);
@@ -109,7 +109,7 @@ int run_part(Part* b, hipStream_t s)
             // Diagnostics: this part's own record buffer (parts run concurrently
             // on slot streams); hcx_timeline reads the last traced part's fp32
             // seg waves, hcx_timeline64 its fp64 waves (records after them).
-            const int need = b->n_seg_waves + int(b->n) + 1;   // + the fp64 plan's record
+            const int need = b->n_seg_waves + int(b->n) + 3;   // + the fp64 plan's records
             if (b->timeline_n < need) {
                 if (b->timeline) {
                     HIP_TRY(hipStreamSynchronize(s));
@@ -121,7 +121,7 @@ int run_part(Part* b, hipStream_t s)
             }
             b->timeline_n32 = b->n_seg_waves;
             HIP_TRY(hipMemsetAsync(b->timeline + 3 * size_t(b->n_seg_waves), 0,
-                                   size_t(b->n + 1) * 3 * sizeof(unsigned long long), s));
+                                   size_t(b->n + 3) * 3 * sizeof(unsigned long long), s));
             std::lock_guard<std::mutex> lk(g_tl.mu);
             g_tl.part = b;
             a.timeline = b->timeline;

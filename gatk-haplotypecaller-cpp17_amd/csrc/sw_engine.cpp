@@ -118,8 +118,6 @@ struct hc_sw_batch {
     hc_sw_params params{};
     int overhang = 9, shortcut = 1;
     int fast = 0;
-    int profile = 0;
-    int spiral = 0;
     char* dev = nullptr;
     SwPair* pairs = nullptr;
     int32_t* order = nullptr;
@@ -240,25 +238,11 @@ int create(int64_t n, const int64_t* ref_off, const int32_t* ref_len, const uint
     b->fast = fast_ok(params, overhang, b->n1max, b->n2max) ? 1 : 0;
     if (const char* e = std::getenv("HC_SW_GENERIC"))   // parity tests of the generic variant
         if (e[0] == '1') b->fast = 0;
-    // The fast path's optional substitution profile (HC_SW_PROFILE=1) holds
-    // score - open as int16. It saves the compare + select of every cell but
-    // its LDS rows halve the waves per CU; on W2/W3 the compare form is faster
-    // (8.7 vs 10.8 ms, 3.6 vs 3.9 ms on MI355X), so it is off by default.
-    const int64_t pm = int64_t(params.match) - params.open, pmm = int64_t(params.mismatch) - params.open;
-    b->profile = 0;
-    if (const char* e = std::getenv("HC_SW_PROFILE"))
-        if (e[0] == '1')
-            b->profile = b->fast && pm >= INT16_MIN && pm <= INT16_MAX && pmm >= INT16_MIN && pmm <= INT16_MAX;
-    // The fast compare path in the spiral layout on request (HC_SW_SPIRAL=1):
-    // it removes the per-stripe skew (W2: 12 % fewer steps) but its stripe
-    // changes make 16 % of the groups run a heavier step, and it measured
-    // slower on MI355X (W2 DP 9.33 vs 8.72 ms, W3 3.66 vs 3.45 ms).
-    b->spiral = 0;
-    if (const char* e = std::getenv("HC_SW_SPIRAL"))
-        if (e[0] == '1') b->spiral = b->fast && !b->profile;
+    // (An LDS substitution profile and a spiral layout of the fast path were
+    // measured slower — W2 DP 10.8 / 9.33 vs 8.72 ms — and removed, round 6.)
     for (auto& P : pairs) {
         P.bt_off = bt_total;
-        bt_total += b->spiral ? spiral_bt_words(P.n1, P.n2) : bt_words(P.n1, P.n2);
+        bt_total += bt_words(P.n1, P.n2);
     }
 
     // One device allocation: descriptors, inputs, outputs, scratch.
@@ -357,8 +341,6 @@ int run(hc_sw_batch* b, hipStream_t s)
     d.n1max = b->n1max;
     d.n2max = b->n2max;
     d.fast = b->fast;
-    d.profile = b->profile;
-    d.spiral = b->spiral;
     // Pairs per workgroup: one for region-sized windows (W2, n2 <= ~650: 8.62 /
     // 9.09 / 9.20 ms at 1 / 2 / 4), four for long ones (W3, n2 ~ 1000: 3.54 /
     // 3.25 / 2.90 ms); HC_SW_WPG overrides.
@@ -375,7 +357,6 @@ int run(hc_sw_batch* b, hipStream_t s)
     t.slots = b->slots;
     t.n_elems = b->n_elems;
     t.offsets = b->offsets;
-    t.spiral = b->spiral;
     HIP_TRY(hipEventRecord(b->ev[0], s));
     HIP_TRY(launch_dp(d, b->n1max, s));
     HIP_TRY(hipEventRecord(b->ev[1], s));

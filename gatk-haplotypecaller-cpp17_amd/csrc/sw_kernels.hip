@@ -26,10 +26,11 @@
 // score arrives ready by DPP, the diagonal needs no add of its own), and keeps
 // the gap scores in VGPRs: 9 full-rate + 11 half-rate instructions per cell
 // (the first form: 11 + 11 plus 5 SGPR-operand adds). The match/mismatch
-// choice is a compare of the haplotype byte with the lane's seq1 byte, or, on
-// request (HC_SW_PROFILE=1), an int16 load from an LDS profile of
-// (score - open) per distinct seq1 byte and column; the profile's LDS halves
-// the waves per CU and loses on W2/W3.
+// choice is a compare of the haplotype byte with the lane's seq1 byte. (An
+// int16 LDS substitution profile per distinct seq1 byte and a spiral layout
+// running lanes on into the next stripe were measured slower on W2 / W3 —
+// DESIGN.md §8.2 — and removed in round 6: their code paths held the kernel's
+// registers at 90 VGPRs, 79 without.)
 //
 // sw_trace_kernel: one wave per pair walks the backtrack from the end point
 // (getCIGAR's state machine), 64 cells per step along the current direction,
@@ -187,7 +188,7 @@ __device__ __forceinline__ void stripe(Lane& L, int lane, int n2, int rb, bool r
     }
 }
 
-// ---- profile path ------------------------------------------------------
+// ---- fast compare path --------------------------------------------------
 struct PLane {
     int h;    // H(i, j-1): this lane's last cell
     int ex;   // E(i, j-1) + extend
@@ -246,36 +247,27 @@ struct PGroupIn {
     int sc[kGroup];    // score(j) - open for this lane's row
 };
 
-// Where a lane's score(j) - open comes from: the LDS profile row of its seq1
-// byte (PROF), or a compare of the haplotype byte with its seq1 byte.
+// A lane's score(j) - open: a compare of the haplotype byte with its seq1 byte.
 struct Scorer {
-    const int16_t* prow;   // PROF: prow[t] = score of the column computed at step t
-    const uint8_t* arow;   // compare: arow[t] = haplotype byte of that column
-    int rb;                // compare: this lane's seq1 byte (-1: no row)
-    int mp, mmp;           // compare: match - open, mismatch - open (VGPRs)
+    const uint8_t* arow;   // arow[t] = haplotype byte of the column computed at step t
+    int rb;                // this lane's seq1 byte (-1: no row)
+    int mp, mmp;           // match - open, mismatch - open (VGPRs)
 };
 
 typedef const volatile __attribute__((address_space(3))) int LdsInt;
-typedef const volatile __attribute__((address_space(3))) int16_t LdsI16;
 typedef const volatile __attribute__((address_space(3))) uint8_t LdsU8;
 
 // Separate 32-bit loads (volatile: not merged into 64/128-bit tuples, whose
 // elements the register allocator will not reuse as the DPP destinations) and
-// one ds_read_i16 / ds_read_u8 per score (no SDWA extract, which issues at
-// half rate).
-template <bool PROF>
+// one ds_read_u8 per score (no SDWA extract, which issues at half rate).
 __device__ __forceinline__ void pload(PGroupIn& g, int t0, LdsInt* rowHo, LdsInt* rowF, const Scorer& sr)
 {
 #pragma unroll
     for (int k = 0; k < kGroup; ++k) {
         g.ho[k] = rowHo[64 + t0 + k];
         g.fxo[k] = rowF[64 + t0 + k];
-        if (PROF) {
-            g.sc[k] = ((LdsI16*)sr.prow)[t0 + k];
-        } else {
-            const int ab = ((LdsU8*)sr.arow)[t0 + k];
-            g.sc[k] = ab == sr.rb ? sr.mp : sr.mmp;
-        }
+        const int ab = ((LdsU8*)sr.arow)[t0 + k];
+        g.sc[k] = ab == sr.rb ? sr.mp : sr.mmp;
     }
 }
 
@@ -288,207 +280,33 @@ __device__ __forceinline__ int in_vgpr(int x)
     return v;
 }
 
-template <int MODE, bool LASTW, bool PROF>
+template <int MODE, bool LASTW>
 __device__ __forceinline__ void pgroup(PLane& L, int t0, int lane, int n2, bool row_ok, int open, int extend,
                                        int* rowHo, int* rowF, const Scorer& sr)
 {
     PGroupIn g;
-    pload<PROF>(g, t0, (LdsInt*)rowHo, (LdsInt*)rowF, sr);
+    pload(g, t0, (LdsInt*)rowHo, (LdsInt*)rowF, sr);
 #pragma unroll
     for (int k = 0; k < kGroup; ++k)
         pstep<MODE, LASTW>(L, t0 + k, lane, n2, row_ok, g.ho[k], g.fxo[k], g.sc[k], open, extend, rowHo, rowF);
 }
 
-template <bool LASTW, bool PROF>
+template <bool LASTW>
 __device__ __forceinline__ void pstripe(PLane& L, int lane, int n2, bool row_ok, int T, uint32_t* btw, int open,
                                         int extend, int* rowHo, int* rowF, const Scorer& sr)
 {
     for (int t0 = 0; t0 < T; t0 += kGroup) {
         const bool fill = t0 < kStripe, drain = t0 + kGroup > n2;
         if (!fill && !drain)
-            pgroup<kBulk, LASTW, PROF>(L, t0, lane, n2, row_ok, open, extend, rowHo, rowF, sr);
+            pgroup<kBulk, LASTW>(L, t0, lane, n2, row_ok, open, extend, rowHo, rowF, sr);
         else if (fill && drain)
-            pgroup<kBoth, LASTW, PROF>(L, t0, lane, n2, row_ok, open, extend, rowHo, rowF, sr);
+            pgroup<kBoth, LASTW>(L, t0, lane, n2, row_ok, open, extend, rowHo, rowF, sr);
         else if (fill)
-            pgroup<kFill, LASTW, PROF>(L, t0, lane, n2, row_ok, open, extend, rowHo, rowF, sr);
+            pgroup<kFill, LASTW>(L, t0, lane, n2, row_ok, open, extend, rowHo, rowF, sr);
         else
-            pgroup<kDrain, LASTW, PROF>(L, t0, lane, n2, row_ok, open, extend, rowHo, rowF, sr);
+            pgroup<kDrain, LASTW>(L, t0, lane, n2, row_ok, open, extend, rowHo, rowF, sr);
         btw[(t0 / kGroup) * kStripe + lane] = L.acc;
     }
-}
-
-// ---- spiral path (HC_SW_SPIRAL=1) -----------------------------------------
-// Lanes run on into the next stripe (sw_kernels.hpp spiral_period): one skew
-// per pair instead of one per stripe (W2: 12 % fewer steps). Bit-exact, but
-// the groups around each stripe change (16 % on W2) run a step with the
-// change's bookkeeping, and on MI355X it measured slower than the striped
-// sweep (W2 DP 9.33 vs 8.72 ms), so it is not the default.
-// Per lane: vm = v mod P of the current step (negative before the lane's
-// first step, kSpDone after its last stripe), the current row irow and the
-// LDS/alt base (slot of the current step's column = base + t). hd is the last
-// computed H before a stripe change resets h: the lane below still needs it
-// (H(i, n2) + open) on the step after.
-constexpr int kSpDone = INT_MIN / 2;
-
-struct SpLane {
-    int h, hd, ex, fx, dg;
-    uint32_t acc;
-    int rb;     // this row's seq1 byte (-1: no row)
-    int base;   // 63 - lane - stripe * P
-    int vm;
-    int irow;   // 1-based row of the current stripe
-    int okc;    // row buffer writes on (valid row, not done)
-    // next stripe's values, ready before the lane's stripe change
-    int rbn, okn, hbn, dgn;
-};
-
-struct SpConst {
-    int open, extend, mp, mmp, lowx;   // VGPR copies
-    int n1, n2, P, S;
-    int ovh, open_s, extend_s;         // scalar copies for the boundaries
-};
-
-__device__ __forceinline__ void sp_next(SpLane& L, const SpConst& c, const uint8_t* s1)
-{
-    const int in = L.irow + kStripe;   // the next stripe's row
-    L.okn = in <= c.n1;
-    L.rbn = L.okn ? int(s1[in - 1]) : -1;
-    L.hbn = boundary(c.ovh, c.open_s, c.extend_s, in);                // H(in, 0)
-    L.dgn = boundary(c.ovh, c.open_s, c.extend_s, in - 1) + c.open;   // H(in - 1, 0) + open
-}
-
-// One step. SLOW: stripe changes, idle lanes (before the first step, pads,
-// done), writes only from valid rows. Bulk: every lane computing a cell of
-// its stripe, no stripe change within this step or the one before.
-template <bool SLOW, bool GUARD>
-__device__ __forceinline__ void sp_step(SpLane& L, const SpConst& c, int t, int ho, int fxo, int ab, int* rowHo,
-                                        int* rowF, int* colG)
-{
-    const int eo = L.h + c.open;
-    const int eod = SLOW ? L.hd + c.open : eo;
-    const int fo = shr1(ho, eod);
-    const int fe = shr1(fxo, L.fx);
-    const int sc = ab == L.rb ? c.mp : c.mmp;
-    const int fn = max(fe, fo);
-    const int en = max(eo, L.ex);
-    const int hn0 = L.dg + sc;
-    const int hn1 = max(hn0, en);
-    const int hn = max(hn1, fn);
-    L.acc = __builtin_amdgcn_alignbit(L.acc, uint32_t(L.ex - eo), 31);
-    L.acc = __builtin_amdgcn_alignbit(L.acc, uint32_t(fe - fo), 31);
-    L.acc = __builtin_amdgcn_alignbit(L.acc, uint32_t(hn0 - en), 31);
-    L.acc = __builtin_amdgcn_alignbit(L.acc, uint32_t(hn1 - fn), 31);
-    L.fx = fn + c.extend;
-    L.dg = fo;
-    if (!SLOW) {
-        L.h = hn;
-        L.ex = en + c.extend;
-        if (!GUARD || L.okc) {
-            rowHo[L.base + t] = eo;
-            rowF[L.base + 1 + t] = L.fx;
-        }
-        return;
-    }
-    const bool act = unsigned(L.vm) < unsigned(c.n2);
-    const int hu = act ? hn : L.h;
-    const int exu = act ? en + c.extend : L.ex;
-    if (L.okc) {
-        rowHo[L.base + t] = eo;
-        rowF[L.base + 1 + t] = L.fx;
-    }
-    L.hd = hu;
-    L.h = hu;
-    L.ex = exu;
-    if (L.vm == c.P - 1) {   // the lane leaves column P of its stripe
-        if (L.irow <= c.n1) colG[L.irow] = hu;   // H(i, n2): frozen since column n2
-        if (L.okc) rowHo[L.base + t + 1] = hu + c.open;   // column n2's H + open for the next stripe's lane 0
-        if (L.irow + kStripe <= c.S * kStripe) {   // not the last stripe: start the next one
-            L.h = L.hbn;
-            L.ex = c.lowx;
-            L.dg = L.dgn;
-            L.rb = L.rbn;
-            L.okc = L.okn;
-            L.base -= c.P;
-            L.irow += kStripe;
-            L.vm = -1;
-        } else {
-            L.okc = 0;
-            L.base -= c.P;   // its haplotype reads stay inside the buffer
-            L.vm = kSpDone;
-        }
-    }
-    ++L.vm;
-}
-
-template <bool SLOW, bool GUARD>
-__device__ __forceinline__ void sp_group(SpLane& L, const SpConst& c, int t0, int q0, const int* rowHo_c,
-                                         const int* rowF_c, const uint8_t* altB, int* rowHo, int* rowF, int* colG)
-{
-    // lane 0's row-buffer inputs: column (t mod P) + 1 of the previous stripe's
-    // last row, slot 64 + (t mod P) (uniform); every lane's haplotype bytes at
-    // its base (the 8-byte cyclic pad behind column P serves a lane whose
-    // stripe changes inside the group).
-    int ho[kGroup], fxo[kGroup], ab[kGroup];
-    if (!SLOW) {
-        // no stripe change for any lane (lane 0 included): contiguous slots,
-        // one address for the group
-        LdsInt* h = (LdsInt*)rowHo_c + 64 + q0;
-        LdsInt* f = (LdsInt*)rowF_c + 64 + q0;
-#pragma unroll
-        for (int j = 0; j < kGroup; ++j) {
-            ho[j] = h[j];
-            fxo[j] = f[j];
-            ab[j] = ((LdsU8*)altB)[L.base + 1 + t0 + j];
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < kGroup; ++j) {
-            const int q = q0 + j < c.P ? q0 + j : q0 + j - c.P;
-            ho[j] = ((LdsInt*)rowHo_c)[64 + q];
-            fxo[j] = ((LdsInt*)rowF_c)[64 + q];
-            ab[j] = ((LdsU8*)altB)[L.base + 1 + t0 + j];
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < kGroup; ++j) sp_step<SLOW, GUARD>(L, c, t0 + j, ho[j], fxo[j], ab[j], rowHo, rowF, colG);
-    if (!SLOW) {   // bulk steps leave the stripe bookkeeping alone
-        L.vm += kGroup;
-        L.hd = L.h;
-    }
-}
-
-// Rank the distinct bytes of seq1 (the row bases): codeOf[b] = rank, alpha[rank]
-// = b. Returns the number of distinct bytes (wave-uniform).
-__device__ int build_alphabet(const uint8_t* s1, int n1, int lane, uint8_t* codeOf, uint8_t* alpha)
-{
-    reinterpret_cast<int*>(codeOf)[lane] = 0;
-    wave_sync();
-    for (int x = lane; x < n1; x += 64) codeOf[s1[x]] = 1;
-    wave_sync();
-    const uint32_t w = reinterpret_cast<const uint32_t*>(codeOf)[lane];
-    const int c0 = (w & 0xff) != 0, c1 = (w & 0xff00) != 0, c2 = (w & 0xff0000) != 0, c3 = (w >> 24) != 0;
-    const int cnt = c0 + c1 + c2 + c3;
-    int incl = cnt;   // inclusive prefix over lanes
-    for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(incl, o);
-        if (lane >= o) incl += v;
-    }
-    const int K = __shfl(incl, 63);
-    int r = incl - cnt;
-    wave_sync();
-    uint32_t out = 0;
-    const int cs[4] = {c0, c1, c2, c3};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        if (cs[q]) {
-            if (r < kProfCodes) alpha[r] = uint8_t(4 * lane + q);
-            out |= uint32_t(r & 0xff) << (8 * q);
-            ++r;
-        }
-    }
-    reinterpret_cast<uint32_t*>(codeOf)[lane] = out;
-    wave_sync();
-    return K;
 }
 
 template <bool FAST, int WPG>
@@ -520,12 +338,7 @@ __global__ __launch_bounds__(64 * WPG) void sw_dp_kernel(SwDpArgs a)
     const int slots = row_slots(a.n2max);
     int* rowH = lds;
     int* rowF = rowH + slots;
-    uint8_t* tail = reinterpret_cast<uint8_t*>(rowF + fslots(a.n1max, a.n2max));
-    uint8_t* altB = tail;   // 64 pads, columns, pads (compare paths)
-    int16_t* prof = reinterpret_cast<int16_t*>(tail);   // profile path
-    const int PS = prof_slots(a.n2max);
-    uint8_t* codeOf = tail + dp_tail_bytes(a.n2max);
-    uint8_t* alpha = codeOf + 256;
+    uint8_t* altB = reinterpret_cast<uint8_t*>(rowF + fslots(a.n1max, a.n2max));   // 64 pads, columns, pads
     // H(i, n2) of every row goes to this pair's CIGAR-element scratch in HBM
     // (the trace kernel reuses it later); after the last stripe it is copied
     // into rowF, free by then, for the end-point scan.
@@ -538,109 +351,15 @@ __global__ __launch_bounds__(64 * WPG) void sw_dp_kernel(SwDpArgs a)
     const int nw = T / kGroup;
     int hofs = 0;   // the row buffer holds H + hofs
 
-    const int K = (FAST && a.profile) ? build_alphabet(s1, n1, lane, codeOf, alpha) : 0;
-    const bool use_prof = FAST && a.profile && K <= kProfCodes;
-    if (FAST && a.spiral) {
-        hofs = open;
-        const int Pp = spiral_period(n2);
-        const int Pmax = spiral_period(a.n2max);
-        const int Ts = spiral_steps(n1, n2);
-        // Row 0: H(0, j) + open, F(0, j) + extend; haplotype bytes at 64 + c with
-        // pads to P and an 8-byte cyclic copy of the first columns behind P.
-        for (int j = lane; j < Pmax + kStripe + 2 * kGroup; j += 64) {
-            rowH[j] = (j >= 64 ? boundary(ovh, open, extend, j - 63) : 0) + open;
-            rowF[j] = kLow + extend;
-        }
-        for (int x = lane; x < kStripe + Pp + 2 * kGroup; x += 64) {
-            const int cc = x - kStripe;
-            const int col = cc >= Pp ? cc - Pp : cc;
-            altB[x] = (cc >= 0 && col < n2) ? s2[col] : 0;
-        }
-        wave_sync();
-        SpConst c;
-        c.open = in_vgpr(open);
-        c.extend = in_vgpr(extend);
-        c.mp = in_vgpr(a.match - open);
-        c.mmp = in_vgpr(a.mismatch - open);
-        c.lowx = in_vgpr(kLow + extend);
-        c.n1 = n1;
-        c.n2 = n2;
-        c.P = Pp;
-        c.S = nstripes;
-        c.ovh = ovh;
-        c.open_s = open;
-        c.extend_s = extend;
-        SpLane L;
-        L.irow = lane + 1;
-        L.h = L.hd = boundary(ovh, open, extend, L.irow);   // H(i, 0)
-        L.ex = kLow + extend;                                // E(i, 0) + extend
-        L.fx = kLow + extend;
-        L.dg = boundary(ovh, open, extend, lane) + open;     // lane 0: H(0, 0) + open
-        L.acc = 0;
-        L.okc = L.irow <= n1;
-        L.rb = L.okc ? int(s1[L.irow - 1]) : -1;
-        L.base = 63 - lane;
-        L.vm = -lane;
-        sp_next(L, c, s1);
-        const int V = nstripes * Pp;
-        const bool partial = (n1 % kStripe) != 0;
-        int q0 = 0;   // t0 mod P
-        // Groups whose lanes' v over the group and the step before
-        // ([t0 - 64, t0 + 7]) include a stripe change, an idle lane or the
-        // pair's end run the slow step; the rest the bulk step, with guarded
-        // row-buffer writes once some lane may be on a missing row of a
-        // partial last stripe (a separate loop: the two bulk forms must not
-        // share hoisted loads, which costs a copy per DPP destination).
-        const int tg = partial ? std::min(Ts, std::max(0, ((nstripes - 1) * Pp - kGroup + 1 + kGroup - 1) & ~(kGroup - 1))) : Ts;
-        auto slow_at = [&](int t0) {
-            const int vlo = t0 - kStripe, vhi = t0 + kGroup - 1;
-            const int lo = vlo > 0 ? vlo : 0;
-            return vlo < 0 || vhi >= V || Pp > n2 || (vhi + 1) / Pp > lo / Pp;
-        };
-        int t0 = 0;
-        for (; t0 < tg; t0 += kGroup) {
-            const bool slow = slow_at(t0);
-            if (slow)
-                sp_group<true, true>(L, c, t0, q0, rowH, rowF, altB, rowH, rowF, colG);
-            else
-                sp_group<false, false>(L, c, t0, q0, rowH, rowF, altB, rowH, rowF, colG);
-            bt[int64_t(t0 / kGroup) * kStripe + lane] = L.acc;
-            if (slow) sp_next(L, c, s1);
-            q0 += kGroup;
-            if (q0 >= Pp) q0 -= Pp;
-        }
-        for (; t0 < Ts; t0 += kGroup) {
-            const bool slow = slow_at(t0);
-            if (slow)
-                sp_group<true, true>(L, c, t0, q0, rowH, rowF, altB, rowH, rowF, colG);
-            else
-                sp_group<false, true>(L, c, t0, q0, rowH, rowF, altB, rowH, rowF, colG);
-            bt[int64_t(t0 / kGroup) * kStripe + lane] = L.acc;
-            if (slow) sp_next(L, c, s1);
-            q0 += kGroup;
-            if (q0 >= Pp) q0 -= Pp;
-        }
-        wave_sync();
-    } else if (FAST) {
+    if (FAST) {
         hofs = open;
         // Row 0 in this path's form: H(0, j) + open, F(0, j) + extend.
         for (int j = lane; j < kStripe + T + 2 * kGroup; j += 64) {
             rowH[j] = (j >= 64 ? boundary(ovh, open, extend, j - 63) : 0) + open;
             rowF[j] = kLow + extend;
         }
-        if (use_prof) {
-            for (int c = 0; c < K; ++c) {
-                const int b = alpha[c];
-                for (int v = lane; v < PS; v += 64) {
-                    const int j = v - 63;
-                    const int x = (j >= 1 && j <= n2) ? ((s2[j - 1] == b ? a.match : a.mismatch) - open) : 0;
-                    prof[c * PS + v] = int16_t(x);
-                }
-            }
-        } else {
-            for (int c = lane; c < kStripe + T + kGroup; c += 64)
-                altB[c] = (c >= kStripe && c < kStripe + n2) ? s2[c - kStripe] : 0;
-        }
+        for (int c = lane; c < kStripe + T + kGroup; c += 64)
+            altB[c] = (c >= kStripe && c < kStripe + n2) ? s2[c - kStripe] : 0;
         wave_sync();
         const int open_v = in_vgpr(open), extend_v = in_vgpr(extend);
         Scorer sr;
@@ -661,21 +380,12 @@ __global__ __launch_bounds__(64 * WPG) void sw_dp_kernel(SwDpArgs a)
             // (lane r - 1 leaves column n2), not n2 + 63: its unwritten
             // backtrack words lie past every cell the trace reads.
             const int Ts = lastw ? std::min(T, (n2 + (n1 - s * kStripe) + kGroup - 1) & ~(kGroup - 1)) : T;
-            if (use_prof) {
-                const int code = row_ok ? int(codeOf[s1[i - 1]]) : 0;
-                sr.prow = prof + code * PS + 64 - lane;
-                if (lastw)
-                    pstripe<true, true>(L, lane, n2, row_ok, Ts, btw, open_v, extend_v, rowH, rowF, sr);
-                else
-                    pstripe<false, true>(L, lane, n2, row_ok, T, btw, open_v, extend_v, rowH, rowF, sr);
-            } else {
-                sr.rb = row_ok ? int(s1[i - 1]) : -1;   // never equals a byte
-                sr.arow = altB + 64 - lane;
-                if (lastw)
-                    pstripe<true, false>(L, lane, n2, row_ok, Ts, btw, open_v, extend_v, rowH, rowF, sr);
-                else
-                    pstripe<false, false>(L, lane, n2, row_ok, T, btw, open_v, extend_v, rowH, rowF, sr);
-            }
+            sr.rb = row_ok ? int(s1[i - 1]) : -1;   // never equals a byte
+            sr.arow = altB + 64 - lane;
+            if (lastw)
+                pstripe<true>(L, lane, n2, row_ok, Ts, btw, open_v, extend_v, rowH, rowF, sr);
+            else
+                pstripe<false>(L, lane, n2, row_ok, T, btw, open_v, extend_v, rowH, rowF, sr);
             if (row_ok) colG[i] = L.h;   // H(i, n2): frozen since the lane left column n2
             wave_sync();
         }
@@ -752,13 +462,13 @@ __global__ __launch_bounds__(64 * WPG) void sw_dp_kernel(SwDpArgs a)
     if (lane == 0) a.res[p] = SwResult{best, bi, bj, 0};
 }
 
-// 4-bit backtrack code of cell (i, j), 1-based (layout of sw_dp_kernel):
-// striped ([stripe][word][lane], P = 0) or spiral ([group][lane], period P).
-__device__ __forceinline__ int bt_nibble(const uint32_t* bt, int nw, int P, int i, int j)
+// 4-bit backtrack code of cell (i, j), 1-based (layout of sw_dp_kernel:
+// [stripe][word][lane]).
+__device__ __forceinline__ int bt_nibble(const uint32_t* bt, int nw, int i, int j)
 {
     const int k = (i - 1) & (kStripe - 1), s = (i - 1) / kStripe;
-    const int t = P ? s * P + j - 1 + k : j - 1 + k;
-    const uint32_t w = bt[(P ? int64_t(t >> 3) : int64_t(s) * nw + (t >> 3)) * kStripe + k];
+    const int t = j - 1 + k;
+    const uint32_t w = bt[(int64_t(s) * nw + (t >> 3)) * kStripe + k];
     return (w >> ((7 - (t & 7)) * 4)) & 15;
 }
 
@@ -789,7 +499,6 @@ __global__ __launch_bounds__(256) void sw_trace_kernel(SwTraceArgs a)
     }
     const uint32_t* bt = a.bt + P.bt_off;
     const int nw = stripe_steps(n2) / kGroup;
-    const int Psp = a.spiral ? spiral_period(n2) : 0;
     const int ovh = a.overhang;
     int i = __builtin_amdgcn_readfirstlane(r.max_i), j = __builtin_amdgcn_readfirstlane(r.max_j);
     if (ovh == 10) {
@@ -815,7 +524,7 @@ __global__ __launch_bounds__(256) void sw_trace_kernel(SwTraceArgs a)
         const int di = state == 4 ? 0 : lane, dj = state == 8 ? 0 : lane;
         const int ci = i - di, cj = j - dj;
         const bool valid = ci > 0 && cj > 0;
-        const int b = valid ? bt_nibble(bt, nw, Psp, ci, cj) : 0;
+        const int b = valid ? bt_nibble(bt, nw, ci, cj) : 0;
         // nibble [eo > ee][fo > fe][E wins][F wins] (see step): the reference's
         // code is op | INSERT_EXT(4) | DELETE_EXT(8), the EXT bits being "not open".
         const int op = (b & 1) ? kOpD : (b & 2) ? kOpI : kOpM;
@@ -878,19 +587,18 @@ __global__ __launch_bounds__(256) void sw_trace_kernel(SwTraceArgs a)
 
 }  // namespace
 
-size_t dp_lds_bytes(int n1max, int n2max, bool profile, bool spiral)
+size_t dp_lds_bytes(int n1max, int n2max)
 {
-    // [rowH | rowF | altB or the profile | codeOf 256 | alpha 8]
+    // [rowH | rowF | altB]
     const size_t rows = sizeof(int) * (size_t(row_slots(n2max)) + size_t(fslots(n1max, n2max)));
-    if (spiral) return rows + size_t(std::max(alt_slots(n2max), (kStripe + spiral_period(n2max) + 3 * kGroup + 3) & ~3));
-    return profile ? rows + size_t(dp_tail_bytes(n2max)) + 256 + 8 : rows + size_t(alt_slots(n2max));
+    return rows + size_t(alt_slots(n2max));
 }
 
 hipError_t launch_dp(const SwDpArgs& a, int n1max, hipStream_t s)
 {
     if (a.n <= 0) return hipSuccess;
     SwDpArgs b = a;
-    b.lds_wave_bytes = int((dp_lds_bytes(n1max, a.n2max, a.fast && a.profile, a.fast && a.spiral) + 15) & ~size_t(15));
+    b.lds_wave_bytes = int((dp_lds_bytes(n1max, a.n2max) + 15) & ~size_t(15));
     const int wpg = a.wpg == 4 ? 4 : a.wpg == 2 ? 2 : 1;
     const size_t lds = size_t(b.lds_wave_bytes) * wpg;
     const dim3 grid((a.n + wpg - 1) / wpg), block(64 * wpg);

@@ -37,41 +37,6 @@ __host__ __device__ inline int fslots(int n1max, int n2max)
 // columns, then pads up to the last step of a stripe.
 __host__ __device__ inline int alt_slots(int n2max) { return (kStripe + n2max + kStripe + 2 * kGroup + 3) & ~3; }
 
-// Substitution profile of the fast path: for each distinct seq1 byte c (up
-// to kProfCodes per pair) and column slot 63 + j, int16 score(seq2[j-1], c) -
-// open. A lane reads its row's profile along its columns (no compare per cell).
-constexpr int kProfCodes = 5;
-__host__ __device__ inline int prof_slots(int n2max) { return (n2max + 2 * kStripe + 4 * kGroup + 7) & ~7; }
-
-// Bytes after the row buffers: the compare paths' haplotype bytes or the
-// profile path's kProfCodes int16 rows.
-__host__ __device__ inline int dp_tail_bytes(int n2max)
-{
-    const int p = 2 * kProfCodes * prof_slots(n2max), b = alt_slots(n2max);
-    return ((p > b ? p : b) + 7) & ~7;
-}
-
-// Spiral layout of the fast compare path: lane k at global step t computes
-// virtual cell v = t - k of its row sweep — stripe v / P, column v % P + 1,
-// columns past n2 idle (P = spiral_period(n2) >= n2) — so a lane that leaves
-// the last column of stripe s starts stripe s + 1 on the next step and the
-// one-row skew is paid once per pair, not once per stripe. P >= 80 keeps lane
-// 0's reads of the row buffer (the previous stripe's last row, written P - 63
-// steps earlier) clear of a group's look-ahead.
-constexpr int kSpiralMinPeriod = 80;
-__host__ __device__ inline int spiral_period(int n2) { return n2 > kSpiralMinPeriod ? n2 : kSpiralMinPeriod; }
-// Global steps of one pair: S * P + 63 (skew) + 1 (the last column's hand-off),
-// rounded up to whole backtrack words.
-__host__ __device__ inline int spiral_steps(int n1, int n2)
-{
-    return (((n1 + kStripe - 1) / kStripe) * spiral_period(n2) + kStripe + kGroup - 1) & ~(kGroup - 1);
-}
-// Backtrack words: one per lane per 8 global steps, [group][lane].
-__host__ __device__ inline int64_t spiral_bt_words(int n1, int n2)
-{
-    return int64_t(spiral_steps(n1, n2) / kGroup) * kStripe;
-}
-
 struct SwPair {
     int64_t ref_off;   // seq1 bytes in refs[]
     int64_t alt_off;   // seq2 bytes in alts[]
@@ -101,8 +66,6 @@ struct SwDpArgs {
     int shortcut;
     int n1max, n2max;   // size the dynamic LDS
     int fast;    // host-proven: no cutoff, no int32 overflow (sw_engine.cpp fast_ok)
-    int profile;   // fast path with the LDS substitution profile (scores - open fit int16)
-    int spiral;    // fast compare path in the spiral layout (backtrack words [group][lane])
     int wpg;       // pairs (waves) per workgroup: 1, 2 or 4
     int lds_wave_bytes;   // set by launch_dp
 };
@@ -117,7 +80,6 @@ struct SwTraceArgs {
     uint16_t* slots;     // the first kSlotElems elements of pair p as uint16 at p * kSlotElems
     int32_t* n_elems;
     int32_t* offsets;
-    int spiral;   // backtrack in the spiral layout (SwDpArgs::spiral)
 };
 
 // Fixed per-pair result slots: CIGAR elements fit 16 bits (len <= n1 + n2 < 2^11,
@@ -127,7 +89,7 @@ constexpr int kSlotElems = 32;
 // CIGAR element op codes (smithwaterman_common.h:21-26).
 constexpr int kOpM = 0, kOpI = 1, kOpD = 2, kOpS = 9;
 
-size_t dp_lds_bytes(int n1max, int n2max, bool profile, bool spiral);
+size_t dp_lds_bytes(int n1max, int n2max);
 hipError_t launch_dp(const SwDpArgs& a, int n1max, hipStream_t s);
 hipError_t launch_trace(const SwTraceArgs& a, hipStream_t s);
 

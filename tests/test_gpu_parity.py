@@ -656,3 +656,32 @@ def test_rescue_shapes(engine, oracle_lib, shape):
     st = bt.stats()
     assert st.n_rescued == n_resc
     bt.close()
+
+
+@pytest.mark.parametrize("case", ["long-haps", "mixed-reads", "short-reads"])
+def test_fp64_long_haps_many_waves(engine, oracle_lib, case):
+    """An fp64 pass of many waves over long haps: 4 000 pairs of 1 025-2 048-
+    base haps, most rescued, so the plan sorts thousands of 64-lane waves and
+    dispatches them greedily from the wave counter (more than two waves per
+    SIMD) — against the oracle, flat and through a prepared batch run twice.
+    mixed-reads: some reads with an 'N' base, some with insertion != deletion
+    gap qualities and a hap with an 'N'; short-reads: R 40-639."""
+    r_range = (40, 639) if case == "short-reads" else (150, 250)
+    b = W.generate(4000, (1025, 2048), r_range, 0.08, seed=97)
+    if case == "mixed-reads":
+        rs, dels, hap = b["rs"].copy(), b["dels"].copy(), b["hap"].copy()
+        ro = b["read_off"]
+        for p in range(0, 4000, 37):
+            rs[ro[p] + 5] = ord("N")
+        for p in range(3, 4000, 53):
+            dels[ro[p]:ro[p] + b["R"][p]] = ord("J")   # constant gaps, insertion != deletion
+        hap[b["hap_off"][11] + 100] = ord("N")
+        b = dict(b, rs=rs, dels=dels, hap=hap)
+    ref = oracle_lib.pairs(b, nthreads=16)
+    assert ref["rescued"].sum() > 3000
+    assert_same(engine.pairs(b), ref, f"{case} flat")
+    bt = engine.Batch(b)
+    for k in range(2):
+        bt.run()
+        assert_same(bt.results(), ref, f"{case} run {k}")
+    bt.close()

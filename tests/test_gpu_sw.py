@@ -18,21 +18,14 @@ def sw():
     return hcsw
 
 
-@pytest.mark.parametrize("variant", ["auto", "spiral", "profile", "generic"])
+@pytest.mark.parametrize("variant", ["auto", "generic"])
 def test_sw_golden_every_case(sw, sw_golden, variant, monkeypatch):
     # auto: the fast DP variant wherever the host proves it exact (every
     # reference parameter set), the generic one for CUTOFF_PARAMS;
-    # spiral: the fast compare variant in the spiral layout (lanes run on
-    # into the next stripe: one skew per pair);
-    # profile: the fast variant with the LDS substitution profile when the
-    # pair's seq1 has at most 5 distinct bytes (the compare form otherwise);
-    # generic: the cutoff + compare variant forced everywhere.
+    # generic: the cutoff + compare variant forced everywhere. (The spiral and
+    # LDS-profile variants measured slower and were removed in round 6.)
     if variant == "generic":
         monkeypatch.setenv("HC_SW_GENERIC", "1")
-    if variant == "spiral":
-        monkeypatch.setenv("HC_SW_SPIRAL", "1")
-    if variant == "profile":
-        monkeypatch.setenv("HC_SW_PROFILE", "1")
     for c in sw_golden["cases"]:
         b = sw_golden["sets"][c["set"]]
         off, cig = sw.align_flat(b, c["params"], c["strategy"], True)

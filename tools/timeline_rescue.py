@@ -36,6 +36,8 @@ r32 = buf[:3 * n32].reshape(n32, 3).astype(np.int64).copy()
 n64 = L.hcx_timeline64(buf.ctypes.data, cap)
 r64 = buf[:3 * n64].reshape(n64, 3).astype(np.int64).copy()
 plan = r64[len(b["R"])] if n64 > len(b["R"]) else None   # {planner start, plan published, list length}
+# the planner's phase stamps: counted, table, scattered, costs, prefix, planned
+phases = r64[len(b["R"]) + 1:len(b["R"]) + 3].reshape(-1) if n64 >= len(b["R"]) + 3 else None
 r64 = r64[:len(b["R"])]
 r64 = r64[r64[:, 1] > 0]
 bt.close()
@@ -68,6 +70,16 @@ if len(r64):
         out["fp64_plan"] = dict(start_us=round((plan[0] - t0) / 100.0, 1), published_us=round((plan[1] - t0) / 100.0, 1),
                                 plan_us=round((plan[1] - plan[0]) / 100.0, 1), listed=int(plan[2]),
                                 launch_gap_us=round((plan[0] - t0) / 100.0 - e32.max(), 1))
+        if phases is not None:
+            names = ["count", "table", "scatter", "costs", "prefix", "order"]
+            prev = plan[0]
+            ph = {}
+            for nm, v in zip(names, phases):
+                if v > 0:
+                    ph[nm] = round((int(v) - int(prev)) / 100.0, 1)
+                    prev = v
+            ph["publish"] = round((int(plan[1]) - int(prev)) / 100.0, 1)
+            out["fp64_plan"]["phase_us"] = ph
     out["fp64"] = dict(first_start_us=round(s64.min(), 1), last_start_us=round(s64.max(), 1),
                        last_end_us=round(e64.max(), 1), gap_after_fp32_us=round(s64.min() - e32.max(), 1),
                        dur_p10_us=round(float(np.percentile(d64, 10)), 1),
