@@ -88,14 +88,21 @@ struct DiagArgs {
 // hap on those lanes, so the slot's lanes are all used: (k, width) is its
 // class. Classes are numbered widest slot and block first (the longest waves
 // are dispatched first); the last class holds haps wider than 64 blocks of 32
-// (anti-diagonal kernel, through `big`).
+// (anti-diagonal kernel, through `big`). In passes of many waves the 64-lane
+// pairs (haps over 1 024 columns) are mostly chained: a chain class per width,
+// numbered before the others, whose waves stream up to `chain` pairs through
+// the same 64 lanes one after the other (lane_kernel.hip chain_run: the 63-step
+// skew of a 64-lane pair paid once per chain instead of once per pair).
 constexpr int kSeg64Widths = 7;   // fp64 block widths 8, 12, ..., 32
-constexpr int kSeg64Classes = 7 * kSeg64Widths + 1;
+constexpr int kChainClasses = kSeg64Widths;
+constexpr int kMaxChain = 4;
+constexpr int kSeg64Classes = kChainClasses + 7 * kSeg64Widths + 1;
 constexpr int kSeg64MaxH = 64 * 32;   // longer haps: anti-diagonal fp64 kernel (host n_wide)
 __host__ __device__ constexpr int seg64_width(int wi) { return 8 + 4 * wi; }
 struct Seg64Plan {
     int bc0;                        // block width bound of the pass (32, or 16 / 8 for short lists)
     int dynamic;                    // waves fetched from a counter (more than two per SIMD)
+    int chain;                      // pairs per wave of the chain classes (1: none chained)
     int n_class[kSeg64Classes];
     int off_class[kSeg64Classes];   // class c's entries in `sorted` start here
     int wave_base[kSeg64Classes];   // first wave of class c; [last] = total waves
@@ -122,6 +129,8 @@ struct Seg64Args {
     long long min_lanes;      // narrower blocks below this many lanes at bc = 32
     int* wave_order;          // dispatch position -> wave (n entries), see rescue_plan_kernel
     int* next_wave;           // dynamic wave counter (zeroed by the plan)
+    int chain;                // longest chain of 64-lane pairs in one wave (1: no chains)
+    int chain_tail;           // rounds of single 64-lane waves (two per SIMD) kept unchained at the end
     int n_simd;               // SIMDs of the device (4 per CU)
     // Gather of the seg slots' result records (LaneArgs::rec) into the
     // per-pair outputs, done by this launch before its rescue work: pair p's

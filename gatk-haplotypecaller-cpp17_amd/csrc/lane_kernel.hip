@@ -214,7 +214,17 @@ __device__ __forceinline__ int rescue_class(int H, int bc0)
     const int need = (H + (1 << k) - 1) >> k;   // columns per lane on 2^k lanes (<= bc0 when nb0 <= 64)
     if (need > seg64_width(kSeg64Widths - 1)) return kSeg64Classes - 1;
     const int wi = need <= 8 ? 0 : (need - 8 + 3) / 4;
-    return (6 - k) * kSeg64Widths + (kSeg64Widths - 1 - wi);
+    return kChainClasses + (6 - k) * kSeg64Widths + (kSeg64Widths - 1 - wi);
+}
+// Class c's lanes per pair (log2) and block width; the chain classes are
+// 64-lane classes (their pairs one after the other, not side by side).
+__device__ __forceinline__ int class_k(int c)
+{
+    return c < kChainClasses ? 6 : 6 - (c - kChainClasses) / kSeg64Widths;
+}
+__device__ __forceinline__ int class_bc(int c)
+{
+    return seg64_width(kSeg64Widths - 1 - (c < kChainClasses ? c : c - kChainClasses) % kSeg64Widths);
 }
 
 // Wave order of the pass. With at most two waves per SIMD (fp64 occupancy)
@@ -231,8 +241,9 @@ constexpr int kPlanThreads = 256;   // the planning workgroup (a phmm_seg64_kern
 constexpr int kPlanPhases = 6;      // (diagnostics) the planner's phase stamps
 
 struct PlanLds {
-    int cnt[kSeg64Classes], fill[kSeg64Classes], wbase[kSeg64Classes];
+    int cnt[kSeg64Classes], fill[kSeg64Classes], wbase[kSeg64Classes], off[kSeg64Classes];
     int cnt3[3][kSeg64Classes];   // class counts at bc0 = 32, 16, 8 (one walk counts all three)
+    int chain;
     alignas(16) int hist[256];
     unsigned long long lanes;
     unsigned cmax;
@@ -240,10 +251,10 @@ struct PlanLds {
     unsigned cost[kMaxSortWaves];
 };
 
-// Entries [e0, e1) of `sorted` and the class shape of wave w (class order)
-// of the plan in L.
+// Entries [e0, e1) of `sorted` and the class of wave w (class order) of the
+// plan in L.
 struct WaveSpan {
-    int e0, e1, kk, bc;
+    int e0, e1, c;
 };
 __device__ __forceinline__ WaveSpan wave_span(const PlanLds& L, int w)
 {
@@ -255,10 +266,9 @@ __device__ __forceinline__ WaveSpan wave_span(const PlanLds& L, int w)
         else hi = mid;
     }
     const int c = lo;
-    const int kk = 6 - c / kSeg64Widths, per = 64 >> kk;
-    const int off = L.fill[c] - L.cnt[c];   // the class's first entry (fill ran past it)
-    const int e0 = off + (w - L.wbase[c]) * per;
-    return WaveSpan{e0, min(off + L.cnt[c], e0 + per), kk, seg64_width(kSeg64Widths - 1 - c % kSeg64Widths)};
+    const int per = c < kChainClasses ? L.chain : 64 >> class_k(c);
+    const int e0 = L.off[c] + (w - L.wbase[c]) * per;
+    return WaveSpan{e0, min(L.off[c] + L.cnt[c], e0 + per), c};
 }
 
 // The planner is one workgroup walking the list, so its time is load
@@ -290,30 +300,37 @@ __device__ __forceinline__ void plan_walk(const Seg64Args& a, int n, F&& f)
 }
 
 // Modelled costs of waves [0, W) into L.cost (and their maximum into L.cmax):
-// (rows + skew) steps x (14 ops per column + ~40 per step), the rows from
-// sorted_r (written by the scatter: no dependent load of the descriptors).
+// steps x (14 ops per column + ~40 per step), steps = max R + skew (pairs side
+// by side) or sum of R + skew (a chain); the rows from sorted_r (written by
+// the scatter: no dependent load of the descriptors).
 __device__ __forceinline__ void wave_costs(const Seg64Args& a, PlanLds& L, int W)
 {
     for (int b = threadIdx.x; b < W; b += kPlanBatch * kPlanThreads) {
         WaveSpan sp[kPlanBatch];
-        int r[kPlanBatch];
+        int r[kPlanBatch], rs[kPlanBatch];
 #pragma unroll
         for (int k = 0; k < kPlanBatch; ++k) {
             const int w = b + k * kPlanThreads;
-            sp[k] = w < W ? wave_span(L, w) : WaveSpan{0, 0, 0, 0};
+            sp[k] = w < W ? wave_span(L, w) : WaveSpan{0, 0, 0};
         }
 #pragma unroll
-        for (int k = 0; k < kPlanBatch; ++k) r[k] = sp[k].e0 < sp[k].e1 ? a.sorted_r[sp[k].e0] : 0;
+        for (int k = 0; k < kPlanBatch; ++k) r[k] = rs[k] = sp[k].e0 < sp[k].e1 ? a.sorted_r[sp[k].e0] : 0;
         unsigned cm = 0;
 #pragma unroll
         for (int k = 0; k < kPlanBatch; ++k) {
 #pragma unroll 4
-            for (int e = sp[k].e0 + 1; e < sp[k].e1; ++e) r[k] = max(r[k], a.sorted_r[e]);
+            for (int e = sp[k].e0 + 1; e < sp[k].e1; ++e) {
+                const int v = a.sorted_r[e];
+                r[k] = max(r[k], v);
+                rs[k] += v;
+            }
             const int w = b + k * kPlanThreads;
             if (w < W) {
-                const unsigned c = unsigned(r[k] + (1 << sp[k].kk) - 1) * unsigned(sp[k].bc * 14 + 40);
-                L.cost[w] = c;
-                cm = max(cm, c);
+                const int c = sp[k].c;
+                const int steps = (c < kChainClasses ? rs[k] : r[k]) + (1 << class_k(c)) - 1;
+                const unsigned cost = unsigned(steps) * unsigned(class_bc(c) * 14 + 40);
+                L.cost[w] = cost;
+                cm = max(cm, cost);
             }
         }
         if (cm) atomicMax(&L.cmax, cm);
@@ -326,21 +343,37 @@ __device__ __forceinline__ void plan_stamp(const Seg64Args& a, PlanLds& L, int i
     if (a.timeline && threadIdx.x == 0) L.phase[i] = __builtin_amdgcn_s_memrealtime();
 }
 
+// Exclusive prefix sum over the 64 lanes of a wave (and the total).
+__device__ __forceinline__ int wave_excl_scan(int v, int& total)
+{
+    const int lane = __lane_id();
+    int inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int u = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += u;
+    }
+    total = __shfl(inc, 63, 64);
+    return inc - v;
+}
+
 // The fp64 pass's plan over the n > 0 listed pairs, by one workgroup of the
 // fp64 launch (the first to arrive; the others wait for its flag): the width
 // bound bc0 (32 unless the lanes at width 32 give fewer than min_lanes, 2
-// waves per SIMD, then 16, then 8), the classes, the list scattered into class
-// order (`sorted`, with each pair's R in `sorted_r`; the last class into
-// `big`), and the dispatch order. Its time is on the pass's critical path
-// (every other workgroup waits) and it is load latency, so the list is walked
-// twice only: once counting the classes at all three candidate bc0 together
-// (with the lanes that choose bc0), once scattering; the wave costs read R
-// from sorted_r. (Three walks and the costs' dependent descriptor loads:
-// 55 us from the fp32 pass's last wave to the first fp64 wave on S4, 91 us on
-// S4-20k, profiles/r06_timeline_*.)
-__device__ void plan_rescue(const Seg64Args& a, int n, PlanLds& L)
+// waves per SIMD, then 16, then 8), the classes (and in passes of many waves
+// the chains), the list scattered into class order (`sorted`, with each
+// pair's R in `sorted_r`; the last class into `big`), and the dispatch order.
+// Its time is on the pass's critical path (every other workgroup waits) and
+// it is load latency, so the list is walked twice only: once counting the
+// classes at all three candidate bc0 together (with the lanes that choose
+// bc0), once scattering; the class table is one wave's scans and the wave
+// costs read R from sorted_r. (Three walks, a serial class table and the
+// costs' dependent descriptor loads: 55 us from the fp32 pass's last wave to
+// the first fp64 wave on S4, 91 us on S4-20k, profiles/r06_timeline_*.)
+__device__ __forceinline__ void plan_rescue(const Seg64Args& a, int n, PlanLds& L)
 {
     constexpr int NC = kSeg64Classes;
+    static_assert(NC <= 64, "the class table is one wave");
     const int t = threadIdx.x;
     for (int q = t; q < 3 * NC; q += kPlanThreads) (&L.cnt3[0][0])[q] = 0;
     if (t == 0) {
@@ -364,38 +397,63 @@ __device__ void plan_rescue(const Seg64Args& a, int n, PlanLds& L)
     const long long l32 = (long long)L.lanes;
     const int b3 = l32 >= a.min_lanes ? 0 : (2 * l32 >= a.min_lanes ? 1 : 2);
     const int bc0 = 32 >> b3;
-    if (t == 0) {
-        Seg64Plan* __restrict__ p = a.plan;   // written in place (a local copy would live in registers)
-        p->bc0 = bc0;
-        int off = 0, wb = 0;
-        for (int c = 0; c < NC; ++c) {
-            const int nc = L.cnt3[b3][c];
+    if (t < 64) {   // the class table: lane c holds class c
+        const int c = t;
+        const int S = a.n_simd;
+        const bool real = c >= kChainClasses && c < NC;
+        const int n0 = real ? L.cnt3[b3][c] : 0;
+        const int per0 = 64 >> class_k(min(c, NC - 1));
+        int w_all, n64;
+        (void)wave_excl_scan(real && c < NC - 1 ? (n0 + per0 - 1) / per0 : 0, w_all);
+        const bool is64 = c >= kChainClasses && c < kChainClasses + kSeg64Widths;   // 64-lane classes
+        (void)wave_excl_scan(is64 ? n0 : 0, n64);
+        // Chains only in passes of many waves (fetched greedily), and only the
+        // 64-lane pairs past chain_tail rounds of single waves (two per SIMD),
+        // so the greedy order still ends on short waves; spread over the
+        // widths by their share.
+        const int L_ch = (a.wave_order && a.chain > 1 && w_all > 2 * S) ? a.chain : 1;
+        const long long chained = L_ch > 1 ? max(0LL, (long long)n64 - (long long)a.chain_tail * 2 * S) : 0;
+        const int cc = is64 && chained > 0 ? int((long long)n0 * chained / n64) / L_ch * L_ch : 0;
+        const int cc_chain = __shfl(cc, c + kChainClasses < 64 ? c + kChainClasses : c, 64);   // chain class c's pairs
+        const int nc = c < kChainClasses ? cc_chain : n0 - cc;
+        const int per = c < kChainClasses ? L_ch : per0;
+        int tot_n, tot_w;
+        const int off = wave_excl_scan(c < NC ? nc : 0, tot_n);
+        const int wb = wave_excl_scan(c < NC - 1 ? (nc + per - 1) / per : 0, tot_w);
+        if (c < NC) {
+            Seg64Plan* __restrict__ p = a.plan;
             L.cnt[c] = nc;
+            L.off[c] = off;
+            L.fill[c] = 0;
+            L.wbase[c] = wb;
             p->n_class[c] = nc;
             p->off_class[c] = off;
-            L.fill[c] = off;
-            off += nc;
             p->wave_base[c] = wb;
-            L.wbase[c] = wb;
-            if (c < NC - 1) {
-                const int per = 64 >> (6 - c / kSeg64Widths);
-                wb += (nc + per - 1) / per;
-            }
+            if (c == NC - 1) *a.big_count = nc;
         }
-        p->dynamic = a.wave_order != nullptr && wb > 2 * a.n_simd;
-        *a.big_count = L.cnt[NC - 1];
+        if (c == 0) {
+            L.chain = L_ch;
+            a.plan->bc0 = bc0;
+            a.plan->chain = L_ch;
+            a.plan->dynamic = a.wave_order != nullptr && w_all > 2 * S;
+        }
     }
     __syncthreads();
     plan_stamp(a, L, 1);
     plan_walk(a, n, [&](int pid, int R, int H) {
         const int c = rescue_class(H, bc0);
-        const int pos = atomicAdd(&L.fill[c], 1);
-        if (c < NC - 1) {
-            a.sorted[pos] = pid;
-            a.sorted_r[pos] = R;
-        } else {
-            a.big[pos - (n - L.cnt[NC - 1])] = pid;
+        const int q = atomicAdd(&L.fill[c], 1);   // this pair's place in its class
+        if (c == NC - 1) {
+            a.big[q] = pid;
+            return;
         }
+        // A 64-lane class's first pairs go to its chain class.
+        const bool c64 = c < kChainClasses + kSeg64Widths;
+        const int ch = c - kChainClasses;
+        const int nch = c64 ? L.cnt[ch] : 0;
+        const int pos = q < nch ? L.off[ch] + q : L.off[c] + q - nch;
+        a.sorted[pos] = pid;
+        a.sorted_r[pos] = R;
     });
     __syncthreads();
     plan_stamp(a, L, 2);
@@ -416,14 +474,8 @@ __device__ void plan_rescue(const Seg64Args& a, int n, PlanLds& L)
     __syncthreads();
     if (t < 64) {   // exclusive prefix over the buckets: one wave, 4 buckets a lane
         const int4 h = reinterpret_cast<const int4*>(L.hist)[t];
-        const int s4 = h.x + h.y + h.z + h.w;
-        int inc = s4;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int v = __shfl_up(inc, d, 64);
-            if (t >= d) inc += v;
-        }
-        const int ex = inc - s4;
+        int tot;
+        const int ex = wave_excl_scan(h.x + h.y + h.z + h.w, tot);
         reinterpret_cast<int4*>(L.hist)[t] = make_int4(ex, ex + h.x, ex + h.x + h.y, ex + h.x + h.y + h.z);
     }
     __syncthreads();
@@ -576,13 +628,232 @@ __device__ __forceinline__ void wave_record(const Seg64Args& a, int w, unsigned 
         ((unsigned long long)unsigned(pid) << 40);
 }
 
+// Wave wk of a class of 2^k-lane slots (entries [ok, ok + nk) of `sorted`):
+// its pairs side by side, 64 >> k of them, each over 2^k lanes of bc columns
+// (seg_common.hpp run_seg). Returns the lane's pair id.
+__device__ __forceinline__ int slot_wave(const Seg64Args& a, const double* __restrict__ slut, uint2* __restrict__ mt,
+                                         int lane, int k, int bc, int ok, int nk, int wk, int pmode)
+{
+    const int e = wk * (64 >> k) + (lane >> k);
+    const bool valid = e < nk;
+    int s = lane & ((1 << k) - 1);
+    const int pid = a.sorted[ok + (valid ? e : wk * (64 >> k))];
+    const LaneCtx cx = pair_ctx(a.pairs, a.rows, a.hapw, pid);
+    const int nb = (cx.H + bc - 1) / bc;
+    const bool owner = valid && s == nb - 1;
+    if (!valid) s = 0;
+    const SegSteps st{wave_max(valid ? cx.R : 0), wave_min(valid ? cx.R : INT32_MAX),
+                      wave_max(valid ? cx.R + nb - 1 : 0), pmode, __builtin_amdgcn_s_memrealtime()};
+    const uint32_t w1 = row_word(cx, 0);
+    const double T0 = row0_t<double>(a.lut, w1, cx.H);
+    const bool wave_eq = __builtin_amdgcn_ballot_w64(!read_eq(w1)) == 0;
+    double sumM = 0.0, sumX = 0.0;
+    switch (bc) {
+#define HC_SEG64_CASE(WI) \
+    case seg64_width(WI): run_seg_bc<double, seg64_width(WI)>(a.lut, slut, st, lane, s, cx, T0, sumM, sumX, mt, wave_eq); break;
+        HC_SEG64_CASE(0) HC_SEG64_CASE(1) HC_SEG64_CASE(2) HC_SEG64_CASE(3) HC_SEG64_CASE(4) HC_SEG64_CASE(5)
+        HC_SEG64_CASE(6)
+#undef HC_SEG64_CASE
+    default: break;
+    }
+    if (owner) a.raw_out[pid] = sumM + sumX;
+    return pid;
+}
+
+// A chain's pairs (wave-uniform, in LDS): descriptor fields, the first row
+// word (the constant-gap check) and row 0's diagonal T0.
+struct ChainEnt {
+    int pid, R, H, nb;
+    unsigned rb, hb, w1, pad_;
+    double T0;
+};
+constexpr int kMtSlot = 5 * 64;   // one pair's match windows (uint2 per lane and read code)
+
+// A chain wave: np <= kMaxChain pairs of one 64-lane class (entries e0 ..
+// e0 + np - 1 of `sorted`) streamed through the same lanes one after the
+// other. Lane s sweeps global row g = k - s of the rows of pair 0, then pair
+// 1, ... (run_seg's column-segmented recurrence, EQ path): on reaching row 1
+// of the next pair it hands its owner's sums out, resets its block to that
+// pair's row 0 (T0 from column 0 on, X = 0) and takes its diagonal T0 and its
+// match window, so the pipeline fill and drain of 63 steps is paid once per
+// chain, not once per pair (S4-20k: R ~ 200 rows + 63 skew steps per pair).
+// The hand-offs need no change: lane s-1 is one row ahead in the same global
+// row order. The next row's word comes from the next pair's rows once past
+// the current pair's R (the prefetch base switches a row early). Every pair
+// must be an EQ read with the same gap constants (the reference's constant
+// 'I'/'I'/'+'): else returns false and the caller runs the pairs one by one.
+template <int BC>
+__device__ __forceinline__ bool chain_run(const Seg64Args& a, const double* __restrict__ slut, uint2* __restrict__ mt,
+                                          ChainEnt* __restrict__ ce, int lane, int e0, int np, int pmode)
+{
+    using T = double;
+    constexpr bool AND = BC * int(sizeof(T)) <= 128;
+    if (lane < np) {
+        const int pid = a.sorted[e0 + lane];
+        const LaneCtx cx = pair_ctx(a.pairs, a.rows, a.hapw, pid);
+        const uint32_t w1 = row_word(cx, 0);
+        ChainEnt e;
+        e.pid = pid;
+        e.R = cx.R;
+        e.H = cx.H;
+        e.nb = (cx.H + BC - 1) / BC;
+        e.rb = cx.rbyte;
+        e.hb = cx.hbyte;
+        e.w1 = w1;
+        e.pad_ = 0;
+        e.T0 = row0_t<T>(a.lut, w1, cx.H);
+        ce[lane] = e;
+    }
+    // (one wave: its LDS operations are in order; the fences keep the compiler's too)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t wa = ce[0].w1;
+    bool ok = read_eq(wa);
+    for (int q = 1; q < np; ++q) {
+        const uint32_t w = ce[q].w1;
+        ok = ok && read_eq(w) && row_i(w) == row_i(wa) && row_c(w) == row_c(wa);
+    }
+    if (!__builtin_amdgcn_readfirstlane(ok ? 1 : 0)) return false;
+    for (int q = 0; q < np; ++q) {
+        const ChainEnt e = ce[q];
+        const LaneCtx cx{a.rows - kRowPadBefore, e.rb, a.hapw, e.hb, e.R, e.H};
+        fill_window(mt + q * kMtSlot, lane, cx, lane * BC - (e.nb * BC - e.H));
+    }
+    const ChainEnt ea = ce[0];
+    const LaneCtx cx0{a.rows - kRowPadBefore, ea.rb, a.hapw, ea.hb, ea.R, ea.H};
+    const char* rbase = reinterpret_cast<const char*>(a.rows - kRowPadBefore);
+    int q = 0, G = 0, Rc = ea.R;
+    unsigned rbc = ea.rb;
+    unsigned rbn = np > 1 ? ce[1].rb - unsigned(Rc) * 4u : rbc;   // word widx >= Rc: the next pair's widx - Rc
+    T Tt[BC], X[BC];
+    const int c0a = lane * BC - (ea.nb * BC - ea.H);
+#pragma unroll
+    for (int j = 0; j < BC; ++j) {
+        Tt[j] = c0a + j + 1 >= 0 ? ea.T0 : T(0);
+        X[j] = T(0);
+    }
+    uint32_t wq = row_word(cx0, min(max(2 - lane, 1), Rc) - 1);   // the word of row i + 1 (PD = 1)
+    // The gap constants are the chain's (checked above): wave-uniform, so
+    // scalar loads and SGPRs (the per-lane form of run_seg spills here).
+    RowConst<T> k;
+    row_const<T>(a.lut, __builtin_amdgcn_readfirstlane(row_word(cx0, 0)),
+                 __builtin_amdgcn_readfirstlane(row_word(cx0, min(2, Rc) - 1)), k);
+    uint2 mrow = mt[k.rc * 64 + lane];
+    uint32_t keep = (lane + 1) * BC < ea.H ? 0xffffffffu : 0u;
+    T y_out = T(0);
+    T t_out = masked<AND>(ea.T0, keep);
+    T t_hold = c0a >= 0 ? ea.T0 : T(0);
+    T sumM = T(0), sumX = T(0);
+    auto step = [&](int kk, auto sum_tag) {
+        constexpr bool SUM = decltype(sum_tag)::value;
+        int i = kk - lane - G;   // this lane's row of its current pair
+        if (i > Rc && q + 1 < np) {   // row 1 of the next pair (once per pair and lane)
+            if (lane == ce[q].nb - 1) a.raw_out[ce[q].pid] = sumM + sumX;   // the finished pair's owner
+            G += Rc;
+            i -= Rc;
+            ++q;
+            const ChainEnt e = ce[q];
+            Rc = e.R;
+            rbc = e.rb;
+            rbn = q + 1 < np ? ce[q + 1].rb - unsigned(Rc) * 4u : rbc;
+            const int c0 = lane * BC - (e.nb * BC - e.H);
+            keep = (lane + 1) * BC < e.H ? 0xffffffffu : 0u;
+            const T T0 = e.T0;
+#pragma unroll
+            for (int j = 0; j < BC; ++j) {
+                Tt[j] = T0;
+                X[j] = T(0);
+            }
+            if (c0 < -1) {   // block 0's padding columns: 0 left of column 0
+#pragma unroll
+                for (int j = 0; j < BC; ++j)
+                    if (c0 + j + 1 < 0) Tt[j] = T(0);
+            }
+            t_hold = c0 >= 0 ? T0 : T(0);
+        }
+        const uint32_t wn = wq;   // row i + 1
+        const int qn = (i >= Rc && q + 1 < np) ? q + 1 : q;   // the pair of row i + 1
+        const int qo = row_q(wn), mo = row_rc(wn) * 64 + lane + qn * kMtSlot;
+        int widx = i + 1;   // the word of row i + 2
+        asm volatile("" : "+v"(widx) : "v"(qo), "v"(mo));
+        const T pm_n = slut[kOffPm + qo];
+        const T px_n = slut[kOffPx + qo];
+        const uint2 m_n = mt[mo];
+        wq = *reinterpret_cast<const uint32_t*>(rbase + ((widx < Rc ? rbc : rbn) + unsigned(widx) * 4u));
+        const T y_in = from_left(y_out);
+        const T t_in = from_left(t_out);
+        T sM_in = T(0), sX_in = T(0);
+        if constexpr (SUM) {
+            sM_in = from_left(sumM);
+            sX_in = from_left(sumX);
+        }
+        const T Tdiag = t_hold;
+        t_hold = t_in;
+        if (unsigned(i - 1) < unsigned(Rc)) {
+            if (SUM && i == Rc) {
+                sumM = lane ? sM_in : T(0);
+                sumX = lane ? sX_in : T(0);
+            }
+            T Ml = T(0), Yl = y_in;
+            const T M0 = Tdiag * prior_of<31>(mrow.x, k.pm, k.px);
+            cell<T, BC, 0, BC, SUM, true>(Tt, X, M0, Ml, Yl, mrow.x, mrow.y, k.pm, k.px, k, 0, sumM, sumX);
+            y_out = masked<AND>(y_next<true>(Ml, Yl, k.my, k.yy), keep);
+            t_out = masked<AND>(Tt[BC - 1], keep);
+        }
+        k.pm = pm_n;
+        k.px = px_n;
+        mrow = m_n;
+    };
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    // The chain's steps (for the issue priority): its rows and the last skew.
+    int nsteps = 0;
+    for (int qq = 0, g = 0; qq < np; ++qq) {
+        const int Rq = __builtin_amdgcn_readfirstlane(ce[qq].R), nbq = __builtin_amdgcn_readfirstlane(ce[qq].nb);
+        g += Rq;
+        nsteps = max(nsteps, g + nbq - 1);
+    }
+    // Row sums only in each pair's window of last rows (lane s: step G + R + s);
+    // the issue priority by remaining steps as the single waves set it.
+    int kk = 1, we = 0, Gq = 0;
+    int pk = pmode ? 1 : INT32_MAX;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    auto prio = [&]() {
+        if (kk >= pk) {
+            set_prio(pmode, kk, nsteps, t0);
+            pk += 16;
+        }
+    };
+    for (int qq = 0; qq < np; ++qq) {
+        const int Rq = __builtin_amdgcn_readfirstlane(ce[qq].R), nbq = __builtin_amdgcn_readfirstlane(ce[qq].nb);
+        const int ws = Gq + Rq;
+        we = max(we, ws + nbq - 1);
+        for (; kk < ws; ++kk) {
+            prio();
+            step(kk, std::false_type{});
+        }
+        for (; kk <= we; ++kk) {
+            prio();
+            step(kk, std::true_type{});
+        }
+        Gq += Rq;
+    }
+    if (lane == ce[q].nb - 1) a.raw_out[ce[q].pid] = sumM + sumX;
+    return true;
+}
+
 template <int OCC>
 __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
 {
-    __shared__ uint2 mtab[4][5 * 64];
+    // The planner's scratch, then (its plan published) the waves' match windows.
+    __shared__ union alignas(16) {
+        PlanLds plan;
+        uint2 mt[4][kMaxChain * kMtSlot];
+    } lds_u;
     __shared__ double slut[kSlutLen];
-    __shared__ PlanLds plan_lds;
+    __shared__ ChainEnt chain_lds[4][kMaxChain];
     __shared__ int role;
+    PlanLds& plan_lds = lds_u.plan;
     const int t = threadIdx.x;
     // The fp32 pass's rescue list is complete (stream order). Its plan is
     // made here, not by a launch of its own: an empty list (most runs) needs
@@ -605,6 +876,9 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
         plan_rescue(a, n, plan_lds);
         __syncthreads();
         plan_stamp(a, plan_lds, 5);
+        unsigned long long ph[kPlanPhases] = {};
+        if (t == 0 && a.timeline)   // (read before the waves reuse the LDS)
+            for (int i = 0; i < kPlanPhases; ++i) ph[i] = plan_lds.phase[i];
         // Publish (MI355X_MICROARCH.md, inter-workgroup visibility): every
         // storing wave drains its stores, then one lane releases and flags.
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -613,11 +887,11 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(a.ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (a.timeline) {   // (diagnostics) the plan's span
+            if (a.timeline) {   // (diagnostics) the plan's span and phases
                 a.timeline[3 * size_t(a.n_pairs)] = t_plan0;
                 a.timeline[3 * size_t(a.n_pairs) + 1] = __builtin_amdgcn_s_memrealtime();
                 a.timeline[3 * size_t(a.n_pairs) + 2] = (unsigned long long)n;
-                for (int i = 0; i < kPlanPhases; ++i) a.timeline[3 * size_t(a.n_pairs + 1) + i] = plan_lds.phase[i];
+                for (int i = 0; i < kPlanPhases; ++i) a.timeline[3 * size_t(a.n_pairs + 1) + i] = ph[i];
             }
         }
     }
@@ -662,13 +936,16 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
     const int total = __builtin_amdgcn_readfirstlane(p->wave_base[kSeg64Classes - 1]);
     if (int(blockIdx.x) * 4 >= total) return;   // workgroup-uniform: a short list costs no LDS fill
     load_slut(slut, a.lut);
-    uint2* mt = mtab[threadIdx.x >> 6];
+    uint2* mt = lds_u.mt[threadIdx.x >> 6];
+    ChainEnt* ce = chain_lds[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     // Lane l holds the first wave of class l + 1: a wave's class is the number
     // of class starts at or below it (wave_base is non-decreasing).
     static_assert(kSeg64Classes <= 65, "one ballot covers the classes");
     const int next_base = lane < kSeg64Classes - 1 ? p->wave_base[lane + 1] : INT32_MAX;
     const bool dyn = __builtin_amdgcn_readfirstlane(p->dynamic) != 0;
+    const int chain = __builtin_amdgcn_readfirstlane(p->chain);
+    const int pmode = a.prio ? (dyn ? 2 : 1) : 0;   // issue priority mode (seg_common.hpp set_prio)
     for (int pos = blockIdx.x * 4 + (threadIdx.x >> 6);;) {
         if (dyn) {   // greedy: the next wave in descending cost
             int v = 0;
@@ -679,34 +956,36 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
         const unsigned long long t_start = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
         const int w = (total > 1 && a.wave_order) ? __builtin_amdgcn_readfirstlane(a.wave_order[pos]) : pos;
         const int c = __popcll(__builtin_amdgcn_ballot_w64(next_base <= w));
-        const int k = 6 - c / kSeg64Widths;
-        const int bc = seg64_width(kSeg64Widths - 1 - c % kSeg64Widths);
+        const int bc = class_bc(c);
         const int nk = __builtin_amdgcn_readfirstlane(p->n_class[c]);
         const int ok = __builtin_amdgcn_readfirstlane(p->off_class[c]);
         const int wk = w - __builtin_amdgcn_readfirstlane(p->wave_base[c]);
-        const int e = wk * (64 >> k) + (lane >> k);
-        const bool valid = e < nk;
-        int s = lane & ((1 << k) - 1);
-        const int pid = a.sorted[ok + (valid ? e : wk * (64 >> k))];
-        const LaneCtx cx = pair_ctx(a.pairs, a.rows, a.hapw, pid);
-        const int nb = (cx.H + bc - 1) / bc;
-        const bool owner = valid && s == nb - 1;
-        if (!valid) s = 0;
-        const SegSteps st{wave_max(valid ? cx.R : 0), wave_min(valid ? cx.R : INT32_MAX),
-                          wave_max(valid ? cx.R + nb - 1 : 0), a.prio};
-        const uint32_t w1 = row_word(cx, 0);
-        const double T0 = row0_t<double>(a.lut, w1, cx.H);
-        const bool wave_eq = __builtin_amdgcn_ballot_w64(!read_eq(w1)) == 0;
-        double sumM = 0.0, sumX = 0.0;
-        switch (bc) {
-#define HC_SEG64_CASE(WI) \
-    case seg64_width(WI): run_seg_bc<double, seg64_width(WI)>(a.lut, slut, st, lane, s, cx, T0, sumM, sumX, mt, wave_eq); break;
-            HC_SEG64_CASE(0) HC_SEG64_CASE(1) HC_SEG64_CASE(2) HC_SEG64_CASE(3) HC_SEG64_CASE(4) HC_SEG64_CASE(5)
-            HC_SEG64_CASE(6)
-#undef HC_SEG64_CASE
-        default: break;
+        int pid;
+        // A chain of 64-lane pairs; with chains on, the single 64-lane pairs
+        // run as chains of one: the pass's 64-lane waves then run one step
+        // loop per width, not two (the instruction cache holds fewer loops;
+        // S4-20k's first round of chain waves beside single waves ran ~2.5x
+        // slower per step than either alone).
+        if (c < kChainClasses || (chain > 1 && class_k(c) == 6)) {
+            const int per = c < kChainClasses ? chain : 1;
+            const int e0 = ok + wk * per, np = min(per, nk - wk * per);
+            bool done = false;
+            switch (bc) {   // (64-lane pairs at bc0 = 32: 17-32 columns per lane)
+            case 20: done = chain_run<20>(a, slut, mt, ce, lane, e0, np, pmode); break;
+            case 24: done = chain_run<24>(a, slut, mt, ce, lane, e0, np, pmode); break;
+            case 28: done = chain_run<28>(a, slut, mt, ce, lane, e0, np, pmode); break;
+            case 32: done = chain_run<32>(a, slut, mt, ce, lane, e0, np, pmode); break;
+            default: break;
+            }
+            if (!done)   // not one gap-constant set: the pairs one at a time
+                for (int qq = 0; qq < np; ++qq) {
+                    __builtin_amdgcn_wave_barrier();
+                    (void)slot_wave(a, slut, mt, lane, 6, bc, e0 + qq, 1, 0, pmode);
+                }
+            pid = a.sorted[e0];
+        } else {
+            pid = slot_wave(a, slut, mt, lane, class_k(c), bc, ok, nk, wk, pmode);
         }
-        if (owner) a.raw_out[pid] = sumM + sumX;
         if (a.timeline && lane == 0) wave_record(a, w, t_start, pid);   // (diagnostics)
         __builtin_amdgcn_wave_barrier();   // the next wave's match table reuses mt
         if (!dyn) pos += gridDim.x * 4;

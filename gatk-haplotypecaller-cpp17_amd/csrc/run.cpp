@@ -54,6 +54,9 @@ int run_part(Part* b, hipStream_t s)
     r.min_lanes = int64_t(2) * 4 * dv.n_cu * 64;
     r.wave_order = env_i64("HC_PHMM_RESCUE_ORDER", 1) != 0 ? b->d_worder : nullptr;   // 0: class order (A/B)
     r.next_wave = b->d_count + kNextWave;
+    // 64-lane pairs chained in passes of many waves; 1: none (A/B)
+    r.chain = int(std::min<int64_t>(kMaxChain, std::max<int64_t>(1, env_i64("HC_PHMM_CHAIN", kMaxChain))));
+    r.chain_tail = int(std::max<int64_t>(0, env_i64("HC_PHMM_CHAIN_TAIL", 2)));
     r.n_simd = 4 * dv.n_cu;
     r.n_pairs = int(b->n);
     // Issue priority by remaining steps (seg_common.hpp set_prio_by_remaining):

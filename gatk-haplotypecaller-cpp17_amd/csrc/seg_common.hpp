@@ -230,7 +230,8 @@ struct SegSteps {
     int rmax;     // max R of the wave's pairs
     int rmin;     // first step that may need the row sums
     int nsteps;   // max over the wave's pairs of R + nb - 1
-    int prio = 0; // 1: issue priority by remaining steps (set_prio_by_remaining)
+    int prio = 0; // issue priority: 0 off, 1 by remaining steps, 2 by age (set_prio)
+    unsigned long long t0 = 0;   // the wave's start (s_memrealtime), for prio 2
 };
 
 // VALU issue between the waves of a SIMD is arbitrated by priority, then age
@@ -245,6 +246,29 @@ __device__ __forceinline__ void set_prio_by_remaining(int rem)
     else if (rem > 96) __builtin_amdgcn_s_setprio(2);
     else if (rem > 32) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
+}
+// In a pass whose waves are fetched from a counter, a hardware wave keeps its
+// slot for the whole launch, so between the two waves of a SIMD the older
+// always wins a tie: with chains of four, one wave per SIMD took 3.2 ms while
+// the other slot ran four 0.78 ms chains (tools/chain_probe.py, DESIGN.md
+// §16.2), and neither the remaining-steps bands nor bands by progress undid
+// it (a fresh wave on the older slot ties or outranks the starved one). There
+// the priority rises with the time since the wave's start instead (quanta of
+// ~100 us): the wave that started first goes first, as if each wave were a
+// fresh hardware wave dispatched in order.
+__device__ __forceinline__ void set_prio_by_age(unsigned long long t0)
+{
+    const unsigned long long q = (__builtin_amdgcn_s_memrealtime() - t0) / 10000;   // 100 MHz ticks
+    if (q >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (q == 2) __builtin_amdgcn_s_setprio(2);
+    else if (q == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
+// prio mode: 1 by remaining steps, 2 by the wave's age (SegSteps::prio).
+__device__ __forceinline__ void set_prio(int mode, int kk, int nsteps, unsigned long long t0)
+{
+    if (mode == 2) set_prio_by_age(t0);
+    else set_prio_by_remaining(nsteps - kk);
 }
 
 // Rows of read words a lane keeps in flight (loaded PD steps before use). A
@@ -435,14 +459,14 @@ __device__ __forceinline__ void run_seg(const T* __restrict__ lut, const T* __re
     int pk = st.prio ? 1 : INT32_MAX;   // next step at which the priority is updated (every 16 steps)
     for (; kk + PD - 1 < st.rmin; kk += PD) {
         if (kk >= pk) {
-            set_prio_by_remaining(st.nsteps - kk);
+            set_prio(st.prio, kk, st.nsteps, st.t0);
             pk += 16;
         }
         for_phases<0, PD>([&](auto ph) { step(kk + decltype(ph)::value, std::false_type{}, ph); });
     }
     for (; kk <= st.nsteps; kk += PD) {
         if (kk >= pk) {
-            set_prio_by_remaining(st.nsteps - kk);
+            set_prio(st.prio, kk, st.nsteps, st.t0);
             pk += 16;
         }
         for_phases<0, PD>([&](auto ph) { step(kk + decltype(ph)::value, std::true_type{}, ph); });

@@ -658,14 +658,25 @@ def test_rescue_shapes(engine, oracle_lib, shape):
     bt.close()
 
 
-@pytest.mark.parametrize("case", ["long-haps", "mixed-reads", "short-reads"])
-def test_fp64_long_haps_many_waves(engine, oracle_lib, case):
+@pytest.mark.parametrize("case", ["long-haps", "mixed-reads", "short-reads", "long-haps-chained",
+                                  "mixed-reads-chained", "short-reads-chained", "long-haps-chain2"])
+def test_fp64_long_haps_many_waves(engine, oracle_lib, monkeypatch, case):
     """An fp64 pass of many waves over long haps: 4 000 pairs of 1 025-2 048-
     base haps, most rescued, so the plan sorts thousands of 64-lane waves and
     dispatches them greedily from the wave counter (more than two waves per
     SIMD) — against the oracle, flat and through a prepared batch run twice.
     mixed-reads: some reads with an 'N' base, some with insertion != deletion
-    gap qualities and a hap with an 'N'; short-reads: R 40-639."""
+    gap qualities and a hap with an 'N'; short-reads: R 40-639 (a chain's
+    windows of last rows overlap). -chained: every 64-lane pair chained
+    (HC_PHMM_CHAIN_TAIL=0; by default only passes past two rounds of single
+    waves chain), up to 4 pairs a wave through the same lanes (lane_kernel.hip
+    chain_run; a chain holding a non-EQ read or other gap constants runs its
+    pairs one by one); -chain2: chains of 2."""
+    if case.endswith("-chained") or case.endswith("-chain2"):
+        monkeypatch.setenv("HC_PHMM_CHAIN_TAIL", "0")
+    if case.endswith("-chain2"):
+        monkeypatch.setenv("HC_PHMM_CHAIN", "2")
+    case = case.replace("-chained", "").replace("-chain2", "")
     r_range = (40, 639) if case == "short-reads" else (150, 250)
     b = W.generate(4000, (1025, 2048), r_range, 0.08, seed=97)
     if case == "mixed-reads":
@@ -675,8 +686,12 @@ def test_fp64_long_haps_many_waves(engine, oracle_lib, case):
             rs[ro[p] + 5] = ord("N")
         for p in range(3, 4000, 53):
             dels[ro[p]:ro[p] + b["R"][p]] = ord("J")   # constant gaps, insertion != deletion
+        ins = b["ins"].copy()
+        for p in range(5, 4000, 61):   # EQ reads with other gap constants than the rest
+            ins[ro[p]:ro[p] + b["R"][p]] = ord("J")
+            dels[ro[p]:ro[p] + b["R"][p]] = ord("J")
         hap[b["hap_off"][11] + 100] = ord("N")
-        b = dict(b, rs=rs, dels=dels, hap=hap)
+        b = dict(b, rs=rs, ins=ins, dels=dels, hap=hap)
     ref = oracle_lib.pairs(b, nthreads=16)
     assert ref["rescued"].sum() > 3000
     assert_same(engine.pairs(b), ref, f"{case} flat")

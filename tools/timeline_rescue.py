@@ -88,6 +88,10 @@ if len(r64):
                                      start_us=round(s64[k], 1), dur_us=round(d64[k], 1)),
                        longest=dict(pair=int(pid[kd]), R=int(b["R"][pid[kd]]), H=int(b["H"][pid[kd]]),
                                     dur_us=round(d64[kd], 1)))
+    out["fp64"]["dur_pct_us"] = {str(q): round(float(np.percentile(d64, q)), 1) for q in (75, 90, 95, 99)}
+    top = np.argsort(-d64)[:12]
+    out["fp64"]["longest_waves"] = [dict(pair=int(pid[j]), R=int(b["R"][pid[j]]), H=int(b["H"][pid[j]]),
+                                         start_us=round(s64[j], 1), dur_us=round(d64[j], 1)) for j in top]
     sim = simd_of(r64[:, 2])
     busy = {}
     cnt = {}
