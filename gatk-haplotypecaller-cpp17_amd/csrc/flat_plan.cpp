@@ -666,7 +666,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     const size_t o_rec = L.take(sizeof(uint4) * n1);   // seg slot records (every pair is a seg pair)
     const size_t o_slotof = L.take(sizeof(int) * n1);
     const size_t o_sdesc = L.take(sizeof(PairDesc) * n1);
-    const size_t o_sorted = L.take(2 * sizeof(int) * n1);   // pair ids, then their R (Seg64Args::sorted_r)
+    const size_t o_sorted = L.take(sizeof(int) * n1);
     const size_t o_worder = L.take(sizeof(int) * n1);
     const size_t o_big = L.take(sizeof(int) * n1);
     const size_t o_bigc = L.take(sizeof(int));

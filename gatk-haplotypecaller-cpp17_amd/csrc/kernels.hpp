@@ -121,7 +121,6 @@ struct Seg64Args {
     int* ticket_reset;        // the other run parity's ticket and flag, zeroed for the next run
     int* ready_reset;
     int* sorted;              // list in class order (n entries)
-    int* sorted_r;            // each sorted entry's R (n entries; the wave costs read it)
     int* big;                 // last-class pairs (anti-diagonal fp64 kernel)
     int* big_count;
     Seg64Plan* plan;

@@ -251,26 +251,6 @@ struct PlanLds {
     unsigned cost[kMaxSortWaves];
 };
 
-// Entries [e0, e1) of `sorted` and the class of wave w (class order) of the
-// plan in L.
-struct WaveSpan {
-    int e0, e1, c;
-};
-__device__ __forceinline__ WaveSpan wave_span(const PlanLds& L, int w)
-{
-    constexpr int NC = kSeg64Classes;
-    int lo = 0, hi = NC - 1;   // the last class whose first wave is <= w
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (L.wbase[mid] <= w) lo = mid;
-        else hi = mid;
-    }
-    const int c = lo;
-    const int per = c < kChainClasses ? L.chain : 64 >> class_k(c);
-    const int e0 = L.off[c] + (w - L.wbase[c]) * per;
-    return WaveSpan{e0, min(L.off[c] + L.cnt[c], e0 + per), c};
-}
-
 // The planner is one workgroup walking the list, so its time is load
 // latency: each thread takes kPlanBatch entries at a time and issues their
 // independent loads together (the list entries, then their pairs' R and H)
@@ -301,40 +281,25 @@ __device__ __forceinline__ void plan_walk(const Seg64Args& a, int n, F&& f)
 
 // Modelled costs of waves [0, W) into L.cost (and their maximum into L.cmax):
 // steps x (14 ops per column + ~40 per step), steps = max R + skew (pairs side
-// by side) or sum of R + skew (a chain); the rows from sorted_r (written by
-// the scatter: no dependent load of the descriptors).
-__device__ __forceinline__ void wave_costs(const Seg64Args& a, PlanLds& L, int W)
+// by side) or sum of R + skew (a chain). L.cost[w] holds wave w's max / sum of
+// R on entry (aggregated in LDS by the scatter: no loads here).
+__device__ __forceinline__ void wave_costs(PlanLds& L, int W)
 {
-    for (int b = threadIdx.x; b < W; b += kPlanBatch * kPlanThreads) {
-        WaveSpan sp[kPlanBatch];
-        int r[kPlanBatch], rs[kPlanBatch];
-#pragma unroll
-        for (int k = 0; k < kPlanBatch; ++k) {
-            const int w = b + k * kPlanThreads;
-            sp[k] = w < W ? wave_span(L, w) : WaveSpan{0, 0, 0};
+    constexpr int NC = kSeg64Classes;
+    unsigned cm = 0;
+    for (int w = threadIdx.x; w < W; w += kPlanThreads) {
+        int lo = 0, hi = NC - 1;   // wave w's class: the last whose first wave is <= w
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (L.wbase[mid] <= w) lo = mid;
+            else hi = mid;
         }
-#pragma unroll
-        for (int k = 0; k < kPlanBatch; ++k) r[k] = rs[k] = sp[k].e0 < sp[k].e1 ? a.sorted_r[sp[k].e0] : 0;
-        unsigned cm = 0;
-#pragma unroll
-        for (int k = 0; k < kPlanBatch; ++k) {
-#pragma unroll 4
-            for (int e = sp[k].e0 + 1; e < sp[k].e1; ++e) {
-                const int v = a.sorted_r[e];
-                r[k] = max(r[k], v);
-                rs[k] += v;
-            }
-            const int w = b + k * kPlanThreads;
-            if (w < W) {
-                const int c = sp[k].c;
-                const int steps = (c < kChainClasses ? rs[k] : r[k]) + (1 << class_k(c)) - 1;
-                const unsigned cost = unsigned(steps) * unsigned(class_bc(c) * 14 + 40);
-                L.cost[w] = cost;
-                cm = max(cm, cost);
-            }
-        }
-        if (cm) atomicMax(&L.cmax, cm);
+        const int steps = int(L.cost[w]) + (1 << class_k(lo)) - 1;
+        const unsigned cost = unsigned(steps) * unsigned(class_bc(lo) * 14 + 40);
+        L.cost[w] = cost;
+        cm = max(cm, cost);
     }
+    if (cm) atomicMax(&L.cmax, cm);
 }
 
 // (diagnostics) phase stamp i of the planner, after a barrier
@@ -361,13 +326,13 @@ __device__ __forceinline__ int wave_excl_scan(int v, int& total)
 // fp64 launch (the first to arrive; the others wait for its flag): the width
 // bound bc0 (32 unless the lanes at width 32 give fewer than min_lanes, 2
 // waves per SIMD, then 16, then 8), the classes (and in passes of many waves
-// the chains), the list scattered into class order (`sorted`, with each
-// pair's R in `sorted_r`; the last class into `big`), and the dispatch order.
+// the chains), the list scattered into class order (`sorted`; the last class
+// into `big`), and the dispatch order.
 // Its time is on the pass's critical path (every other workgroup waits) and
 // it is load latency, so the list is walked twice only: once counting the
 // classes at all three candidate bc0 together (with the lanes that choose
-// bc0), once scattering; the class table is one wave's scans and the wave
-// costs read R from sorted_r. (Three walks, a serial class table and the
+// bc0), once scattering (and aggregating each wave's R in LDS); the class
+// table is one wave's scans. (Three walks, a serial class table and the
 // costs' dependent descriptor loads: 55 us from the fp32 pass's last wave to
 // the first fp64 wave on S4, 91 us on S4-20k, profiles/r06_timeline_*.)
 __device__ __forceinline__ void plan_rescue(const Seg64Args& a, int n, PlanLds& L)
@@ -439,6 +404,12 @@ __device__ __forceinline__ void plan_rescue(const Seg64Args& a, int n, PlanLds& 
         }
     }
     __syncthreads();
+    const int W = L.wbase[NC - 1];   // segmented waves
+    const bool sort = W > 1 && a.wave_order && W <= kMaxSortWaves;
+    if (sort) {   // the waves' R aggregates (max, or sum for a chain), filled by the scatter
+        for (int w = t; w < W; w += kPlanThreads) L.cost[w] = 0;
+        __syncthreads();
+    }
     plan_stamp(a, L, 1);
     plan_walk(a, n, [&](int pid, int R, int H) {
         const int c = rescue_class(H, bc0);
@@ -451,20 +422,26 @@ __device__ __forceinline__ void plan_rescue(const Seg64Args& a, int n, PlanLds& 
         const bool c64 = c < kChainClasses + kSeg64Widths;
         const int ch = c - kChainClasses;
         const int nch = c64 ? L.cnt[ch] : 0;
-        const int pos = q < nch ? L.off[ch] + q : L.off[c] + q - nch;
-        a.sorted[pos] = pid;
-        a.sorted_r[pos] = R;
+        const bool chained = q < nch;
+        const int cls = chained ? ch : c, idx = chained ? q : q - nch;
+        a.sorted[L.off[cls] + idx] = pid;
+        if (sort) {
+            const int w = L.wbase[cls] + (chained ? idx / L.chain : idx >> (6 - class_k(cls)));
+            if (chained)
+                atomicAdd(&L.cost[w], unsigned(R));
+            else
+                atomicMax(&L.cost[w], unsigned(R));
+        }
     });
     __syncthreads();
     plan_stamp(a, L, 2);
-    const int W = L.wbase[NC - 1];   // segmented waves
     if (W <= 1 || !a.wave_order) return;
     if (W > kMaxSortWaves) {   // classes longest first, fetched in that order
         for (int w = t; w < W; w += kPlanThreads) a.wave_order[w] = w;
         return;
     }
     // Costs, then a counting sort by cost descending over 256 buckets.
-    wave_costs(a, L, W);
+    wave_costs(L, W);
     L.hist[t] = 0;
     __syncthreads();
     plan_stamp(a, L, 3);

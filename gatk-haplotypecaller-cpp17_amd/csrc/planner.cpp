@@ -1076,7 +1076,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const size_t o_rec = L.take(sizeof(uint4) * std::max<size_t>(size_t(n_seg_slots), 1));   // seg slot records
     const size_t o_sdesc = L.take(sizeof(PairDesc) * std::max<size_t>(size_t(n_seg_slots), 1));   // slot -> descriptor
     const size_t o_list = L.take(sizeof(int) * n1);
-    const size_t o_sorted = L.take(2 * sizeof(int) * n1);   // pair ids, then their R (Seg64Args::sorted_r)
+    const size_t o_sorted = L.take(sizeof(int) * n1);
     const size_t o_worder = L.take(sizeof(int) * n1);
     const size_t o_big = L.take(sizeof(int) * n1);
     const size_t o_bigc = L.take(sizeof(int));

@@ -46,7 +46,6 @@ int run_part(Part* b, hipStream_t s)
     r.ready = b->d_count + kPlanReady + par;
     r.ready_reset = b->d_count + kPlanReady + (par ^ 1);
     r.sorted = b->d_sorted;
-    r.sorted_r = b->d_sorted + b->n;
     r.big = b->d_big;
     r.big_count = b->d_big_count;
     r.plan = b->d_plan;

@@ -32,6 +32,10 @@ buf = np.zeros(3 * cap, np.uint64)
 n64 = L.hcx_timeline64(buf.ctypes.data, cap)
 r = buf[:3 * n64].reshape(n64, 3).astype(np.int64)[:n]
 r = r[r[:, 1] > 0]
+if not len(r):   # (HC_PHMM_TIMELINE=0: the kernel time only, e.g. under rocprofv3 --pmc)
+    print(json.dumps(dict(R=R, H=H, pairs=n, kernel_ms_f64=round(st.kernel_ms_f64, 4))), flush=True)
+    bt.close()
+    sys.exit(0)
 d = (r[:, 1] - r[:, 0]) / 100.0
 s = (r[:, 0] - r[:, 0].min()) / 100.0
 e = (r[:, 1] - r[:, 0].min()) / 100.0
