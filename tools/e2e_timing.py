@@ -15,6 +15,11 @@ hcphmm.init(0)
 print(f"init: {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
 b = W.config(sys.argv[1] if len(sys.argv) > 1 else "S2")
 cells = W.cells(b)
+if os.environ.get("PRE_BATCH"):   # as bench.py: a resident batch of the same pairs created and run first
+    bt = hcphmm.Batch(b)
+    for _ in range(3):
+        bt.run()
+    print(f"resident batch: {bt.stats().run_ms:.2f} ms", flush=True)
 out = hcphmm.result_arrays(len(b["R"]))
 for v in out.values():
     v.fill(0)
