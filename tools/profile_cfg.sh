@@ -25,7 +25,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$NAME
 rm -rf $OUT; mkdir -p $OUT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B > $OUT/trace.log 2>&1
+HC_BENCH_DETAIL=$PWD/$OUT/detail.json timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B > $OUT/trace.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $B > $OUT/fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $B > $OUT/write.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $OUT/sq -o run -- $B > $OUT/sq.log 2>&1
@@ -33,9 +33,9 @@ if [ "$WL" = region ]; then
     CELLS=$(python3 -c "import sys; sys.path.insert(0, 'gatk-haplotypecaller-cpp17_amd'); import workloads as W; print(W.cells(W.region_flat(*W.region(415, $NP))))")
     RC=0
 else
-    # cells and rescued cells of the profiled batch, from the bench line itself
-    CELLS=$(python3 -c "import json; d=[json.loads(l) for l in open('$OUT/trace.log') if l.startswith('{')][-1]; print(d['config']['cells'])")
-    RC=$(python3 -c "import json; d=[json.loads(l) for l in open('$OUT/trace.log') if l.startswith('{')][-1]; print(d['config'].get('rescued_cells') or 0)")
+    # cells and rescued cells of the profiled batch, from the bench run's detail record
+    CELLS=$(python3 -c "import json; d=json.load(open('$OUT/detail.json')); print(d['config']['cells'])")
+    RC=$(python3 -c "import json; d=json.load(open('$OUT/detail.json')); print(d['config'].get('rescued_cells') or 0)")
 fi
 python3 tools/profile_summary.py $OUT/${ROUND}_pmc_$NAME.json --trace $OUT/trace --skip $W --cells $CELLS --rescued-cells $RC $EXTRA \
     fetch=$OUT/fetch write=$OUT/write sq=$OUT/sq > $OUT/summary.log
