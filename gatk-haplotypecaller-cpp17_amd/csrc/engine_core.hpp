@@ -119,7 +119,13 @@ struct Device {
     // mean over the calls so far (0: none yet): sizes a call's parts
     // (api.cpp submit_flat, HC_PHMM_PART_GROWTH_PCT).
     std::atomic<double> stage_ps_per_cell{0.0};
+    // Flat parts left to start with the nibble records without trying the
+    // compact ones: set when a part's compact attempt is refused in pass 2 (a
+    // rare 'N' its sample missed), so data that carries them pays one refusal
+    // per kNibbleParts parts, not one per part (flat_plan.cpp plan_flat_device).
+    std::atomic<int> nibble_parts{0};
 };
+constexpr int kNibbleParts = 64;
 
 // Engine state, guarded by g_mu: the device list, the slot pools, the
 // outstanding counters, and the number of parts alive and calls running (a

@@ -14,6 +14,14 @@ t0 = time.perf_counter()
 hcphmm.init(0)
 print(f"init: {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
 b = W.config(sys.argv[1] if len(sys.argv) > 1 else "S2")
+if os.environ.get("N_FRAC"):   # put an 'N' base into this fraction of the reads (real reads carry them)
+    frac = float(os.environ["N_FRAC"])
+    rng = np.random.default_rng(7)
+    rs = b["rs"].copy()
+    picks = np.where(rng.random(len(b["R"])) < frac)[0]
+    rs[b["read_off"][picks] + (b["R"][picks] // 2)] = ord("N")
+    b = dict(b, rs=rs)
+    print(f"reads with an N: {len(picks)}", flush=True)
 cells = W.cells(b)
 if os.environ.get("PRE_BATCH"):   # as bench.py: a resident batch of the same pairs created and run first
     bt = hcphmm.Batch(b)
