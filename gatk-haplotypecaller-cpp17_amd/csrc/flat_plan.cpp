@@ -662,7 +662,7 @@ int plan_flat_try(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, 
     const size_t o_wcost = L.take(tail > 0 ? sizeof(int) * size_t(max_waves) : 0);
     const size_t o_nw = L.take(2 * sizeof(int));   // wave count, then the largest modelled wave cost
     const size_t o_res = L.take(res_bytes);
-    const size_t o_list = L.take(sizeof(int) * n1);
+    const size_t o_list = L.take(2 * sizeof(int) * n1);   // pair ids, then pack_rh (Seg64Args::list_rh)
     const size_t o_rec = L.take(sizeof(uint4) * n1);   // seg slot records (every pair is a seg pair)
     const size_t o_slotof = L.take(sizeof(int) * n1);
     const size_t o_sdesc = L.take(sizeof(PairDesc) * n1);

@@ -238,7 +238,11 @@ __global__ __launch_bounds__(64) void phmm_diag_kernel(DiagArgs a)
                 const bool resc = raw < 1e-28f;   // MIN_ACCEPTED, pairhmm_common.h:16
                 a.rescue_flag[pid] = resc;
                 a.raw64_zero[pid] = 0.0;
-                if (resc) a.rescue_list[atomicAdd(a.rescue_count, 1)] = pid;
+                if (resc) {
+                    const int pos = atomicAdd(a.rescue_count, 1);
+                    a.rescue_list[pos] = pid;
+                    a.rescue_rh[pos] = pack_rh(R, H);
+                }
             }
         }
         __syncthreads();   // ring reuse by the next pair group of this wave

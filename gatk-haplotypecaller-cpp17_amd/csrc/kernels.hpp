@@ -73,6 +73,7 @@ struct DiagArgs {
     void* raw_out;            // float[n_pairs] or double[n_pairs], by pair id
     uint8_t* rescue_flag;     // fp32 pass: 1 if raw < 1e-28f (by pair id)
     int* rescue_list;         // fp32 pass: appended pair ids
+    int* rescue_rh;           // fp32 pass: each appended pair's pack_rh(R, H) (the fp64 plan reads it)
     int* rescue_count;        // fp32 pass: append counter
     double* raw64_zero;       // fp32 pass: raw f64 result slot of each pair, zeroed
                               // (the rescue pass overwrites the rescued ones)
@@ -93,6 +94,13 @@ struct DiagArgs {
 // numbered before the others, whose waves stream up to `chain` pairs through
 // the same 64 lanes one after the other (lane_kernel.hip chain_run: the 63-step
 // skew of a 64-lane pair paid once per chain instead of once per pair).
+// A rescue list entry's R and H for the fp64 plan, written beside the pair id
+// (each clamped to 16 bits: H only selects the class, past 2 048 columns the
+// anti-diagonal one, and R only prices the wave).
+__host__ __device__ inline int pack_rh(int R, int H)
+{
+    return ((R < 65535 ? R : 65535) << 16) | (H < 65535 ? H : 65535);
+}
 constexpr int kSeg64Widths = 7;   // fp64 block widths 8, 12, ..., 32
 constexpr int kChainClasses = kSeg64Widths;
 constexpr int kMaxChain = 4;
@@ -113,6 +121,7 @@ struct Seg64Args {
     const uint32_t* hapw;
     const double* lut;
     int* list;                // rescue list (fp32 pass, arbitrary order)
+    const int* list_rh;       // each entry's pack_rh(R, H): the plan's walks read it coalesced
     const int* count;         // its length
     int* count_reset;         // the other run parity's counter, zeroed for the next run
     int* inker_reset;         // the other run parity's in-wave rescue counter, likewise
@@ -176,6 +185,7 @@ struct LaneArgs {
     float* raw_out;
     uint8_t* rescue_flag;
     int* rescue_list;
+    int* rescue_rh;           // as DiagArgs::rescue_rh
     int* rescue_count;
     double* raw64_zero;       // as DiagArgs::raw64_zero
     // Rescue inside the fp32 pass (column-segmented waves): a wave with at most
@@ -231,7 +241,8 @@ hipError_t launch_rescue_seg64(const Seg64Args& a, int grid, hipStream_t s);
 // 0 for every pair, so every pair takes the fp64 path. The fp32 pass is
 // replaced by this fill: raw_f32 = 0, rescued = 1 and the rescue list = all n
 // pairs (pair ids 0 .. n-1), *count = n.
-hipError_t launch_all_f64_list(int n, float* raw32, uint8_t* flag, int* list, int* count, hipStream_t s);
+hipError_t launch_all_f64_list(int n, float* raw32, uint8_t* flag, int* list, int* count, const PairDesc* pairs,
+                               int* list_rh, hipStream_t s);
 
 // Launchers (kernels.hip). W = lanes per pair: 16, 32 or 64.
 hipError_t launch_diag_f32(int W, const DiagArgs& a, int grid, hipStream_t s);

@@ -140,13 +140,17 @@ __device__ __forceinline__ LaneWave load_wave(const LaneWave* waves, int wid)
 
 // fp32 pass result of one pair: raw sum, rescue decision (intel_pairhmm.hpp:
 // 133-139), the pair's raw f64 slot zeroed (the rescue pass fills rescued ones).
-__device__ __forceinline__ void emit(const LaneArgs& a, int pid, float raw)
+__device__ __forceinline__ void emit(const LaneArgs& a, int pid, float raw, int R, int H)
 {
     a.raw_out[pid] = raw;
     const bool resc = raw < 1e-28f;   // MIN_ACCEPTED, pairhmm_common.h:16
     a.rescue_flag[pid] = resc;
     a.raw64_zero[pid] = 0.0;
-    if (resc) a.rescue_list[atomicAdd(a.rescue_count, 1)] = pid;
+    if (resc) {
+        const int pos = atomicAdd(a.rescue_count, 1);
+        a.rescue_list[pos] = pid;
+        a.rescue_rh[pos] = pack_rh(R, H);
+    }
 }
 
 // One lane per pair, column blocks of BC with the carry buffer between blocks.
@@ -174,7 +178,7 @@ __global__ __launch_bounds__(256, OCC) void phmm_lane_kernel(LaneArgs a)
         run_pairs<BC, true, false>(a, wv, lane, cx, T0, sumM, sumX, mt);
     else
         run_pairs<BC, false, false>(a, wv, lane, cx, T0, sumM, sumX, mt);
-    if (active) emit(a, pid, sumM + sumX);
+    if (active) emit(a, pid, sumM + sumX, cx.R, cx.H);
 }
 
 // Column-segmented fp32 waves (host-planned). The wave's npairs pairs are the
@@ -239,10 +243,15 @@ __device__ __forceinline__ int class_bc(int c)
 constexpr int kMaxSortWaves = 8192;
 constexpr int kPlanThreads = 256;   // the planning workgroup (a phmm_seg64_kernel workgroup)
 constexpr int kPlanPhases = 6;      // (diagnostics) the planner's phase stamps
+constexpr int kPlanCopies = 16;     // PlanLds counter copies
 
 struct PlanLds {
-    int cnt[kSeg64Classes], fill[kSeg64Classes], wbase[kSeg64Classes], off[kSeg64Classes];
-    int cnt3[3][kSeg64Classes];   // class counts at bc0 = 32, 16, 8 (one walk counts all three)
+    int cnt[kSeg64Classes], wbase[kSeg64Classes], off[kSeg64Classes];
+    // Class counts at the pass's bc0 and the scatter's cursors, in
+    // kPlanCopies copies by lane (lane & 15), so a class's LDS atomics from
+    // one wave hit 16 addresses, not one.
+    int cntx[kPlanCopies][kSeg64Classes];
+    int fillx[kPlanCopies][kSeg64Classes];
     int chain;
     alignas(16) int hist[256];
     unsigned long long lanes;
@@ -251,13 +260,13 @@ struct PlanLds {
     unsigned cost[kMaxSortWaves];
 };
 
-// The planner is one workgroup walking the list, so its time is load
-// latency: each thread takes kPlanBatch entries at a time and issues their
-// independent loads together (the list entries, then their pairs' R and H)
-// instead of one dependent pair per step (S4's 1 861 rescues: one round of
-// loads). f(pid, R, H) per listed pair.
-constexpr int kPlanBatch = 8;
-template <typename F>
+// The planner is one workgroup walking the list: each thread takes
+// kPlanBatch entries at a time, their pair ids and their R and H (written
+// beside the list by the fp32 pass: coalesced loads; gathering them from the
+// pair descriptors, 37 000 scattered lines for S4-20k from one CU, took its
+// count and scatter walks 34 and 40 us). f(pid, R, H) per listed pair.
+constexpr int kPlanBatch = 16;
+template <bool PID = true, typename F>
 __device__ __forceinline__ void plan_walk(const Seg64Args& a, int n, F&& f)
 {
     for (int b = threadIdx.x; b < n; b += kPlanBatch * kPlanThreads) {
@@ -266,12 +275,13 @@ __device__ __forceinline__ void plan_walk(const Seg64Args& a, int n, F&& f)
 #pragma unroll
         for (int k = 0; k < kPlanBatch; ++k) {
             const int i = b + k * kPlanThreads;
-            pid[k] = i < n ? a.list[i] : -1;
+            pid[k] = i < n ? (PID ? a.list[i] : 0) : -1;
         }
 #pragma unroll
-        for (int k = 0; k < kPlanBatch; ++k) {   // the descriptor {rows, R, table, H}: R and H
-            const int2* d = reinterpret_cast<const int2*>(a.pairs + (pid[k] >= 0 ? pid[k] : 0));
-            rh[k] = pid[k] >= 0 ? make_int2(d[0].y, d[1].y) : make_int2(0, 0);
+        for (int k = 0; k < kPlanBatch; ++k) {   // R and H beside the list (coalesced)
+            const int i = b + k * kPlanThreads;
+            const unsigned v = i < n ? unsigned(a.list_rh[i]) : 0u;
+            rh[k] = make_int2(int(v >> 16), int(v & 0xffffu));
         }
 #pragma unroll
         for (int k = 0; k < kPlanBatch; ++k)
@@ -340,33 +350,43 @@ __device__ __forceinline__ void plan_rescue(const Seg64Args& a, int n, PlanLds& 
     constexpr int NC = kSeg64Classes;
     static_assert(NC <= 64, "the class table is one wave");
     const int t = threadIdx.x;
-    for (int q = t; q < 3 * NC; q += kPlanThreads) (&L.cnt3[0][0])[q] = 0;
+    for (int q = t; q < kPlanCopies * NC; q += kPlanThreads) (&L.cntx[0][0])[q] = 0;
+    const int cp = t & (kPlanCopies - 1);   // this thread's counter copy
     if (t == 0) {
         L.lanes = 0;
         L.cmax = 1;
         *a.next_wave = 0;
     }
     __syncthreads();
+    // The lanes at width 32 (which choose bc0), then the class counts at that
+    // bc0: the LDS atomics are the walks' cost (one lane-op a cycle per CU:
+    // counting all three candidate bc0 in one walk took S4-20k's 52 us), the
+    // loads beside them are coalesced (list_rh).
     unsigned long long mine = 0;
-    plan_walk(a, n, [&](int, int, int H) {
-        mine += (H + 31) / 32;
-        atomicAdd(&L.cnt3[0][rescue_class(H, 32)], 1);
-        atomicAdd(&L.cnt3[1][rescue_class(H, 16)], 1);
-        atomicAdd(&L.cnt3[2][rescue_class(H, 8)], 1);
-    });
+    plan_walk<false>(a, n, [&](int, int, int H) { mine += (H + 31) / 32; });
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) mine += __shfl_xor(mine, d, 64);
     if (__lane_id() == 0 && mine) atomicAdd(&L.lanes, mine);
     __syncthreads();
-    plan_stamp(a, L, 0);
     const long long l32 = (long long)L.lanes;
     const int b3 = l32 >= a.min_lanes ? 0 : (2 * l32 >= a.min_lanes ? 1 : 2);
     const int bc0 = 32 >> b3;
+    plan_walk<false>(a, n, [&](int, int, int H) { atomicAdd(&L.cntx[cp][rescue_class(H, bc0)], 1); });
+    __syncthreads();
+    plan_stamp(a, L, 0);
     if (t < 64) {   // the class table: lane c holds class c
         const int c = t;
         const int S = a.n_simd;
         const bool real = c >= kChainClasses && c < NC;
-        const int n0 = real ? L.cnt3[b3][c] : 0;
+        int n0 = 0;
+        if (real) {   // the copies' counts, and each copy's first place in the class (the scatter's cursors)
+            for (int k = 0; k < kPlanCopies; ++k) {
+                L.fillx[k][c] = n0;
+                n0 += L.cntx[k][c];
+            }
+        } else if (c < NC) {
+            for (int k = 0; k < kPlanCopies; ++k) L.fillx[k][c] = 0;
+        }
         const int per0 = 64 >> class_k(min(c, NC - 1));
         int w_all, n64;
         (void)wave_excl_scan(real && c < NC - 1 ? (n0 + per0 - 1) / per0 : 0, w_all);
@@ -389,7 +409,6 @@ __device__ __forceinline__ void plan_rescue(const Seg64Args& a, int n, PlanLds& 
             Seg64Plan* __restrict__ p = a.plan;
             L.cnt[c] = nc;
             L.off[c] = off;
-            L.fill[c] = 0;
             L.wbase[c] = wb;
             p->n_class[c] = nc;
             p->off_class[c] = off;
@@ -413,7 +432,7 @@ __device__ __forceinline__ void plan_rescue(const Seg64Args& a, int n, PlanLds& 
     plan_stamp(a, L, 1);
     plan_walk(a, n, [&](int pid, int R, int H) {
         const int c = rescue_class(H, bc0);
-        const int q = atomicAdd(&L.fill[c], 1);   // this pair's place in its class
+        const int q = atomicAdd(&L.fillx[cp][c], 1);   // this pair's place in its class
         if (c == NC - 1) {
             a.big[q] = pid;
             return;
@@ -541,7 +560,7 @@ __device__ __forceinline__ void seg_wave(const LaneArgs& a, int wid, const float
         }
     }
     const uint64_t todo = __builtin_amdgcn_ballot_w64(resc);
-    if (todo) rescue_in_wave(a, todo, pid, slot, cx.H, lane, mt);
+    if (todo) rescue_in_wave(a, todo, pid, slot, cx.H, cx.R, lane, mt);
     if (a.timeline && lane == 0) {
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
         a.timeline[3 * size_t(wid)] = t_start;
@@ -971,12 +990,14 @@ __global__ __launch_bounds__(256, OCC) void phmm_seg64_kernel(Seg64Args a)
 
 __global__ __launch_bounds__(256) void all_f64_list_kernel(int n, float* __restrict__ raw32,
                                                           uint8_t* __restrict__ flag, int* __restrict__ list,
-                                                          int* __restrict__ count)
+                                                          int* __restrict__ count, const PairDesc* __restrict__ pairs,
+                                                          int* __restrict__ list_rh)
 {
     for (int p = blockIdx.x * 256 + threadIdx.x; p < n; p += gridDim.x * 256) {
         raw32[p] = 0.f;   // result_float = 0.0f (intel_pairhmm.hpp:135)
         flag[p] = 1;      // 0 < MIN_ACCEPTED: the double kernel for every pair
         list[p] = p;
+        list_rh[p] = pack_rh(pairs[p].y, pairs[p].w);
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) *count = n;
 }
@@ -1039,10 +1060,11 @@ hipError_t launch_lane_seg_f32(const LaneArgs& a, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_all_f64_list(int n, float* raw32, uint8_t* flag, int* list, int* count, hipStream_t s)
+hipError_t launch_all_f64_list(int n, float* raw32, uint8_t* flag, int* list, int* count, const PairDesc* pairs,
+                               int* list_rh, hipStream_t s)
 {
     const int grid = n <= 0 ? 1 : std::min((n + 255) / 256, 1024);
-    hipLaunchKernelGGL(all_f64_list_kernel, dim3(grid), dim3(256), 0, s, n, raw32, flag, list, count);
+    hipLaunchKernelGGL(all_f64_list_kernel, dim3(grid), dim3(256), 0, s, n, raw32, flag, list, count, pairs, list_rh);
     return hipGetLastError();
 }
 

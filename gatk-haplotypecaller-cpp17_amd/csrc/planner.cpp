@@ -1075,7 +1075,7 @@ int plan_part(Device& dv, const Src& src, const PartSpec& spec, Slot* slot, bool
     const size_t o_res = L.take(res_bytes);
     const size_t o_rec = L.take(sizeof(uint4) * std::max<size_t>(size_t(n_seg_slots), 1));   // seg slot records
     const size_t o_sdesc = L.take(sizeof(PairDesc) * std::max<size_t>(size_t(n_seg_slots), 1));   // slot -> descriptor
-    const size_t o_list = L.take(sizeof(int) * n1);
+    const size_t o_list = L.take(2 * sizeof(int) * n1);   // pair ids, then pack_rh (Seg64Args::list_rh)
     const size_t o_sorted = L.take(sizeof(int) * n1);
     const size_t o_worder = L.take(sizeof(int) * n1);
     const size_t o_big = L.take(sizeof(int) * n1);

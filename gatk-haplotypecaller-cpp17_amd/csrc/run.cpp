@@ -38,6 +38,7 @@ int run_part(Part* b, hipStream_t s)
     r.hapw = b->d_hapw;
     r.lut = dv.lut_d;
     r.list = b->d_list;
+    r.list_rh = b->d_list + b->n;
     r.count = count;
     r.count_reset = b->d_count + (par ^ 1);
     r.inker_reset = b->d_count + 2 + (par ^ 1);
@@ -79,7 +80,7 @@ int run_part(Part* b, hipStream_t s)
     // (intel_pairhmm.hpp:71,81,135-140).
     const bool all_f64 = (b->spec.flags & HC_PHMM_FLAG_F64) != 0;   // the call's mode (PartSpec::flags)
     bool solo = false;   // no fp64 launch after the fp32 pass (below)
-    if (all_f64) HIP_TRY(launch_all_f64_list(int(b->n), b->d_raw32, b->d_flag, b->d_list, count, s));
+    if (all_f64) HIP_TRY(launch_all_f64_list(int(b->n), b->d_raw32, b->d_flag, b->d_list, count, b->d_pairs, b->d_list + b->n, s));
     if (b->n_lane > 0 && !all_f64) {
         LaneArgs a{};
         a.pairs = b->d_pairs;
@@ -92,6 +93,7 @@ int run_part(Part* b, hipStream_t s)
         a.raw_out = b->d_raw32;
         a.rescue_flag = b->d_flag;
         a.rescue_list = b->d_list;
+        a.rescue_rh = b->d_list + b->n;   // (the list block holds 2n ints)
         a.rescue_count = count;
         a.raw64_zero = b->d_raw64;
         a.lut64 = dv.lut_d;
@@ -198,6 +200,7 @@ int run_part(Part* b, hipStream_t s)
         a.raw_out = b->d_raw32;
         a.rescue_flag = b->d_flag;
         a.rescue_list = b->d_list;
+        a.rescue_rh = b->d_list + b->n;   // (the list block holds 2n ints)
         a.rescue_count = count;
         a.raw64_zero = b->d_raw64;
         const int G = 64 / c.W;

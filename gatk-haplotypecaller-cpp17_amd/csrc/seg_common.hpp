@@ -527,7 +527,7 @@ __device__ __forceinline__ void rescue_one(const LaneArgs& a, const PairDesc pd,
 // Rescue pair rp (slot rs, hap length H) in this wave if it qualifies and the
 // run's in-wave budget allows (wave-uniform), else append it to the fp64
 // launch's list (lane `owner_lane`).
-__device__ __forceinline__ void rescue_or_defer(const LaneArgs& a, bool few, int rp, int rs, int H, int lane,
+__device__ __forceinline__ void rescue_or_defer(const LaneArgs& a, bool few, int rp, int rs, int H, int R, int lane,
                                                 int owner_lane, uint2* __restrict__ mt)
 {
     bool here = few && H <= kInWaveRescueMaxH;
@@ -538,12 +538,15 @@ __device__ __forceinline__ void rescue_or_defer(const LaneArgs& a, bool few, int
     }
     if (here)
         rescue_one(a, a.sdesc[rs], rp, rs, lane, mt);   // sdesc[rs] = pairs[rp]
-    else if (lane == owner_lane)
-        a.rescue_list[atomicAdd(a.rescue_count, 1)] = rp;
+    else if (lane == owner_lane) {
+        const int pos = atomicAdd(a.rescue_count, 1);
+        a.rescue_list[pos] = rp;
+        a.rescue_rh[pos] = pack_rh(R, H);
+    }
 }
 
-__device__ __forceinline__ void rescue_in_wave(const LaneArgs& a, uint64_t todo, int pid, int slot, int H, int lane,
-                                               uint2* __restrict__ mt)
+__device__ __forceinline__ void rescue_in_wave(const LaneArgs& a, uint64_t todo, int pid, int slot, int H, int R,
+                                               int lane, uint2* __restrict__ mt)
 {
     // (No fp64 launch after this pass: every one, the list would go unread.)
     const bool few = a.inker_count != nullptr && (a.solo_counters != nullptr || __popcll(todo) <= 2);
@@ -554,7 +557,7 @@ __device__ __forceinline__ void rescue_in_wave(const LaneArgs& a, uint64_t todo,
         const int l = __builtin_ctzll(todo);
         todo &= todo - 1;
         rescue_or_defer(a, few, __builtin_amdgcn_readlane(pid, l), __builtin_amdgcn_readlane(slot, l),
-                        __builtin_amdgcn_readlane(H, l), lane, l, mt);
+                        __builtin_amdgcn_readlane(H, l), __builtin_amdgcn_readlane(R, l), lane, l, mt);
     }
 }
 
