@@ -141,6 +141,8 @@ def lib():
     L.hc_phmm_batch_destroy.argtypes = [C.c_void_p]
     L.hc_phmm_get_luts.argtypes = [_f32p, _f64p, _f32p, _f64p]
     L.hcx_test_plan_timeout.argtypes = [C.c_int]   # test hook (tests only)
+    L.hcx_flat_nibble_parts.argtypes = [C.c_int]   # test hook (tests only)
+    L.hcx_flat_nibble_parts.restype = C.c_int
     _lib = L
     return L
 

@@ -289,4 +289,35 @@ def test_flat_compact_fallbacks(engine, oracle_lib, case):
         ins = b["ins"].copy()
         ins[ro[29] + 1] = ord("J")      # pair 29's gap qualities vary
         b = dict(b, ins=ins)
+    L = engine.lib()
+    L.hcx_flat_nibble_parts(0)   # (an earlier refusal would make this call skip the compact attempt)
     assert_same(engine.pairs(b), oracle_lib.pairs(b, nthreads=16), case)
+    refused = case != "many_n"   # the sample sees one of 300 'N' reads; the others slip past it
+    assert (L.hcx_flat_nibble_parts(-1) > 0) == refused, case
+    L.hcx_flat_nibble_parts(0)
+
+
+def test_flat_rare_n_after_refusal(engine, oracle_lib):
+    """Rare 'N's the part samples miss: the first call's refusal makes the
+    device's next parts start with the nibble records (Device::nibble_parts,
+    DESIGN.md §16.7): two calls, both against the oracle, the second planned
+    without the compact attempt; with the counter run out, a third call tries
+    the compact records again (and is refused again)."""
+    b = W.config("S2", 20000)
+    rs = b["rs"].copy()
+    ro = b["read_off"]
+    for p in (7, 4007, 12345):   # off every 1-in-19 sample
+        rs[ro[p] + 2] = ord("N")
+    b = dict(b, rs=rs)
+    ref = oracle_lib.pairs(b, nthreads=16)
+    L = engine.lib()
+    L.hcx_flat_nibble_parts(0)
+    assert_same(engine.pairs(b), ref, "first call (refused, planned again)")
+    left = L.hcx_flat_nibble_parts(-1)
+    assert 0 < left <= 64
+    assert_same(engine.pairs(b), ref, "second call (nibble records from the start)")
+    assert L.hcx_flat_nibble_parts(-1) < left
+    L.hcx_flat_nibble_parts(0)
+    assert_same(engine.pairs(b), ref, "third call (compact attempt again)")
+    assert L.hcx_flat_nibble_parts(-1) > 0
+    L.hcx_flat_nibble_parts(0)
